@@ -1,0 +1,132 @@
+/*
+ * thor_amd -- MI355X-native per-block reconstruction for the Thor video codec.
+ *
+ * Public C-ABI of libthor_amd.so (thor_amd/csrc).  Two surfaces:
+ *
+ *  1. The reference's SIMD kernel surface, same names and signatures, so the
+ *     reference Thorenc/Thordec host C links this library in place of
+ *     common/common_kernels.c and enc/enc_kernels.c (see thor_kernels.h).
+ *
+ *  2. A batched per-frame surface (this header): block-descriptor arrays in,
+ *     one launch per stage, frames resident in HBM.  This is what a restated
+ *     decode_frame (dec/decode_frame.c:45-148) calls; the per-block symbols
+ *     alone would be launch-latency bound.
+ *
+ * No torch types cross this boundary: plain pointers, sizes and int status
+ * codes (0 = ok, <0 = error; the reference has no error convention and aborts,
+ * common/global.h:38-44 -- this library never aborts).
+ */
+#ifndef THOR_AMD_H
+#define THOR_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define THOR_OK 0
+#define THOR_ERR_ARG (-1)
+#define THOR_ERR_HIP (-2)
+#define THOR_ERR_NOMEM (-3)
+#define THOR_ERR_REF (-4) /* a block names a reference frame that is not resident */
+
+/* ---- block descriptor ------------------------------------------------- *
+ * One decoded CU as the parser leaves it (dec/maindec.h:47-57, block_param_t
+ * common/types.h:153-170).  72 bytes, naturally aligned.                     */
+typedef struct thor_block {
+  uint16_t ypos, xpos;      /* luma position of the CU                        */
+  uint8_t size;             /* 8..64                                           */
+  uint8_t bwidth, bheight;  /* clipped to the frame (rectangular edge SKIP,
+                               dec/decode_block.c:222-226)                     */
+  uint8_t mode;             /* block_mode_t: 0 SKIP 1 INTRA 2 INTER 3 BIPRED 4 MERGE */
+  uint8_t intra_mode;       /* intra_mode_t (common/types.h:137-149)           */
+  uint8_t tb_split;         /* 4 transform blocks                              */
+  uint8_t pb_part;          /* part_t, deblocking only                         */
+  uint8_t dir;              /* 2 = bi-directional SKIP/MERGE                   */
+  uint8_t qp;               /* block qp (frame qp + delta qp)                  */
+  uint8_t cbp_y, cbp_u, cbp_v; /* cbp as stored in deblock_data             */
+  uint8_t coeff_mask;       /* bit c: component c (Y,U,V) has coefficients     */
+  uint8_t rsv[3];
+  int16_t mv0[8];           /* mv_arr0[4] as (x, y) pairs, quarter-pel luma    */
+  int16_t mv1[8];           /* mv_arr1[4]                                      */
+  int32_t ref0, ref1;       /* display frame_num of the reference (-1 none)    */
+  uint32_t coeff_off[3];    /* int16 offset of each component in the frame's
+                               compact coefficient pool                        */
+} thor_block_t;
+
+/* Compact coefficient pool: per component of a CU, one qsize x qsize int16
+ * tile per transform block (qsize = min(N,16): only the low-frequency corner
+ * can be non-zero, common/transform.c:309-327), tb-split quarters consecutive
+ * in raster order, row-major inside a tile. */
+
+/* ---- sequence / frame parameters -------------------------------------- */
+typedef struct thor_seq {
+  int32_t width, height;
+  int32_t bipred;      /* sequence-level enable_bipred: selects the luma MC table
+                          for every luma call (dec/maindec.c:147)            */
+  int32_t deblocking;  /* dec/maindec.c:144 */
+  int32_t clpf;        /* dec/maindec.c:145 */
+  int32_t tb_split_enable;
+} thor_seq_t;
+
+typedef struct thor_frame_hdr {
+  int32_t frame_num;   /* display frame number */
+  int32_t frame_type;  /* 0 I, 1 P, 2 B */
+  int32_t qp;          /* frame qp: drives deblocking (dec/decode_frame.c:124-128) */
+  int32_t clpf_on;     /* CLPF signalled on for this frame (dec/decode_frame.c:130) */
+} thor_frame_hdr_t;
+
+/* ---- batched decoder context ------------------------------------------ */
+typedef struct thor_dec thor_dec_t;
+
+/* Create a device-resident decoder: a ring of padded reference frames (pad 96
+ * luma / 48 chroma, stride as create_yuv_frame, common/common_frame.c:324-351)
+ * on HIP device `device`.  Returns NULL on failure. */
+thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots);
+void thor_dec_destroy(thor_dec_t *d);
+
+/* Decode (reconstruct) one frame.  `blocks`, `coeffs`, `clpf_flags` and
+ * `intra_list` are DEVICE pointers (inputs resident in HBM); `nblocks`
+ * descriptors in decode order.  `intra_list` holds the indices of the intra
+ * CUs in decode order (thor_build_intra_list), the only planning data the
+ * parser hands over besides the descriptors.  Enqueues every stage on the
+ * context's stream and returns without waiting: per-4x4 side info, inter MC +
+ * dequant + inverse transform + reconstruction, intra, deblock Y/UV, CLPF,
+ * padding.  The reconstructed frame becomes reference `frame_num`. */
+int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
+                   const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra);
+
+/* Host helper: write the decode-order indices of the intra CUs of a frame
+ * (host descriptors) to `out` (may be NULL to count); returns the count. */
+int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);
+
+/* Stage control for parity debugging: 0 recon only, 1 +deblock, 2 +CLPF (default 2). */
+int thor_dec_set_stop_stage(thor_dec_t *d, int stage);
+
+/* Copy frame `frame_num` (unpadded I420, tightly packed) to host memory. */
+int thor_dec_read_frame(thor_dec_t *d, int frame_num, uint8_t *y, uint8_t *u, uint8_t *v);
+/* Upload a frame (e.g. an externally decoded reference) into a slot. */
+int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const uint8_t *u, const uint8_t *v);
+int thor_dec_sync(thor_dec_t *d);
+
+/* The HIP stream the context enqueues on (hipStream_t as void*), so callers
+ * can record events / capture graphs around thor_dec_frame. */
+void *thor_dec_stream(thor_dec_t *d);
+/* Set the stream (e.g. torch's current stream); NULL = the context's own. */
+int thor_dec_set_stream(thor_dec_t *d, void *stream);
+
+/* ---- device memory helpers (so the C-ABI is usable without torch) ------ */
+void *thor_dev_alloc(size_t bytes);
+int thor_dev_free(void *p);
+int thor_h2d(void *dst, const void *src, size_t bytes);
+int thor_d2h(void *dst, const void *src, size_t bytes);
+int thor_device_count(void);
+const char *thor_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

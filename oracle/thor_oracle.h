@@ -1,0 +1,57 @@
+/*
+ * TEST INFRASTRUCTURE ONLY -- the checker, never the thing measured or shipped.
+ *
+ * Clean-room CPU restatement of the Thor per-block reconstruction hot path
+ * (SURVEY.md sec. 8(a)).  Every function cites the reference file:line whose
+ * behaviour it restates.  Parity of this restatement is pinned against the
+ * reference itself: kernel-level vectors generated from the reference build
+ * (tests/golden/ kernel vectors, tools/make_goldens.py) and per-stage frame digests of the
+ * reference decoder on committed streams (tests/golden/streams.json).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load liboracle.so.
+ */
+#ifndef THOR_ORACLE_H
+#define THOR_ORACLE_H
+#include <stdint.h>
+#include "../include/thor_amd.h"
+
+/* ---- block kernels ------------------------------------------------------ */
+void or_mc_luma(uint8_t *pblock, int pstride, const uint8_t *ref, int rstride, int width, int height, int mvx,
+                int mvy, int sign, int bipred);
+void or_mc_chroma(uint8_t *pblock, int pstride, const uint8_t *ref, int rstride, int width, int height, int mvx,
+                  int mvy, int sign);
+void or_dequantize(const int16_t *coeff, int16_t *rcoeff, int qp, int size);
+void or_inverse_transform(const int16_t *coeff, int16_t *block, int size);
+void or_transform(const int16_t *block, int16_t *coeff, int size, int fast);
+int or_quantize(const int16_t *coeff, int16_t *coeffq, int qp, int size, int coeff_block_type);
+void or_reconstruct_block(const int16_t *block, const uint8_t *pblock, uint8_t *rec, int size, int stride);
+void or_make_top_and_left(uint8_t *left, uint8_t *top, uint8_t *top_left, const uint8_t *rec_frame, int fstride,
+                          const uint8_t *rblock, int rbstride, int i, int j, int ypos, int xpos, int size,
+                          int upright_available, int downleft_available, int tb_split);
+void or_intra_pred(const uint8_t *left, const uint8_t *top, uint8_t top_left, int ypos, int xpos, int size,
+                   uint8_t *pblock, int mode);
+int or_upright_available(int ypos, int xpos, int size, int width);
+int or_downleft_available(int ypos, int xpos, int size, int height);
+void or_clpf_block(const uint8_t *src, uint8_t *dst, int sstride, int dstride, int x0, int y0, int size, int width,
+                   int height);
+uint32_t or_sad(const uint8_t *a, const uint8_t *b, int astride, int bstride, int width, int height);
+uint32_t or_ssd(const uint8_t *a, const uint8_t *b, int astride, int bstride, int width, int height);
+
+/* ---- frames ------------------------------------------------------------- */
+typedef struct or_frame {
+  uint8_t *y, *u, *v; /* interior (0,0) pointers of padded planes */
+  int stride_y, stride_c;
+  int frame_num;
+} or_frame_t;
+
+/* Restates decode_block (dec/decode_block.c:158-471) over a frame's
+ * descriptors, then deblock_frame_y/uv (common/common_frame.c:46-321) and
+ * clpf_frame (common/common_frame.c:485-557).  stop_stage: 0 recon only,
+ * 1 + deblock, 2 + CLPF.  Returns 0 or a negative error. */
+int or_decode_frame(const thor_seq_t *seq, const thor_frame_hdr_t *hdr, or_frame_t *cur, const or_frame_t *refs,
+                    int nrefs, const thor_block_t *blocks, int nblocks, const int16_t *coeffs,
+                    const uint8_t *clpf_flags, int stop_stage);
+/* pad_yuv_frame (common/common_frame.c:405-462), pad 96 luma / 48 chroma */
+void or_pad_frame(or_frame_t *f, int width, int height, int pad_y, int pad_c);
+#endif

@@ -1,0 +1,81 @@
+"""GPU parity: the batched HIP path (libthor_amd.so through its C-ABI) replays
+the committed reference traces and must reproduce the reference decoder's
+frames bit-exactly, stage by stage, and the CPU oracle on the same inputs."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import trace_path
+from thor_amd.trace import load_trace
+
+pytestmark = pytest.mark.gpu
+
+STREAMS = ["cif_low", "cif_med", "cif_high", "cif_hdb", "hd_low", "k4_low"]
+
+
+def _md5(b):
+    return hashlib.md5(b).hexdigest()
+
+
+@pytest.mark.parametrize("name", STREAMS)
+def test_gpu_decode_matches_reference(name, streams):
+    from thor_amd.decoder import GpuDecoder
+
+    meta = streams[name]
+    seq, frames = load_trace(trace_path(name))
+    dec = GpuDecoder(seq)
+    try:
+        devs = [dec.upload(fr) for fr in frames]
+        out = {}
+        for fr, d in zip(frames, devs):
+            dec.decode(d)
+            dec.sync()
+            got = dec.read_i420(fr.frame_num)
+            assert _md5(got) == meta["stage_md5"][fr.decode_order]["final"], (name, fr.decode_order)
+            out[fr.frame_num] = got
+        yuv = b"".join(out[k] for k in sorted(out))
+        assert _md5(yuv) == meta["dec_md5"]
+    finally:
+        dec.close()
+
+
+@pytest.mark.parametrize("name", ["cif_low", "cif_high", "cif_hdb", "cif_med"])
+def test_gpu_stages_match_reference(name, streams):
+    from thor_amd.decoder import GpuDecoder
+
+    meta = streams[name]
+    seq, frames = load_trace(trace_path(name))
+    dec = GpuDecoder(seq)
+    try:
+        for fr in frames:
+            d = dec.upload(fr)
+            for stage, key in ((0, "pre_deblock"), (1, "post_deblock"), (2, "final")):
+                dec.set_stop_stage(stage)
+                dec.decode(d)
+                dec.sync()
+                assert _md5(dec.read_i420(fr.frame_num)) == meta["stage_md5"][fr.decode_order][key], (
+                    name, fr.decode_order, key)
+    finally:
+        dec.close()
+
+
+def test_gpu_matches_oracle_pixelwise():
+    """Same inputs through the oracle and the GPU: report the first differing
+    pixel if any (diagnostic companion of the md5 checks)."""
+    from oracle import OracleDecoder
+    from thor_amd.decoder import GpuDecoder
+
+    seq, frames = load_trace(trace_path("cif_high"))
+    gdec = GpuDecoder(seq)
+    odec = OracleDecoder(seq)
+    try:
+        for fr, cur in odec.run(frames):
+            gdec.decode(gdec.upload(fr))
+            gy, gu, gv = gdec.read(fr.frame_num)
+            oy, ou, ov = cur.planes()
+            for nm, g, o in (("Y", gy, oy), ("U", gu, ov * 0 + ou), ("V", gv, ov)):
+                bad = np.argwhere(g != o)
+                assert bad.size == 0, (fr.decode_order, nm, bad[:5].tolist(), int(len(bad)))
+    finally:
+        gdec.close()

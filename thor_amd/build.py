@@ -1,0 +1,36 @@
+"""Build libthor_amd.so in-tree with hipcc for gfx950 (no JIT cache: the .so
+travels to the GPU box with the repository snapshot)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libthor_amd.so")
+SOURCES = ["libthor_amd.hip", "recon.hip", "loopfilter.hip", "capi.hip", "simd_surface.hip", "common.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+         "-Wall", "-Wno-unused-result", "-Wno-bitwise-instead-of-logical"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(HERE, "..", "include", "thor_amd.h"),
+                                                      os.path.join(HERE, "..", "include", "thor_kernels.h")]
+    return any(os.path.exists(p) and os.path.getmtime(p) > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if force or _stale():
+        cmd = [HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "libthor_amd.hip")]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True, cwd=CSRC)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force=True, verbose=True)

@@ -1,0 +1,317 @@
+// Host side of libthor_amd.so: the batched per-frame C-ABI (include/thor_amd.h).
+// Restates the frame-level control of dec/decode_frame.c:45-148 around the
+// GPU stages: a ring of padded reference slots standing in for the
+// decoder's sliding window (decode_frame.c:138-147, MAX_REF_FRAMES = 33,
+// common/global.h:69), then per frame: side-info -> inter -> intra ->
+// deblock -> CLPF -> pad, all enqueued on one HIP stream.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "common.h"
+
+// kernels (recon.hip, loopfilter.hip)
+__global__ void k_prep(const thor_block_t *, int, uint16_t *, int32_t *, int);
+__global__ void k_inter(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int, int);
+__global__ void k_intra(FrameCtx, const thor_block_t *, const int16_t *, const uint32_t *, int, unsigned *,
+                        unsigned *, const int32_t *, unsigned *);
+__global__ void k_deblock_luma_v(uint8_t *, int, int, int, const uint16_t *, int);
+__global__ void k_deblock_luma_h(uint8_t *, int, int, int, const uint16_t *, int);
+__global__ void k_deblock_chroma_v(uint8_t *, uint8_t *, int, int, int, const uint16_t *, int);
+__global__ void k_deblock_chroma_h(uint8_t *, uint8_t *, int, int, int, const uint16_t *, int);
+__global__ void k_clpf(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, const uint8_t *);
+__global__ void k_pad(uint8_t *, uint8_t *, uint8_t *, int, int, int, int);
+
+#define HIPCHK(x)                                                                               \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      fprintf(stderr, "thor_amd: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+              __LINE__);                                                                        \
+      return THOR_ERR_HIP;                                                                      \
+    }                                                                                           \
+  } while (0)
+
+static int chroma_qp_host(int q) {
+  static const int t[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+                            18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33,
+                            34, 34, 35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45};
+  return t[q < 0 ? 0 : (q > 51 ? 51 : q)];
+}
+
+struct thor_dec {
+  thor_seq_t seq;
+  int device;
+  hipStream_t own_stream, stream;
+  int sy, sc;
+  long long offy, offu, offv, slot_bytes;
+  int nslots;
+  uint8_t *slots;
+  std::vector<int> slot_fnum;   // -1 = empty
+  std::vector<long long> slot_age;
+  long long decode_count;
+  uint16_t *cellinfo;
+  int32_t *cellmap;
+  unsigned *ctl;       // [0] intra head, [1] timeout flag, [2..3] pad; then done flags
+  size_t done_cap;
+  unsigned *done;
+  int stop_stage;
+};
+
+extern "C" {
+
+const char *thor_version(void) { return "thor_amd 0.1 (gfx950)"; }
+
+int thor_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void *thor_dev_alloc(size_t bytes) {
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  return p;
+}
+int thor_dev_free(void *p) {
+  HIPCHK(hipFree(p));
+  return THOR_OK;
+}
+int thor_h2d(void *dst, const void *src, size_t bytes) {
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return THOR_OK;
+}
+int thor_d2h(void *dst, const void *src, size_t bytes) {
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return THOR_OK;
+}
+
+thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
+  if (!seq || seq->width <= 0 || seq->height <= 0 || (seq->width & 15) || (seq->height & 7)) return nullptr;
+  if (num_slots <= 1) num_slots = 34;  // 33 references + the frame being decoded
+  if (num_slots > THOR_MAX_SLOTS) num_slots = THOR_MAX_SLOTS;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  thor_dec *d = new thor_dec();
+  d->seq = *seq;
+  d->device = device;
+  int W = seq->width, H = seq->height;
+  d->sy = (W + 2 * THOR_PAD_Y + 15) & ~15;       // common/common_frame.c:331
+  d->sc = (W / 2 + 2 * THOR_PAD_C + 15) & ~15;   // :332
+  long long ybytes = (long long)(H + 2 * THOR_PAD_Y) * d->sy;
+  long long cbytes = (long long)(H / 2 + 2 * THOR_PAD_C) * d->sc;
+  ybytes = (ybytes + 255) & ~255LL;
+  cbytes = (cbytes + 255) & ~255LL;
+  d->offy = (long long)THOR_PAD_Y * d->sy + THOR_PAD_Y;
+  d->offu = ybytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
+  d->offv = ybytes + cbytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
+  d->slot_bytes = ybytes + 2 * cbytes + 256;
+  d->nslots = num_slots;
+  d->slot_fnum.assign(num_slots, -1);
+  d->slot_age.assign(num_slots, -1);
+  d->decode_count = 0;
+  d->stop_stage = 2;
+  d->done_cap = 0;
+  d->done = nullptr;
+  bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
+  d->stream = d->own_stream;
+  ok = ok && hipMalloc(&d->slots, d->slot_bytes * num_slots) == hipSuccess;
+  ok = ok && hipMemset(d->slots, 0, d->slot_bytes * num_slots) == hipSuccess;
+  size_t ncell = (size_t)(W / 4) * (H / 4);
+  ok = ok && hipMalloc(&d->cellinfo, ncell * sizeof(uint16_t)) == hipSuccess;
+  ok = ok && hipMalloc(&d->cellmap, ncell * sizeof(int32_t)) == hipSuccess;
+  ok = ok && hipMemset(d->cellmap, 0, ncell * sizeof(int32_t)) == hipSuccess;
+  ok = ok && hipMemset(d->cellinfo, 0, ncell * sizeof(uint16_t)) == hipSuccess;
+  ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
+  ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
+  if (!ok) {
+    thor_dec_destroy(d);
+    return nullptr;
+  }
+  return d;
+}
+
+void thor_dec_destroy(thor_dec_t *d) {
+  if (!d) return;
+  hipSetDevice(d->device);
+  if (d->own_stream) hipStreamSynchronize(d->own_stream);
+  if (d->slots) hipFree(d->slots);
+  if (d->cellinfo) hipFree(d->cellinfo);
+  if (d->cellmap) hipFree(d->cellmap);
+  if (d->ctl) hipFree(d->ctl);
+  if (d->done) hipFree(d->done);
+  if (d->own_stream) hipStreamDestroy(d->own_stream);
+  delete d;
+}
+
+void *thor_dec_stream(thor_dec_t *d) { return d ? (void *)d->stream : nullptr; }
+int thor_dec_set_stream(thor_dec_t *d, void *stream) {
+  if (!d) return THOR_ERR_ARG;
+  d->stream = stream ? (hipStream_t)stream : d->own_stream;
+  return THOR_OK;
+}
+int thor_dec_set_stop_stage(thor_dec_t *d, int stage) {
+  if (!d || stage < 0 || stage > 2) return THOR_ERR_ARG;
+  d->stop_stage = stage;
+  return THOR_OK;
+}
+int thor_dec_sync(thor_dec_t *d) {
+  if (!d) return THOR_ERR_ARG;
+  HIPCHK(hipStreamSynchronize(d->stream));
+  unsigned to = 0;
+  HIPCHK(hipMemcpy(&to, d->ctl + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (to) {
+    fprintf(stderr, "thor_amd: intra dependency wait timed out\n");
+    return THOR_ERR_HIP;
+  }
+  return THOR_OK;
+}
+
+static int find_slot_host(const thor_dec *d, int fnum) {
+  for (int s = 0; s < d->nslots; s++)
+    if (d->slot_fnum[s] == fnum) return s;
+  return -1;
+}
+
+// Slot for the frame about to be decoded: a free slot, else the one decoded
+// longest ago (sliding window: the reference shifted out, decode_frame.c:138-147).
+static int pick_slot(const thor_dec *d, int frame_num) {
+  for (int s = 0; s < d->nslots; s++)  // re-decoding a frame reuses its slot
+    if (d->slot_fnum[s] == frame_num) return s;
+  int best = 0;
+  for (int s = 0; s < d->nslots; s++) {
+    if (d->slot_fnum[s] < 0) return s;
+    if (d->slot_age[s] < d->slot_age[best]) best = s;
+  }
+  return best;
+}
+
+static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
+  FrameCtx f;
+  memset(&f, 0, sizeof(f));
+  uint8_t *cur = d->slots + (long long)cur_slot * d->slot_bytes;
+  f.cy = cur + d->offy;
+  f.cu = cur + d->offu;
+  f.cv = cur + d->offv;
+  f.slots = d->slots;
+  f.slot_bytes = d->slot_bytes;
+  f.offy = d->offy;
+  f.offu = d->offu;
+  f.offv = d->offv;
+  f.sy = d->sy;
+  f.sc = d->sc;
+  f.W = d->seq.width;
+  f.H = d->seq.height;
+  f.frame_num = frame_num;
+  f.bipred = d->seq.bipred;
+  f.nref = 0;
+  for (int s = 0; s < d->nslots; s++) {
+    if (s == cur_slot || d->slot_fnum[s] < 0) continue;
+    f.ref_fnum[f.nref] = d->slot_fnum[s];
+    f.ref_slot[f.nref] = s;
+    f.nref++;
+  }
+  return f;
+}
+
+int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
+                   const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra) {
+  if (!d || !hdr || nblocks < 0 || (nblocks > 0 && !blocks)) return THOR_ERR_ARG;
+  if (n_intra > 0 && !intra_list) return THOR_ERR_ARG;
+  HIPCHK(hipSetDevice(d->device));
+  int W = d->seq.width, H = d->seq.height;
+  int cur = pick_slot(d, hdr->frame_num);
+  FrameCtx f = make_ctx(d, cur, hdr->frame_num);
+  int cs = W / 4;
+  hipStream_t st = d->stream;
+  if (nblocks > 0) {
+    k_prep<<<(nblocks + 3) / 4, 256, 0, st>>>(blocks, nblocks, d->cellinfo, d->cellmap, cs);
+    HIPCHK(hipGetLastError());
+    int tiles_w = W / 16, tiles_h = (H + 15) / 16;
+    int ntiles = tiles_w * tiles_h;
+    k_inter<<<(ntiles + 3) / 4, 256, 0, st>>>(f, blocks, coeffs, d->cellmap, tiles_w, ntiles);
+    HIPCHK(hipGetLastError());
+  }
+  if (n_intra > 0) {
+    if ((size_t)nblocks > d->done_cap) {
+      if (d->done) HIPCHK(hipFree(d->done));
+      d->done_cap = (size_t)nblocks + 1024;
+      HIPCHK(hipMalloc(&d->done, d->done_cap * sizeof(unsigned)));
+    }
+    HIPCHK(hipMemsetAsync(d->done, 0, (size_t)nblocks * sizeof(unsigned), st));
+    HIPCHK(hipMemsetAsync(d->ctl, 0, sizeof(unsigned), st));
+    int grid = n_intra < 1024 ? n_intra : 1024;
+    k_intra<<<grid, 256, 0, st>>>(f, blocks, coeffs, intra_list, n_intra, d->ctl, d->done, d->cellmap, d->ctl + 1);
+    HIPCHK(hipGetLastError());
+  }
+  if (d->stop_stage >= 1 && d->seq.deblocking) {
+    int nv = ((W >> 3) - 1) * (H >> 3);
+    int nh = (W >> 3) * ((H >> 3) - 1);
+    k_deblock_luma_v<<<(nv + 255) / 256, 256, 0, st>>>(f.cy, d->sy, W, H, d->cellinfo, hdr->qp);
+    k_deblock_luma_h<<<(nh + 255) / 256, 256, 0, st>>>(f.cy, d->sy, W, H, d->cellinfo, hdr->qp);
+    int qpc = chroma_qp_host(hdr->qp);
+    k_deblock_chroma_v<<<dim3((nv + 255) / 256, 2), 256, 0, st>>>(f.cu, f.cv, d->sc, W, H, d->cellinfo, qpc);
+    k_deblock_chroma_h<<<dim3((nh + 255) / 256, 2), 256, 0, st>>>(f.cu, f.cv, d->sc, W, H, d->cellinfo, qpc);
+    HIPCHK(hipGetLastError());
+  }
+  if (d->stop_stage >= 2 && d->seq.clpf && hdr->clpf_on && clpf_flags) {
+    int nsb = (W / 64) * (H / 64);
+    if (nsb > 0) {
+      k_clpf<<<nsb, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, clpf_flags);
+      HIPCHK(hipGetLastError());
+    }
+  }
+  k_pad<<<dim3(H + 2 * THOR_PAD_Y, 3), 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H);
+  HIPCHK(hipGetLastError());
+  d->slot_fnum[cur] = hdr->frame_num;
+  d->slot_age[cur] = d->decode_count++;
+  return THOR_OK;
+}
+
+int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out) {
+  if (nblocks < 0 || (nblocks > 0 && !host_blocks)) return THOR_ERR_ARG;
+  int n = 0;
+  for (int b = 0; b < nblocks; b++)
+    if (host_blocks[b].mode == M_INTRA) {
+      if (out) out[n] = (uint32_t)b;
+      n++;
+    }
+  return n;
+}
+
+int thor_dec_read_frame(thor_dec_t *d, int frame_num, uint8_t *y, uint8_t *u, uint8_t *v) {
+  if (!d) return THOR_ERR_ARG;
+  int s = find_slot_host(d, frame_num);
+  if (s < 0) return THOR_ERR_REF;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  int W = d->seq.width, H = d->seq.height;
+  const uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  if (y) HIPCHK(hipMemcpy2D(y, W, base + d->offy, d->sy, W, H, hipMemcpyDeviceToHost));
+  if (u) HIPCHK(hipMemcpy2D(u, W / 2, base + d->offu, d->sc, W / 2, H / 2, hipMemcpyDeviceToHost));
+  if (v) HIPCHK(hipMemcpy2D(v, W / 2, base + d->offv, d->sc, W / 2, H / 2, hipMemcpyDeviceToHost));
+  return THOR_OK;
+}
+
+int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const uint8_t *u, const uint8_t *v) {
+  if (!d || !y || !u || !v) return THOR_ERR_ARG;
+  HIPCHK(hipSetDevice(d->device));
+  int s = find_slot_host(d, frame_num);
+  if (s < 0) s = pick_slot(d, frame_num);
+  int W = d->seq.width, H = d->seq.height;
+  uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  HIPCHK(hipMemcpy2D(base + d->offy, d->sy, y, W, W, H, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy2D(base + d->offu, d->sc, u, W / 2, W / 2, H / 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy2D(base + d->offv, d->sc, v, W / 2, W / 2, H / 2, hipMemcpyHostToDevice));
+  k_pad<<<dim3(H + 2 * THOR_PAD_Y, 3), 256, 0, d->stream>>>(base + d->offy, base + d->offu, base + d->offv, d->sy,
+                                                            d->sc, W, H);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(d->stream));
+  d->slot_fnum[s] = frame_num;
+  d->slot_age[s] = d->decode_count++;
+  return THOR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// Shared device-side definitions for the thor_amd HIP kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/thor_amd.h"
+
+#define THOR_MAX_SLOTS 40
+#define THOR_PAD_Y 96
+#define THOR_PAD_C 48
+
+// block_mode_t, common/types.h:83-90
+enum { M_SKIP = 0, M_INTRA = 1, M_INTER = 2, M_BIPRED = 3, M_MERGE = 4 };
+
+// Everything a per-frame kernel needs to address the current frame and the
+// resident references.  Passed by value (kernel argument segment).
+struct FrameCtx {
+  uint8_t *cy, *cu, *cv;  // current frame, interior (0,0)
+  const uint8_t *slots;   // base of the reference ring
+  long long slot_bytes;   // bytes per slot
+  long long offy, offu, offv;  // interior (0,0) offsets inside a slot
+  int sy, sc;             // luma / chroma stride (create_yuv_frame, common/common_frame.c:331-332)
+  int W, H;
+  int frame_num;
+  int bipred;             // sequence-level luma filter table select (dec/maindec.c:147)
+  int nref;
+  int ref_fnum[THOR_MAX_SLOTS];
+  int ref_slot[THOR_MAX_SLOTS];
+};
+
+// Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits
+// (replaces the 44-byte deblock_data_t, common/types.h:127-135):
+//   [2:0] mode  [3] cbp.y  [4] cbp.u  [5] cbp.v  [6] |mv| >= 4 (NEW_MV_TEST,
+//   common/common_frame.c:101-102)  [10:8] log2 q_size for vertical edges
+//   [13:11] log2 q_size for horizontal edges  [15:14] log2(size) - 3
+#define CI_MODE(c) ((c)&7)
+#define CI_CBPY(c) (((c) >> 3) & 1)
+#define CI_CBPU(c) (((c) >> 4) & 1)
+#define CI_CBPV(c) (((c) >> 5) & 1)
+#define CI_MVBIG(c) (((c) >> 6) & 1)
+#define CI_LQV(c) (((c) >> 8) & 7)
+#define CI_LQH(c) (((c) >> 11) & 7)
+#define CI_LSZ(c) ((((c) >> 14) & 3) + 3)
+
+__device__ __forceinline__ int clip255(int x) { return x < 0 ? 0 : (x > 255 ? 255 : x); }
+__device__ __forceinline__ int clip16(int x) { return x < -32768 ? -32768 : (x > 32767 ? 32767 : x); }
+__device__ __forceinline__ int wrap16(int x) { return (int)(int16_t)(uint16_t)(x & 0xffff); }
+__device__ __forceinline__ int ilog2i(int x) { return 31 - __clz(x); }
+
+// Ordering of LDS traffic inside one wavefront (no workgroup barrier needed:
+// each wave owns its LDS slice).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// HEVC integer DCT basis used by Thor (g*mat_hevc, common/transform.c:41-245):
+// row k of the N-point matrix is row k*32/N of the 32-point one.
+__device__ __forceinline__ int dct32_entry(int k, int n) {
+  const int c[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                     61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+  if (k == 0) return 64;
+  int t = (k * (2 * n + 1)) & 127;
+  if (t <= 32) return c[t];
+  if (t <= 64) return -c[64 - t];
+  if (t <= 96) return -c[t - 64];
+  return c[128 - t];
+}
+
+__device__ __forceinline__ const uint8_t *slot_plane(const FrameCtx &f, int slot, int comp) {
+  const uint8_t *s = f.slots + (long long)slot * f.slot_bytes;
+  return s + (comp == 0 ? f.offy : (comp == 1 ? f.offu : f.offv));
+}
+
+// Reference lookup by display frame number; -1 if not resident.
+__device__ __forceinline__ int find_slot(const FrameCtx &f, int fnum) {
+  for (int r = 0; r < f.nref; r++)
+    if (f.ref_fnum[r] == fnum) return f.ref_slot[r];
+  return -1;
+}
+
+// gdequant_table, common/common_block.c:98
+__device__ __forceinline__ int dequant_scale(int r) {
+  return r == 0 ? 40 : r == 1 ? 45 : r == 2 ? 51 : r == 3 ? 57 : r == 4 ? 64 : 72;
+}
+// chroma_qp, common/common_block.c:78-83
+__device__ __forceinline__ int chroma_qp(int q) {
+  if (q < 30) return q;
+  const int t[22] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45};
+  return t[q - 30];
+}

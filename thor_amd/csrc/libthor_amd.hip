@@ -1,0 +1,4 @@
+// Single translation unit for libthor_amd.so (no relocatable device code).
+#include "recon.hip"
+#include "loopfilter.hip"
+#include "capi.hip"

@@ -1,0 +1,270 @@
+// In-loop filters and reference padding for gfx950: deblock_frame_y/uv
+// (common/common_frame.c:46-321), clpf_frame (:485-557), pad_yuv_frame
+// (:405-462).  All in place on the current slot.
+#include "common.h"
+
+// beta_table / tc_table, common/common_frame.c:36-44
+__device__ __forceinline__ int beta_of(int qp) {
+  const int t[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                     8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                     34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+  return t[qp];
+}
+__device__ __forceinline__ int tc_of(int qp) {
+  const int t[56] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,  1,  1,  1,  1,  1,  1,  1,  1, 2,
+                     2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14};
+  return t[qp];
+}
+
+// Luma edge decision for one 4-pixel segment (common/common_frame.c:80-115,
+// NEW_DEBLOCK_TEST / NEW_MV_TEST): pos = j (vertical) or i (horizontal).
+__device__ __forceinline__ bool luma_edge_on(uint16_t P, uint16_t Q, int pos, bool vertical) {
+  int lq = vertical ? CI_LQV(Q) : CI_LQH(Q);
+  bool interior = (pos & ((1 << lq) - 1)) != 0;
+  bool mv = CI_MVBIG(P) | CI_MVBIG(Q);
+  bool cbp = CI_CBPY(P) | CI_CBPY(Q);
+  bool intra = CI_MODE(P) == 1 || CI_MODE(Q) == 1;
+  return !interior && (mv || cbp || intra);
+}
+
+__device__ __forceinline__ void filt4(int &p1, int &p0, int &q0, int &q1, int tc) {
+  // NEW_DEBLOCK_FILTER (common/common_frame.c:133-147); delta/2 truncates toward 0
+  int delta = (18 * (q0 - p0) - 6 * (q1 - p1) + 16) >> 5;
+  delta = delta < -tc ? -tc : (delta > tc ? tc : delta);
+  int h = delta / 2;
+  int np1 = clip255(p1 + h), np0 = clip255(p0 + delta), nq0 = clip255(q0 - delta), nq1 = clip255(q1 - h);
+  p1 = np1; p0 = np0; q0 = nq0; q1 = nq1;
+}
+
+// Vertical luma edges: one thread per (edge column j = 8e, 8-row group).
+__global__ __launch_bounds__(256) void k_deblock_luma_v(uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
+                                                        int qp) {
+  int ne = (W >> 3) - 1;
+  int t = blockIdx.x * 256 + threadIdx.x;
+  int g = t / ne, e = t - g * ne + 1;
+  if (g >= (H >> 3)) return;
+  int i = g * 8, j = e * 8;
+  int beta = beta_of(qp), tc = tc_of(qp);
+  uint8_t *base = Y + (long long)i * sy + j - 4;
+  uint32_t A[8], Bv[8];
+  for (int r = 0; r < 8; r++) {
+    A[r] = *(uint32_t *)(base + (long long)r * sy);
+    Bv[r] = *(uint32_t *)(base + (long long)r * sy + 4);
+  }
+  // p1 = A byte2, p0 = A byte3, q0 = B byte0, q1 = B byte1
+#define P1(r) ((int)((A[r] >> 16) & 255))
+#define P0(r) ((int)(A[r] >> 24))
+#define Q0(r) ((int)(Bv[r] & 255))
+#define Q1(r) ((int)((Bv[r] >> 8) & 255))
+  int d = abs(P1(2) - P0(2)) + abs(Q1(2) - Q0(2)) + abs(P1(5) - P0(5)) + abs(Q1(5) - Q0(5));
+  if (d >= beta) return;
+  int cs = W >> 2;
+  bool any = false;
+  for (int m = 0; m < 8; m += 4) {
+    int qi = ((i + m) >> 2) * cs + (j >> 2);
+    if (!luma_edge_on(cell[qi - 1], cell[qi], j, true)) continue;
+    any = true;
+    for (int r = m; r < m + 4; r++) {
+      int p1 = P1(r), p0 = P0(r), q0 = Q0(r), q1 = Q1(r);
+      filt4(p1, p0, q0, q1, tc);
+      A[r] = (A[r] & 0xffffu) | ((uint32_t)p1 << 16) | ((uint32_t)p0 << 24);
+      Bv[r] = (Bv[r] & 0xffff0000u) | (uint32_t)q0 | ((uint32_t)q1 << 8);
+    }
+  }
+#undef P1
+#undef P0
+#undef Q0
+#undef Q1
+  if (!any) return;
+  for (int r = 0; r < 8; r++) {
+    *(uint32_t *)(base + (long long)r * sy) = A[r];
+    *(uint32_t *)(base + (long long)r * sy + 4) = Bv[r];
+  }
+}
+
+// Horizontal luma edges: one thread per (edge row i = 8k >= 8, 8-column group).
+__global__ __launch_bounds__(256) void k_deblock_luma_h(uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
+                                                        int qp) {
+  int ng = W >> 3;
+  int t = blockIdx.x * 256 + threadIdx.x;
+  int k = t / ng, gcol = t - k * ng;
+  int i = (k + 1) * 8, j = gcol * 8;
+  if (i >= H) return;
+  int beta = beta_of(qp), tc = tc_of(qp);
+  uint8_t *base = Y + (long long)(i - 2) * sy + j;
+  uint2 rows[4];  // rows i-2 .. i+1 (p1, p0, q0, q1)
+  for (int r = 0; r < 4; r++) rows[r] = *(uint2 *)(base + (long long)r * sy);
+  auto px = [&](int r, int c) -> int { return (int)(((c < 4 ? rows[r].x : rows[r].y) >> (8 * (c & 3))) & 255); };
+  int d = abs(px(0, 2) - px(1, 2)) + abs(px(3, 2) - px(2, 2)) + abs(px(0, 5) - px(1, 5)) + abs(px(3, 5) - px(2, 5));
+  if (d >= beta) return;
+  int cs = W >> 2;
+  bool any = false;
+  uint32_t out[4][2] = {{rows[0].x, rows[0].y}, {rows[1].x, rows[1].y}, {rows[2].x, rows[2].y}, {rows[3].x, rows[3].y}};
+  for (int n = 0; n < 8; n += 4) {
+    int qi = (i >> 2) * cs + ((j + n) >> 2);
+    if (!luma_edge_on(cell[qi - cs], cell[qi], i, false)) continue;
+    any = true;
+    int w = n >> 2;
+    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+    for (int c = 0; c < 4; c++) {
+      int p1 = px(0, n + c), p0 = px(1, n + c), q0 = px(2, n + c), q1 = px(3, n + c);
+      filt4(p1, p0, q0, q1, tc);
+      o0 |= (uint32_t)p1 << (8 * c);
+      o1 |= (uint32_t)p0 << (8 * c);
+      o2 |= (uint32_t)q0 << (8 * c);
+      o3 |= (uint32_t)q1 << (8 * c);
+    }
+    out[0][w] = o0; out[1][w] = o1; out[2][w] = o2; out[3][w] = o3;
+  }
+  if (!any) return;
+  for (int r = 0; r < 4; r++) *(uint2 *)(base + (long long)r * sy) = make_uint2(out[r][0], out[r][1]);
+}
+
+// Chroma (deblock_frame_uv): intra-only edges, p0/q0 modified.  One thread
+// per (edge, 8-luma-row/column group) per plane (blockIdx.y = plane).
+__global__ __launch_bounds__(256) void k_deblock_chroma_v(uint8_t *U, uint8_t *V, int sc, int W, int H,
+                                                          const uint16_t *cell, int qpc) {
+  uint8_t *C = blockIdx.y ? V : U;
+  int ne = (W >> 3) - 1;
+  int t = blockIdx.x * 256 + threadIdx.x;
+  int g = t / ne, e = t - g * ne + 1;
+  if (g >= (H >> 3)) return;
+  int i = g * 8, j = e * 8;
+  int cs = W >> 2;
+  int qi = (i >> 2) * cs + (j >> 2);
+  uint16_t P = cell[qi - 1], Q = cell[qi];
+  bool intra = CI_MODE(P) == 1 || CI_MODE(Q) == 1;
+  bool interior = (j & ((1 << CI_LSZ(Q)) - 1)) != 0;
+  if (!intra || interior) return;
+  int tc = tc_of(qpc);
+  int i2 = i >> 1, j2 = j >> 1;
+  for (int k = 0; k < 4; k++) {
+    uint8_t *p = C + (long long)(i2 + k) * sc + j2;
+    int p1 = p[-2], p0 = p[-1], q0 = p[0], q1 = p[1];
+    int delta = (4 * (q0 - p0) + (p1 - q1) + 4) >> 3;
+    delta = delta < -tc ? -tc : (delta > tc ? tc : delta);
+    p[-1] = (uint8_t)clip255(p0 + delta);
+    p[0] = (uint8_t)clip255(q0 - delta);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_deblock_chroma_h(uint8_t *U, uint8_t *V, int sc, int W, int H,
+                                                          const uint16_t *cell, int qpc) {
+  uint8_t *C = blockIdx.y ? V : U;
+  int ng = W >> 3;
+  int t = blockIdx.x * 256 + threadIdx.x;
+  int k = t / ng, gcol = t - k * ng;
+  int i = (k + 1) * 8, j = gcol * 8;
+  if (i >= H) return;
+  int cs = W >> 2;
+  int qi = (i >> 2) * cs + (j >> 2);
+  uint16_t P = cell[qi - cs], Q = cell[qi];
+  bool intra = CI_MODE(P) == 1 || CI_MODE(Q) == 1;
+  bool interior = (i & ((1 << CI_LSZ(Q)) - 1)) != 0;
+  if (!intra || interior) return;
+  int tc = tc_of(qpc);
+  int i2 = i >> 1, j2 = j >> 1;
+  for (int l = 0; l < 4; l++) {
+    uint8_t *p = C + (long long)i2 * sc + j2 + l;
+    int p1 = p[-2 * sc], p0 = p[-sc], q0 = p[0], q1 = p[sc];
+    int delta = (4 * (q0 - p0) + (p1 - q1) + 4) >> 3;
+    delta = delta < -tc ? -tc : (delta > tc ? tc : delta);
+    p[-sc] = (uint8_t)clip255(p0 + delta);
+    p[0] = (uint8_t)clip255(q0 - delta);
+  }
+}
+
+// CLPF, one workgroup per whole 64x64 SB (the SB count is floor'd,
+// common/common_frame.c:496-497).  The SB is filtered when some 8x8 block is
+// a candidate (not BIPRED, any cbp) and the stream's decision flag is set.
+// Every 8x8 block that is not BIPRED is filtered per plane with coded
+// residual (clpf_block, common/common_block.c:180-197), reading the
+// unfiltered SB (LDS copy) with clamping at the SB border.
+__global__ __launch_bounds__(256) void k_clpf(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
+                                              const uint16_t *cell, const uint8_t *flags) {
+  __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];
+  __shared__ int cand;
+  int nh = W >> 6;
+  int k = blockIdx.x / nh, l = blockIdx.x - (blockIdx.x / nh) * nh;
+  if (!flags[blockIdx.x]) return;
+  int tid = threadIdx.x;
+  int cs = W >> 2;
+  if (tid == 0) cand = 0;
+  __syncthreads();
+  if (tid < 64) {
+    int m = tid >> 3, n = tid & 7;
+    uint16_t c = cell[((k * 64 + m * 8) >> 2) * cs + ((l * 64 + n * 8) >> 2)];
+    if (CI_MODE(c) != 3 && (CI_CBPY(c) | CI_CBPU(c) | CI_CBPV(c))) atomicOr(&cand, 1);
+  }
+  __syncthreads();
+  if (!cand) return;
+  uint8_t *y0 = Y + (long long)(k * 64) * sy + l * 64;
+  uint8_t *u0 = U + (long long)(k * 32) * sc + l * 32;
+  uint8_t *v0 = V + (long long)(k * 32) * sc + l * 32;
+  for (int p = tid; p < 64 * 16; p += 256) {
+    int r = p >> 4, c4 = (p & 15) * 4;
+    *(uint32_t *)&sY[r * 64 + c4] = *(uint32_t *)(y0 + (long long)r * sy + c4);
+  }
+  for (int p = tid; p < 32 * 8; p += 256) {
+    int r = p >> 3, c4 = (p & 7) * 4;
+    *(uint32_t *)&sU[r * 32 + c4] = *(uint32_t *)(u0 + (long long)r * sc + c4);
+    *(uint32_t *)&sV[r * 32 + c4] = *(uint32_t *)(v0 + (long long)r * sc + c4);
+  }
+  __syncthreads();
+  // luma: 4096 px, 16 per thread
+  for (int p = tid; p < 4096; p += 256) {
+    int r = p >> 6, c = p & 63;
+    uint16_t ci = cell[((k * 64 + (r & ~7)) >> 2) * cs + ((l * 64 + (c & ~7)) >> 2)];
+    if (CI_MODE(ci) == 3 || !CI_CBPY(ci)) continue;
+    int X = sY[r * 64 + c];
+    int A = r == 0 ? X : sY[(r - 1) * 64 + c];
+    int Bv = c == 0 ? X : sY[r * 64 + c - 1];
+    int Cv = c == 63 ? X : sY[r * 64 + c + 1];
+    int D = r == 63 ? X : sY[(r + 1) * 64 + c];
+    int delta = ((A > X) + (Bv > X) + (Cv > X) + (D > X) > 2) - ((A < X) + (Bv < X) + (Cv < X) + (D < X) > 2);
+    y0[(long long)r * sy + c] = (uint8_t)(X + delta);
+  }
+  for (int p = tid; p < 2048; p += 256) {
+    int pl = p >> 10, q = p & 1023;
+    int r = q >> 5, c = q & 31;
+    const uint8_t *s = pl ? sV : sU;
+    uint16_t ci = cell[((k * 64 + 2 * (r & ~3)) >> 2) * cs + ((l * 64 + 2 * (c & ~3)) >> 2)];
+    if (CI_MODE(ci) == 3 || !(pl ? CI_CBPV(ci) : CI_CBPU(ci))) continue;
+    int X = s[r * 32 + c];
+    int A = r == 0 ? X : s[(r - 1) * 32 + c];
+    int Bv = c == 0 ? X : s[r * 32 + c - 1];
+    int Cv = c == 31 ? X : s[r * 32 + c + 1];
+    int D = r == 31 ? X : s[(r + 1) * 32 + c];
+    int delta = ((A > X) + (Bv > X) + (Cv > X) + (D > X) > 2) - ((A < X) + (Bv < X) + (Cv < X) + (D < X) > 2);
+    (pl ? v0 : u0)[(long long)r * sc + c] = (uint8_t)(X + delta);
+  }
+}
+
+// pad_yuv_frame (common/common_frame.c:405-462): every padding byte equals
+// the nearest interior pixel (rows clamp, then columns clamp).  One workgroup
+// per padded row of one plane; blockIdx.y = plane.
+__global__ __launch_bounds__(256) void k_pad(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H) {
+  int plane = blockIdx.y;
+  uint8_t *P = plane == 0 ? Y : (plane == 1 ? U : V);
+  int s = plane ? sc : sy;
+  int w = plane ? W >> 1 : W, h = plane ? H >> 1 : H;
+  int pad = plane ? THOR_PAD_C : THOR_PAD_Y;
+  int row = (int)blockIdx.x - pad;
+  if (row >= h + pad) return;
+  int src_row = row < 0 ? 0 : (row >= h ? h - 1 : row);
+  const uint8_t *src = P + (long long)src_row * s;
+  uint8_t *dst = P + (long long)row * s;
+  if (row >= 0 && row < h) {
+    int t = threadIdx.x;
+    if (t < pad) dst[-pad + t] = src[0];
+    else if (t < 2 * pad) dst[w + t - pad] = src[w - 1];
+  } else {
+    // full padded row: w + 2*pad bytes (multiple of 16 for our strides)
+    int total = w + 2 * pad;
+    for (int c = threadIdx.x; c < total; c += 256) {
+      int sc_ = c - pad;
+      sc_ = sc_ < 0 ? 0 : (sc_ >= w ? w - 1 : sc_);
+      dst[c - pad] = src[sc_];
+    }
+  }
+}

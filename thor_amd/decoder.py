@@ -1,0 +1,131 @@
+"""Batched GPU decode driver: the restated frame loop of the reference decoder
+(dec/maindec.c:167-186 -> dec/decode_frame.c:45-148) over parse-side
+descriptors, with every reconstruction stage on the GPU through the C-ABI.
+
+Typical use (a trace stands in for the serial CPU parser):
+
+    seq, frames = trace.load_trace("stream.trc.z")
+    dec = GpuDecoder(seq)
+    dev = [dec.upload(fr) for fr in frames]     # inputs resident in HBM
+    for d in dev: dec.decode(d)                 # enqueue, no host sync
+    y, u, v = dec.read(frames[-1].frame_num)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import lib as L
+from .trace import BLOCK_DTYPE
+
+
+@dataclass
+class DeviceFrame:
+    hdr: L.ThorFrameHdr
+    blocks: int  # device pointers
+    nblocks: int
+    coeffs: int
+    clpf: int
+    intra: int
+    n_intra: int
+    nbytes: int  # bytes uploaded (descriptors + coefficients + flags + list)
+
+
+class DeviceBuffer:
+    def __init__(self, lib, nbytes: int):
+        self.lib = lib
+        self.nbytes = max(int(nbytes), 16)
+        self.ptr = lib.thor_dev_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError("thor_dev_alloc(%d) failed" % self.nbytes)
+
+    def upload(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        if a.nbytes:
+            L.check(self.lib.thor_h2d(self.ptr, a.ctypes.data, a.nbytes), "thor_h2d")
+
+    def free(self):
+        if self.ptr:
+            self.lib.thor_dev_free(self.ptr)
+            self.ptr = None
+
+
+class GpuDecoder:
+    def __init__(self, seq, device: int = 0, slots: int = 34):
+        self.lib = L.load()
+        if self.lib.thor_device_count() <= 0:
+            raise RuntimeError("no HIP device visible: the GPU decode path has no CPU fallback")
+        self.seq = seq
+        cs = L.ThorSeq(seq.width, seq.height, seq.bipred, seq.deblocking, seq.clpf, seq.tb_split_enable)
+        self.h = self.lib.thor_dec_create(C.byref(cs), device, slots)
+        if not self.h:
+            raise RuntimeError("thor_dec_create failed")
+        self._bufs = []
+
+    def close(self):
+        for b in self._bufs:
+            b.free()
+        self._bufs = []
+        if self.h:
+            self.lib.thor_dec_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _buf(self, arr: np.ndarray) -> DeviceBuffer:
+        b = DeviceBuffer(self.lib, arr.nbytes)
+        b.upload(arr)
+        self._bufs.append(b)
+        return b
+
+    def upload(self, fr) -> DeviceFrame:
+        blocks = np.ascontiguousarray(fr.blocks, dtype=BLOCK_DTYPE)
+        coeffs = np.ascontiguousarray(fr.coeffs, dtype=np.int16)
+        flags = np.ascontiguousarray(fr.clpf_flags, dtype=np.uint8)
+        n_intra = self.lib.thor_build_intra_list(blocks.ctypes.data, len(blocks), None)
+        ilist = np.zeros(max(n_intra, 1), np.uint32)
+        self.lib.thor_build_intra_list(blocks.ctypes.data, len(blocks), ilist.ctypes.data)
+        bb, cb, fb, ib = self._buf(blocks), self._buf(coeffs), self._buf(flags), self._buf(ilist)
+        hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
+        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra
+        return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, nbytes)
+
+    def decode(self, d: DeviceFrame):
+        rc = self.lib.thor_dec_frame(self.h, C.byref(d.hdr), d.blocks, d.nblocks, d.coeffs, d.clpf or None,
+                                     d.intra, d.n_intra)
+        L.check(rc, "thor_dec_frame")
+
+    def set_stop_stage(self, stage: int):
+        L.check(self.lib.thor_dec_set_stop_stage(self.h, stage), "thor_dec_set_stop_stage")
+
+    def set_stream(self, stream_ptr):
+        L.check(self.lib.thor_dec_set_stream(self.h, stream_ptr), "thor_dec_set_stream")
+
+    def stream(self):
+        return self.lib.thor_dec_stream(self.h)
+
+    def sync(self):
+        L.check(self.lib.thor_dec_sync(self.h), "thor_dec_sync")
+
+    def read(self, frame_num: int):
+        W, H = self.seq.width, self.seq.height
+        y = np.empty((H, W), np.uint8)
+        u = np.empty((H // 2, W // 2), np.uint8)
+        v = np.empty((H // 2, W // 2), np.uint8)
+        L.check(self.lib.thor_dec_read_frame(self.h, frame_num, y.ctypes.data, u.ctypes.data, v.ctypes.data),
+                "thor_dec_read_frame")
+        return y, u, v
+
+    def read_i420(self, frame_num: int) -> bytes:
+        return b"".join(p.tobytes() for p in self.read(frame_num))
+
+    def write(self, frame_num: int, y, u, v):
+        y, u, v = (np.ascontiguousarray(p, dtype=np.uint8) for p in (y, u, v))
+        L.check(self.lib.thor_dec_write_frame(self.h, frame_num, y.ctypes.data, u.ctypes.data, v.ctypes.data),
+                "thor_dec_write_frame")

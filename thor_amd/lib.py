@@ -1,0 +1,84 @@
+"""ctypes binding of libthor_amd.so (the C-ABI in include/thor_amd.h and
+include/thor_kernels.h).  The library is the product; there is no CPU
+fallback: if it is missing or no GPU is present, calls fail loudly."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libthor_amd.so")
+
+_lib = None
+
+
+class ThorSeq(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("bipred", C.c_int32), ("deblocking", C.c_int32),
+                ("clpf", C.c_int32), ("tb_split_enable", C.c_int32)]
+
+
+class ThorFrameHdr(C.Structure):
+    _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32)]
+
+
+# Every symbol the public headers declare (checked by tests/test_capi.py).
+BATCHED_SYMBOLS = [
+    "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_build_intra_list", "thor_dec_set_stop_stage",
+    "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
+    "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
+]
+SIMD_SURFACE_SYMBOLS = [
+    "block_avg_simd", "sad_calc_simd_unaligned", "get_inter_prediction_luma_simd", "get_inter_prediction_chroma_simd",
+    "transform_simd", "inverse_transform_simd", "clpf_block4", "clpf_block8",
+    "sad_calc_simd", "ssd_calc_simd", "widesad_calc_simd", "detect_clpf_simd", "sad_calc_fasthalf_simd",
+    "sad_calc_fastquarter_simd",
+]
+
+
+def load(path: str = LIB_PATH):
+    """Load the library (building it first if this checkout can)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        try:
+            from . import build as _b
+
+            _b.build()
+        except Exception as e:  # pragma: no cover - depends on toolchain
+            raise RuntimeError("libthor_amd.so is missing and could not be built: %s" % e) from e
+    L = C.CDLL(path)
+    P, i = C.c_void_p, C.c_int
+    L.thor_version.restype = C.c_char_p
+    L.thor_device_count.restype = i
+    L.thor_dec_create.argtypes = [C.POINTER(ThorSeq), i, i]
+    L.thor_dec_create.restype = P
+    L.thor_dec_destroy.argtypes = [P]
+    L.thor_dec_frame.argtypes = [P, C.POINTER(ThorFrameHdr), P, i, P, P, P, i]
+    L.thor_dec_frame.restype = i
+    L.thor_build_intra_list.argtypes = [P, i, P]
+    L.thor_build_intra_list.restype = i
+    L.thor_dec_set_stop_stage.argtypes = [P, i]
+    L.thor_dec_read_frame.argtypes = [P, i, P, P, P]
+    L.thor_dec_read_frame.restype = i
+    L.thor_dec_write_frame.argtypes = [P, i, P, P, P]
+    L.thor_dec_write_frame.restype = i
+    L.thor_dec_sync.argtypes = [P]
+    L.thor_dec_sync.restype = i
+    L.thor_dec_stream.argtypes = [P]
+    L.thor_dec_stream.restype = P
+    L.thor_dec_set_stream.argtypes = [P, P]
+    L.thor_dev_alloc.argtypes = [C.c_size_t]
+    L.thor_dev_alloc.restype = P
+    L.thor_dev_free.argtypes = [P]
+    L.thor_h2d.argtypes = [P, P, C.c_size_t]
+    L.thor_h2d.restype = i
+    L.thor_d2h.argtypes = [P, P, C.c_size_t]
+    L.thor_d2h.restype = i
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError("%s failed with status %d" % (what, rc))
