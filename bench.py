@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: Thor per-block reconstruction on MI355X.
+
+Workload (config.workload): the reference's own 4K (3840x2160) 8-frame
+config_LDB_low_complexity stream of a seeded synthetic clip
+(tests/golden/k4_low.*).  One step = GPU reconstruction of the whole stream,
+frame after frame as the decoder must (frame n+1 references frame n): per
+frame, per-4x4 side info, inter MC + dequant + inverse transform +
+reconstruction, intra, deblock Y/UV, CLPF and reference padding, all through
+libthor_amd.so's C-ABI.  The parse output (block descriptors, coefficients,
+intra list, CLPF flags) is resident in HBM before timing starts; bit parsing
+is CPU work outside the hot path.  The decoded frames are checked bit-exact
+against the reference decoder's md5s after the timed region.
+
+N > 1: one process per GPU, each reconstructing its own copy of the stream
+(independent streams, no data-path collective): scaling "weak".
+
+Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mpixels/s encode+decode, 4K LDB_low_complexity; bit-exact vs ref"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+STAGES = ["prep", "inter", "intra", "deblock", "clpf", "pad"]
+
+
+def inter_alg_bytes(frames) -> float:
+    """Algorithmic HBM bytes of the inter-reconstruction kernel over a pass of
+    the stream (BASELINE.md 'Algorithmic bytes'):
+    per inter-reconstructed pixel 1.5 B reference read (x2 bi-pred) + 1.5 B
+    reconstruction write (4:2:0, luma px counted, chroma folded into the 1.5),
+    + 2 B per coded coefficient slot read, + 72 B per descriptor read."""
+    total = 0.0
+    for fr in frames:
+        b = fr.blocks
+        inter = b["mode"] != 1
+        px = b["bwidth"].astype(np.float64) * b["bheight"].astype(np.float64)
+        bi = (b["mode"] == 3) | (((b["mode"] == 0) | (b["mode"] == 4)) & (b["dir"] == 2))
+        ref = 1.5 * px * np.where(bi, 2.0, 1.0)
+        total += float(np.sum((ref + 1.5 * px)[inter]))
+        total += 72.0 * float(np.count_nonzero(inter))
+        # coefficient slots of inter CUs
+        for c in range(3):
+            has = inter & ((b["coeff_mask"] >> c) & 1).astype(bool)
+            S = b["size"].astype(np.int64)
+            n = S if c == 0 else S // 2
+            tbs = b["tb_split"].astype(bool) if c == 0 else (b["tb_split"].astype(bool) & (S > 8))
+            nt = np.where(tbs, n // 2, n)
+            q = np.minimum(nt, 16)
+            slots = np.where(tbs, 4 * q * q, q * q)
+            total += 2.0 * float(np.sum(slots[has]))
+    return total
+
+
+def cpu_baseline(meta, gold, budget_s: float = 20.0):
+    """Reference decoder (oracle/_ref/Thordec, SIMD build, 1 thread) on the
+    same .bit, repeated up to ~budget_s; falls back to the oracle port."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "Thordec")
+    bit = os.path.join(gold, "k4_low.bit")
+    px = meta["width"] * meta["height"] * meta["frames"]
+    if os.path.exists(exe):
+        out = "/tmp/thor_bench_dec_%d.yuv" % os.getpid()
+        runs, t_tot = 0, 0.0
+        while t_tot < budget_s and runs < 30:
+            t0 = time.perf_counter()
+            subprocess.run([exe, bit, out], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            t_tot += time.perf_counter() - t0
+            runs += 1
+        ok = hashlib.md5(open(out, "rb").read()).hexdigest() == meta["dec_md5"]
+        os.remove(out)
+        return {"value": round(px * runs / t_tot / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
+                "sample": "reference Thordec (SIMD build, -O3, 1 thread) decoding the same 4K 8-frame .bit "
+                          "%d times (bit parsing included); output md5 %s" % (runs, "ok" if ok else "MISMATCH")}
+    from oracle import OracleDecoder
+    from thor_amd.trace import load_trace
+
+    seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
+    t0 = time.perf_counter()
+    dec = OracleDecoder(seq)
+    for _ in dec.run(frames):
+        pass
+    dt = time.perf_counter() - t0
+    return {"value": round(px / dt / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": "oracle restatement (plain C, 1 thread), full 8-frame stream"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per inter launch (profiles/)")
+    a = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from thor_amd import lib as L
+    from thor_amd.decoder import GpuDecoder
+    from thor_amd.trace import load_trace
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold, "streams.json")))["k4_low"]
+    seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
+    dec = GpuDecoder(seq, device=local)
+    stream = torch.cuda.current_stream(local)
+    dec.set_stream(C.c_void_p(stream.cuda_stream))
+    devs = [dec.upload(fr) for fr in frames]
+    torch.cuda.synchronize(local)
+
+    def step():
+        for d in devs:
+            dec.decode(d)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(local)
+
+    # check bit-exactness of what the steps produce
+    got = {fr.frame_num: dec.read_i420(fr.frame_num) for fr in frames}
+    yuv = b"".join(got[k] for k in sorted(got))
+    bit_exact = hashlib.md5(yuv).hexdigest() == meta["dec_md5"]
+
+    lib = L.load()
+    lib.thor_dec_set_timing(dec.h, 1)
+    ms = (C.c_double * 6)()
+    lib.thor_dec_stage_ms(dec.h, ms, 6)  # reset accumulators
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(local)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(local)
+    elapsed = time.perf_counter() - t0
+    lib.thor_dec_stage_ms(dec.h, ms, 6)
+    stage_ms = [ms[i] / a.steps for i in range(6)]  # per step (whole stream)
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ok = torch.tensor([1 if bit_exact else 0], device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        bit_exact = bool(ok.item())
+
+    px_step = seq.width * seq.height * len(frames)
+    value = world * px_step * a.steps / elapsed / 1e6
+    ms_per_step = elapsed / a.steps * 1e3
+
+    alg = inter_alg_bytes(frames)  # per step (all frames)
+    inter_ms = stage_ms[1]
+    achieved = alg / (inter_ms / 1e3) / 1e9 if inter_ms > 0 else 0.0
+    traffic = None
+    if a.traffic_json and os.path.exists(a.traffic_json):
+        traffic = json.load(open(a.traffic_json)).get("inter_hbm_bytes_per_launch")
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/i16",
+            "data": "synthetic (seeded clip, thor_amd/synth.py) encoded by the reference Thorenc; "
+                    "parse output resident in HBM",
+            "bit_exact": bit_exact,
+            "config": {
+                "workload": "decode-side per-block reconstruction of the 4K (3840x2160) 8-frame "
+                            "config_LDB_low_complexity reference stream: inter MC + dequant + inverse transform + "
+                            "recon, intra, deblock, CLPF, padding (encode-side reconstruction not yet on GPU)",
+                "frames": len(frames),
+                "width": seq.width,
+                "height": seq.height,
+                "parallelism": "replicas%d" % world,
+                "stage_ms_per_step": {k: round(v, 4) for k, v in zip(STAGES, stage_ms)},
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_inter",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": round(alg / len(frames)),
+                "avg_launch_us": round(inter_ms / len(frames) * 1e3, 2),
+            },
+        }
+        if not a.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(meta, gold)
+        print(json.dumps(out), flush=True)
+    dec.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -112,6 +112,13 @@ int thor_dec_read_frame(thor_dec_t *d, int frame_num, uint8_t *y, uint8_t *u, ui
 int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const uint8_t *u, const uint8_t *v);
 int thor_dec_sync(thor_dec_t *d);
 
+/* Per-stage GPU timing with hipEvents on the context's stream.  When on,
+ * thor_dec_frame brackets each stage; thor_dec_stage_ms waits for the stream
+ * and returns the milliseconds accumulated per stage since the last call:
+ * [0] side info, [1] inter recon, [2] intra, [3] deblock, [4] CLPF, [5] pad. */
+int thor_dec_set_timing(thor_dec_t *d, int on);
+int thor_dec_stage_ms(thor_dec_t *d, double *ms, int nstages);
+
 /* The HIP stream the context enqueues on (hipStream_t as void*), so callers
  * can record events / capture graphs around thor_dec_frame. */
 void *thor_dec_stream(thor_dec_t *d);

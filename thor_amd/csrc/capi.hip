@@ -59,6 +59,37 @@ struct thor_dec {
   size_t done_cap;
   unsigned *done;
   int stop_stage;
+  // optional per-stage timing (hipEvents on the decode stream)
+  int timing;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_marks;
+};
+
+enum { ST_PREP = 0, ST_INTER, ST_INTRA, ST_DEBLOCK, ST_CLPF, ST_PAD, ST_COUNT };
+
+static hipEvent_t ev_next(thor_dec *d) {
+  if (d->ev_used == d->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    d->ev_pool.push_back(e);
+  }
+  return d->ev_pool[d->ev_used++];
+}
+struct StageMark {
+  thor_dec *d;
+  int stage;
+  hipEvent_t a;
+  StageMark(thor_dec *d_, int s) : d(d_), stage(s), a(nullptr) {
+    if (d->timing && (a = ev_next(d))) (void)hipEventRecord(a, d->stream);
+  }
+  ~StageMark() {
+    if (!a) return;
+    hipEvent_t b = ev_next(d);
+    if (!b) return;
+    (void)hipEventRecord(b, d->stream);
+    d->ev_marks.push_back({stage, {a, b}});
+  }
 };
 
 extern "C" {
@@ -115,6 +146,8 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->stop_stage = 2;
   d->done_cap = 0;
   d->done = nullptr;
+  d->timing = 0;
+  d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
   d->stream = d->own_stream;
   ok = ok && hipMalloc(&d->slots, d->slot_bytes * num_slots) == hipSuccess;
@@ -142,6 +175,7 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->cellmap) hipFree(d->cellmap);
   if (d->ctl) hipFree(d->ctl);
   if (d->done) hipFree(d->done);
+  for (auto e : d->ev_pool) (void)hipEventDestroy(e);
   if (d->own_stream) hipStreamDestroy(d->own_stream);
   delete d;
 }
@@ -227,10 +261,14 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
   int cs = W / 4;
   hipStream_t st = d->stream;
   if (nblocks > 0) {
+    {
+    StageMark m(d, ST_PREP);
     k_prep<<<(nblocks + 3) / 4, 256, 0, st>>>(blocks, nblocks, d->cellinfo, d->cellmap, cs);
     HIPCHK(hipGetLastError());
+    }
     int tiles_w = W / 16, tiles_h = (H + 15) / 16;
     int ntiles = tiles_w * tiles_h;
+    StageMark m(d, ST_INTER);
     k_inter<<<(ntiles + 3) / 4, 256, 0, st>>>(f, blocks, coeffs, d->cellmap, tiles_w, ntiles);
     HIPCHK(hipGetLastError());
   }
@@ -243,10 +281,12 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     HIPCHK(hipMemsetAsync(d->done, 0, (size_t)nblocks * sizeof(unsigned), st));
     HIPCHK(hipMemsetAsync(d->ctl, 0, sizeof(unsigned), st));
     int grid = n_intra < 1024 ? n_intra : 1024;
+    StageMark m(d, ST_INTRA);
     k_intra<<<grid, 256, 0, st>>>(f, blocks, coeffs, intra_list, n_intra, d->ctl, d->done, d->cellmap, d->ctl + 1);
     HIPCHK(hipGetLastError());
   }
   if (d->stop_stage >= 1 && d->seq.deblocking) {
+    StageMark m(d, ST_DEBLOCK);
     int nv = ((W >> 3) - 1) * (H >> 3);
     int nh = (W >> 3) * ((H >> 3) - 1);
     k_deblock_luma_v<<<(nv + 255) / 256, 256, 0, st>>>(f.cy, d->sy, W, H, d->cellinfo, hdr->qp);
@@ -259,14 +299,38 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
   if (d->stop_stage >= 2 && d->seq.clpf && hdr->clpf_on && clpf_flags) {
     int nsb = (W / 64) * (H / 64);
     if (nsb > 0) {
+      StageMark m(d, ST_CLPF);
       k_clpf<<<nsb, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, clpf_flags);
       HIPCHK(hipGetLastError());
     }
   }
-  k_pad<<<dim3(H + 2 * THOR_PAD_Y, 3), 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H);
-  HIPCHK(hipGetLastError());
+  {
+    StageMark m(d, ST_PAD);
+    k_pad<<<dim3(H + 2 * THOR_PAD_Y, 3), 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H);
+    HIPCHK(hipGetLastError());
+  }
   d->slot_fnum[cur] = hdr->frame_num;
   d->slot_age[cur] = d->decode_count++;
+  return THOR_OK;
+}
+
+int thor_dec_set_timing(thor_dec_t *d, int on) {
+  if (!d) return THOR_ERR_ARG;
+  d->timing = on;
+  return THOR_OK;
+}
+
+int thor_dec_stage_ms(thor_dec_t *d, double *ms, int nstages) {
+  if (!d || !ms || nstages <= 0) return THOR_ERR_ARG;
+  HIPCHK(hipStreamSynchronize(d->stream));
+  for (int i = 0; i < nstages; i++) ms[i] = 0.0;
+  for (auto &m : d->ev_marks) {
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, m.second.first, m.second.second));
+    if (m.first < nstages) ms[m.first] += t;
+  }
+  d->ev_marks.clear();
+  d->ev_used = 0;
   return THOR_OK;
 }
 

@@ -2,3 +2,4 @@
 #include "recon.hip"
 #include "loopfilter.hip"
 #include "capi.hip"
+#include "simd_surface.hip"

@@ -66,6 +66,16 @@ __device__ __forceinline__ void load_bytes8(const uint8_t *p, uint32_t &e0, uint
 }
 __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255; }
 
+// Pack an already-clipped byte into lane-byte j.  The empty asm keeps hipcc
+// (ROCm 7.2, gfx950) from fusing pairs of clip255(x >> n) into
+// v_ashr_pk_u8_i32, which leaves the upper half of its destination register
+// unchanged while the compiler assumes it zero: byte 2 came out corrupted
+// (found by tests/test_gpu_kernels.py).
+__device__ __forceinline__ uint32_t put_byte(int v, int j) {
+  asm volatile("" : "+v"(v));
+  return (uint32_t)v << (8 * j);
+}
+
 // Keep every MC tap inside the padded slot.  Conformant streams stay within
 // +-80 px of the frame (the encoder clamps, enc/encode_block.c:816-828), so
 // these clamps never bind for them; they only make malformed input safe.
@@ -115,7 +125,7 @@ __device__ uint32_t mc_luma4(const uint8_t *src, int stride, int fx, int fy, int
     for (int j = 0; j < 4; j++) {
       int s = r[0][j + 1] + r[0][j + 2] + r[1][j] + 2 * r[1][j + 1] + 2 * r[1][j + 2] + r[1][j + 3] + r[2][j] +
               2 * r[2][j + 1] + 2 * r[2][j + 2] + r[2][j + 3] + r[3][j + 1] + r[3][j + 2];
-      out |= (uint32_t)clip255((s + 8) >> 4) << (8 * j);
+      out |= put_byte(clip255((s + 8) >> 4), j);
     }
     return out;
   }
@@ -136,7 +146,7 @@ __device__ uint32_t mc_luma4(const uint8_t *src, int stride, int fx, int fy, int
   uint32_t out = 0;
   for (int j = 0; j < 4; j++) {  // horizontal (inter_prediction.c:170-178)
     int s = fh[0] * v[j] + fh[1] * v[j + 1] + fh[2] * v[j + 2] + fh[3] * v[j + 3] + fh[4] * v[j + 4] + fh[5] * v[j + 5];
-    out |= (uint32_t)clip255((s + 2048) >> 12) << (8 * j);
+    out |= put_byte(clip255((s + 2048) >> 12), j);
   }
   return out;
 }
@@ -273,13 +283,13 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
       yin = yc - (tb ? (yc >= t.ntu) * t.ntu : 0);
       g = t.ntu >= 16 ? 4 : (t.ntu >> 2);
     }
-    if (res) it_pass1(t, Ms, yin >> t.rep, lane % g, g, T[lane / g]);
+    if (res) it_pass1(t, Ms, yin >> t.rep, lane % g, g, T[lane - lane % g]);
     wave_lds_sync();
     if (res) {
       outv = 0;
       for (int j = 0; j < 4; j++) {
-        int rr = it_pass2(t, Ms, (xin + j) >> t.rep, T[lane / g]);
-        outv |= (uint32_t)clip255(rr + (int)byte_of(pred, j)) << (8 * j);
+        int rr = it_pass2(t, Ms, (xin + j) >> t.rep, T[lane - lane % g]);
+        outv |= put_byte(clip255(rr + (int)byte_of(pred, j)), j);
       }
     }
     if (act) *(uint32_t *)(f.cy + (long long)y * f.sy + x) = outv;
@@ -334,11 +344,11 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
       bool res = act && mode != M_SKIP && (B.coeff_mask & (1 << comp));
       if (res) {
         t.coef = coeffs + B.coeff_off[comp] + ti * t.q * t.q;
-        it_pass1(t, Ms, yin, lane % g, g, T[lane / g]);
+        it_pass1(t, Ms, yin, lane % g, g, T[lane - lane % g]);
       }
       wave_lds_sync();
       int outv = pred;
-      if (res) outv = clip255(it_pass2(t, Ms, xin, T[lane / g]) + pred);
+      if (res) outv = clip255(it_pass2(t, Ms, xin, T[lane - lane % g]) + pred);
       wave_lds_sync();
       if (act) (comp == 1 ? f.cu : f.cv)[(long long)y * f.sc + x] = (uint8_t)outv;
     }

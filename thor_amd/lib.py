@@ -24,7 +24,7 @@ class ThorFrameHdr(C.Structure):
 # Every symbol the public headers declare (checked by tests/test_capi.py).
 BATCHED_SYMBOLS = [
     "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_build_intra_list", "thor_dec_set_stop_stage",
-    "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
+    "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
 SIMD_SURFACE_SYMBOLS = [
@@ -68,6 +68,9 @@ def load(path: str = LIB_PATH):
     L.thor_dec_stream.argtypes = [P]
     L.thor_dec_stream.restype = P
     L.thor_dec_set_stream.argtypes = [P, P]
+    L.thor_dec_set_timing.argtypes = [P, i]
+    L.thor_dec_stage_ms.argtypes = [P, C.POINTER(C.c_double), i]
+    L.thor_dec_stage_ms.restype = i
     L.thor_dev_alloc.argtypes = [C.c_size_t]
     L.thor_dev_alloc.restype = P
     L.thor_dev_free.argtypes = [P]
