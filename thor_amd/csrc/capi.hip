@@ -13,11 +13,11 @@
 
 #include "common.h"
 
-// kernels (recon.hip, loopfilter.hip)
+// kernels (recon.hip, intra.hip, loopfilter.hip)
 __global__ void k_prep(const thor_block_t *, int, uint16_t *, int32_t *, int);
 __global__ void k_inter(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int, int);
 __global__ void k_intra(FrameCtx, const thor_block_t *, const int16_t *, const uint32_t *, int, unsigned *,
-                        unsigned *, const int32_t *, unsigned *);
+                        unsigned *, int);
 __global__ void k_deblock_luma_v(uint8_t *, int, int, int, const uint16_t *, int);
 __global__ void k_deblock_luma_h(uint8_t *, int, int, int, const uint16_t *, int);
 __global__ void k_deblock_chroma_v(uint8_t *, uint8_t *, int, int, int, const uint16_t *, int);
@@ -55,9 +55,8 @@ struct thor_dec {
   long long decode_count;
   uint16_t *cellinfo;
   int32_t *cellmap;
-  unsigned *ctl;       // [0] intra head, [1] timeout flag, [2..3] pad; then done flags
-  size_t done_cap;
-  unsigned *done;
+  unsigned *ctl;       // [0] intra row head, [1] timeout flag
+  unsigned *progress;  // per SB row intra wavefront progress
   int stop_stage;
   // optional per-stage timing (hipEvents on the decode stream)
   int timing;
@@ -144,8 +143,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->slot_age.assign(num_slots, -1);
   d->decode_count = 0;
   d->stop_stage = 2;
-  d->done_cap = 0;
-  d->done = nullptr;
+  d->progress = nullptr;
   d->timing = 0;
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
@@ -158,6 +156,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   ok = ok && hipMemset(d->cellmap, 0, ncell * sizeof(int32_t)) == hipSuccess;
   ok = ok && hipMemset(d->cellinfo, 0, ncell * sizeof(uint16_t)) == hipSuccess;
   ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
+  ok = ok && hipMalloc(&d->progress, (size_t)((H + 63) / 64 + 1) * sizeof(unsigned)) == hipSuccess;
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
   if (!ok) {
     thor_dec_destroy(d);
@@ -174,7 +173,7 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->cellinfo) hipFree(d->cellinfo);
   if (d->cellmap) hipFree(d->cellmap);
   if (d->ctl) hipFree(d->ctl);
-  if (d->done) hipFree(d->done);
+  if (d->progress) hipFree(d->progress);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
   if (d->own_stream) hipStreamDestroy(d->own_stream);
   delete d;
@@ -273,16 +272,11 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     HIPCHK(hipGetLastError());
   }
   if (n_intra > 0) {
-    if ((size_t)nblocks > d->done_cap) {
-      if (d->done) HIPCHK(hipFree(d->done));
-      d->done_cap = (size_t)nblocks + 1024;
-      HIPCHK(hipMalloc(&d->done, d->done_cap * sizeof(unsigned)));
-    }
-    HIPCHK(hipMemsetAsync(d->done, 0, (size_t)nblocks * sizeof(unsigned), st));
+    int nrows = (H + 63) / 64;
+    HIPCHK(hipMemsetAsync(d->progress, 0, (size_t)nrows * sizeof(unsigned), st));
     HIPCHK(hipMemsetAsync(d->ctl, 0, sizeof(unsigned), st));
-    int grid = n_intra < 1024 ? n_intra : 1024;
     StageMark m(d, ST_INTRA);
-    k_intra<<<grid, 256, 0, st>>>(f, blocks, coeffs, intra_list, n_intra, d->ctl, d->done, d->cellmap, d->ctl + 1);
+    k_intra<<<nrows, 256, 0, st>>>(f, blocks, coeffs, intra_list, n_intra, d->ctl, d->progress, nrows);
     HIPCHK(hipGetLastError());
   }
   if (d->stop_stage >= 1 && d->seq.deblocking) {

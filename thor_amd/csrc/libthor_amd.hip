@@ -1,5 +1,6 @@
 // Single translation unit for libthor_amd.so (no relocatable device code).
 #include "recon.hip"
+#include "intra.hip"
 #include "loopfilter.hip"
 #include "capi.hip"
 #include "simd_surface.hip"

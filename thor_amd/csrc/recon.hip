@@ -355,242 +355,3 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_intra: intra CUs in decode order.  Each workgroup dequeues the next intra
-// CU (atomic head), waits until every earlier intra CU whose pixels it reads
-// has been published (done flags, agent-scope release/acquire), then restates
-// decode_and_reconstruct_block_intra (dec/decode_block.c:48-88):
-// make_top_and_left (common/intra_prediction.c:57-143), the ten predictors
-// (:145-388), dequant + inverse transform + reconstruct, per TU in raster
-// order when tb-split.  Dequeuing in decode order makes every awaited CU one
-// already held by a running workgroup, so the grid always drains.
-// ---------------------------------------------------------------------------
-struct IntraLds {
-  uint8_t top[130], left[130], tF[130], lF[130];
-  int pT[64], pL[64];
-  int8_t M[32 * 32];
-  int16_t T[16][64];
-  int tl, tlF, pTL, dc;
-  int item;
-};
-
-__device__ void intra_tu(const FrameCtx &f, IntraLds &L, uint8_t *plane, int stride, int comp, const thor_block_t &B,
-                         int ypos, int xpos, int size, int i0, int j0, int tb, int ur_cb, int dl_cb,
-                         const int16_t *coef, int has_coef, int qp, int planeW, int planeH) {
-  int tid = threadIdx.x;
-  int n = tb ? size >> 1 : size;
-  int len = 2 * n;
-  uint8_t *rf = plane + (long long)ypos * stride + xpos;  // CU origin
-  // ---- make_top_and_left (intra_prediction.c:57-143) ----
-  int dl, ur;
-  if (!tb) { dl = dl_cb; ur = ur_cb; }
-  else {
-    dl = (j0 == 0 && (i0 == 0 || dl_cb)) ? 1 : 0;
-    ur = (j0 == 0 || (i0 == 0 && ur_cb)) ? 1 : 0;
-  }
-  int toplen = ur ? n + 1 : n, leftlen = dl ? n + 1 : n;
-  bool top_none = (ypos + i0) == 0, left_none = (xpos + j0) == 0;
-  // top row source: row (i0-1) relative to the CU, columns j0..
-  const uint8_t *trow = rf + (long long)(i0 - 1) * stride + j0;
-  const uint8_t *lcol = rf + (long long)i0 * stride + j0 - 1;
-  for (int k = tid; k < len; k += 256) {
-    int tv = 128, lv = 128;
-    if (!top_none) tv = trow[k < toplen ? k : toplen - 1];
-    if (!left_none) lv = lcol[(long long)(k < leftlen ? k : leftlen - 1) * stride];
-    L.top[k] = (uint8_t)tv;
-    L.left[k] = (uint8_t)lv;
-  }
-  if (tid == 0) {
-    int tl;
-    if (top_none) tl = 128;
-    else tl = xpos > 0 ? trow[-1] : trow[0];  // both (i==0) and rblock cases read row i0-1, column j0-1
-    if (top_none) tl = left_none ? 128 : lcol[0];  // ypos+i==0: top_left = left[0]
-    L.tl = tl;
-  }
-  __syncthreads();
-  int mode = B.intra_mode;
-  // ---- filtered edges ----
-  if (mode == 4 || mode == 7 || mode == 8 || mode == 5 || mode == 6 || mode == 9) {
-    int flen = (mode == 5 || mode == 6 || mode == 9) ? 2 * n : n;  // filter_121 lengths
-    for (int k = tid; k < flen; k += 256) {
-      const uint8_t *a = (mode == 9) ? L.left : L.top;
-      int v = k == 0 ? (3 * a[0] + a[1] + 2) >> 2
-                     : (k == flen - 1 ? (a[flen - 2] + 3 * a[flen - 1] + 2) >> 2 : (a[k - 1] + 2 * a[k] + a[k + 1] + 2) >> 2);
-      if (mode == 9) L.lF[k] = (uint8_t)v;
-      else L.tF[k] = (uint8_t)v;
-      if (mode == 4 || mode == 7 || mode == 8) {
-        const uint8_t *l = L.left;
-        int w = k == 0 ? (3 * l[0] + l[1] + 2) >> 2
-                       : (k == flen - 1 ? (l[flen - 2] + 3 * l[flen - 1] + 2) >> 2 : (l[k - 1] + 2 * l[k] + l[k + 1] + 2) >> 2);
-        L.lF[k] = (uint8_t)w;
-      }
-    }
-    if (tid == 0) L.tlF = (2 * L.tl + L.left[0] + L.top[0] + 2) >> 2;
-  } else if (mode == 1) {  // planar 5-tap edges (intra_prediction.c:182-214)
-    for (int k = tid; k < 2 * n; k += 256) {
-      const uint8_t *a = k < n ? L.top : L.left;
-      int j = k < n ? k : k - n;
-      int v;
-      if (j == 0) v = 5 * a[0] + 2 * a[1] + a[2];
-      else if (j == 1) v = 3 * a[0] + 2 * a[1] + 2 * a[2] + a[3];
-      else if (j == n - 2) v = a[n - 4] + 2 * a[n - 3] + 2 * a[n - 2] + 3 * a[n - 1];
-      else if (j == n - 1) v = a[n - 3] + 2 * a[n - 2] + 5 * a[n - 1];
-      else v = a[j - 2] + 2 * a[j - 1] + 2 * a[j] + 2 * a[j + 1] + a[j + 2];
-      if (k < n) L.pT[j] = v;
-      else L.pL[j] = v;
-    }
-    if (tid == 0) L.pTL = L.left[1] + 2 * L.left[0] + 2 * L.tl + 2 * L.top[0] + L.top[1];
-  } else if (mode == 0 || mode > 9) {
-    if (tid == 0) {  // DC: get_dc_pred(xpos!=0 ? left:top, ypos!=0 ? top:left), intra_prediction.c:145-160,:366
-      const uint8_t *a = (xpos + j0) != 0 ? L.left : L.top;
-      const uint8_t *c = (ypos + i0) != 0 ? L.top : L.left;
-      int s = 0;
-      for (int k = 0; k < n; k++) s += a[k] + c[k];
-      L.dc = (s + n) / (2 * n);
-    }
-  }
-  // ---- residual pass 1: T[k][y] for all n rows ----
-  int q = n < 16 ? n : 16;
-  int ntu = n, nt = n == 64 ? 32 : n, rep = n == 64;
-  if (has_coef) {
-    int lshift = qp / 6, scale = dequant_scale(qp % 6);
-    int rshift = ilog2i(ntu) - 1, add = 1 << (rshift - 1);
-    int step = 32 / nt;
-    for (int it = tid; it < q * nt; it += 256) {
-      int k = it / nt, yp = it - k * nt;
-      int s = 0;
-      for (int m = 0; m < q; m++) s += (int)L.M[(m * step) * 32 + yp] * dq(coef[m * q + k], scale, lshift, add, rshift);
-      L.T[k][yp] = (int16_t)clip16((s + 64) >> 7);
-    }
-  }
-  __syncthreads();
-  // ---- prediction + residual + reconstruction ----
-  uint8_t *dst = rf + (long long)i0 * stride + j0;
-  for (int p = tid; p < n * n; p += 256) {
-    int i = p / n, j = p - i * n;
-    int v;
-    switch (mode) {
-      case 1: v = clip255((L.pL[i] + L.pT[j] - L.pTL + 4) / 8); break;
-      case 2: v = L.left[i]; break;
-      case 3: v = L.top[j]; break;
-      case 4: { int d = i - j; v = d > 0 ? L.lF[d - 1] : (d == 0 ? L.tlF : L.tF[-d - 1]); } break;
-      case 5: v = L.tF[i + j + 1]; break;
-      case 6: { int d = i + 2 * j; v = (d & 1) ? L.tF[(d + 1) / 2] : (L.tF[d / 2] + L.tF[d / 2 + 1]) >> 1; } break;
-      case 7: {
-        int d = i - 2 * j;
-        if (d > 1) v = L.lF[d - 2];
-        else if (d == 1) v = L.tlF;
-        else if (d == 0) v = (L.tlF + L.tF[0]) >> 1;
-        else if (d & 1) v = L.tF[(-d) / 2];
-        else v = (L.tF[(-d) / 2] + L.tF[(-d) / 2 - 1]) >> 1;
-      } break;
-      case 8: {
-        int d = 2 * i - j;
-        if (d < -1) v = L.tF[-d - 2];
-        else if (d == -1) v = L.tlF;
-        else if (d == 0) v = (L.tlF + L.lF[0]) >> 1;
-        else if (d & 1) v = L.lF[d / 2];
-        else v = (L.lF[d / 2] + L.lF[d / 2 - 1]) >> 1;
-      } break;
-      case 9: { int d = 2 * i + j; v = (d & 1) ? L.lF[(d + 1) / 2] : (L.lF[d / 2] + L.lF[d / 2 + 1]) >> 1; } break;
-      default: v = L.dc; break;
-    }
-    if (has_coef) {
-      int step = 32 / nt;
-      int xp = j >> rep, yp = i >> rep;
-      int s = 0;
-      for (int k = 0; k < q; k++) s += (int)L.M[(k * step) * 32 + xp] * (int)L.T[k][yp];
-      v = clip255(clip16((s + 2048) >> 12) + v);
-    }
-    dst[(long long)i * stride + j] = (uint8_t)v;
-  }
-  __syncthreads();  // the next TU (tb-split, raster order) reads these pixels
-}
-
-__device__ __forceinline__ int upright_available(int ypos, int xpos, int size, int width) {
-  int a = (ypos > 0) && (xpos + size < width);  // common/common_block.c:110-118
-  if (size == 32 && (ypos % 64) == 32) a = 0;
-  if (size == 16 && ((ypos % 32) == 16 || ((ypos % 64) == 32 && (xpos % 32) == 16))) a = 0;
-  if (size == 8 && ((ypos % 16) == 8 || ((ypos % 32) == 16 && (xpos % 16) == 8) || ((ypos % 64) == 32 && (xpos % 32) == 24))) a = 0;
-  return a;
-}
-__device__ __forceinline__ int downleft_available(int ypos, int xpos, int size, int height) {
-  int a = (xpos > 0) && (ypos + size < height);  // common/common_block.c:120-129
-  if (size == 64) a = 0;
-  if (size == 32 && (ypos % 64) == 32) a = 0;
-  if (size == 16 && ((ypos % 64) == 48 || ((ypos % 64) == 16 && (xpos % 32) == 16))) a = 0;
-  if (size == 8 && ((ypos % 64) == 56 || ((ypos % 16) == 8 && (xpos % 16) == 8) || ((ypos % 64) == 24 && (xpos % 32) == 16))) a = 0;
-  return a;
-}
-
-__device__ __forceinline__ unsigned ld_flag(const unsigned *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(256) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,
-                                               const int16_t *__restrict__ coeffs, const uint32_t *__restrict__ list,
-                                               int n_intra, unsigned *head, unsigned *done,
-                                               const int32_t *__restrict__ cellmap, unsigned *timeout) {
-  __shared__ IntraLds L;
-  int tid = threadIdx.x;
-  for (int i = tid; i < 1024; i += 256) L.M[i] = (int8_t)dct32_entry(i >> 5, i & 31);
-  int cs = f.W >> 2;
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) L.item = (int)atomicAdd(head, 1u);
-    __syncthreads();
-    int item = L.item;
-    if (item >= n_intra) return;
-    int b = (int)list[item];
-    const thor_block_t &B = blk[b];
-    int S = B.size, x = B.xpos, y = B.ypos;
-    // ---- wait for earlier intra CUs that own pixels this CU reads ----
-    // top row y-1 over x-1..x+S, left column x-1 over y..y+S (one extra
-    // pixel each way is the most make_top_and_left reads)
-    int ncell_t = (y > 0) ? ((S >> 2) + 2) : 0;
-    int ncell_l = (x > 0) ? ((S >> 2) + 1) : 0;
-    for (int c = tid; c < ncell_t + ncell_l; c += 256) {
-      int cx, cy;
-      if (c < ncell_t) { cy = (y - 1) >> 2; cx = ((x - 4) >> 2) + c; }
-      else { cx = (x - 1) >> 2; cy = (y >> 2) + (c - ncell_t); }
-      if (cx < 0 || cx >= cs || cy < 0 || cy >= (f.H >> 2)) continue;
-      int nb = cellmap[cy * cs + cx];
-      if (nb >= b || blk[nb].mode != M_INTRA) continue;
-      unsigned spins = 0;
-      while (ld_flag(&done[nb]) == 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 26)) { atomicOr(timeout, 1u); break; }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
-    int ur = upright_available(y, x, S, f.W), dl = downleft_available(y, x, S, f.H);
-    int tb = B.tb_split != 0;
-    int qpy = B.qp, qpc = chroma_qp(B.qp);
-    for (int comp = 0; comp < 3; comp++) {
-      int size = comp ? S >> 1 : S;
-      int tbc = comp ? (tb && S > 8) : tb;
-      uint8_t *plane = comp == 0 ? f.cy : (comp == 1 ? f.cu : f.cv);
-      int stride = comp ? f.sc : f.sy;
-      int yp = comp ? y >> 1 : y, xp = comp ? x >> 1 : x;
-      const int16_t *cp = coeffs + B.coeff_off[comp];
-      int has = (B.coeff_mask >> comp) & 1;
-      int qp = comp ? qpc : qpy;
-      if (!tbc) {
-        intra_tu(f, L, plane, stride, comp, B, yp, xp, size, 0, 0, 0, ur, dl, cp, has, qp, 0, 0);
-      } else {
-        int h = size >> 1, qq = h < 16 ? h : 16;
-        for (int t = 0; t < 4; t++)
-          intra_tu(f, L, plane, stride, comp, B, yp, xp, size, (t >> 1) * h, (t & 1) * h, 1, ur, dl, cp + t * qq * qq, has,
-                   qp, 0, 0);
-      }
-    }
-    // ---- publish ----
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&done[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
