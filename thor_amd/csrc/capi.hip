@@ -15,9 +15,9 @@
 
 // kernels (recon.hip, intra.hip, loopfilter.hip)
 __global__ void k_prep(const thor_block_t *, int, uint16_t *, int32_t *, int);
-__global__ void k_inter(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int, int);
-__global__ void k_intra(FrameCtx, const thor_block_t *, const int16_t *, const uint32_t *, int, unsigned *,
-                        unsigned *, int);
+__global__ void k_inter(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int, int, int16_t *);
+__global__ void k_intra(FrameCtx, const thor_block_t *, const uint32_t *, int, unsigned *, unsigned *, int,
+                        unsigned long long *, int, int, const int16_t *);
 __global__ void k_deblock_luma_v(uint8_t *, int, int, int, const uint16_t *, int);
 __global__ void k_deblock_luma_h(uint8_t *, int, int, int, const uint16_t *, int);
 __global__ void k_deblock_chroma_v(uint8_t *, uint8_t *, int, int, int, const uint16_t *, int);
@@ -56,7 +56,10 @@ struct thor_dec {
   uint16_t *cellinfo;
   int32_t *cellmap;
   unsigned *ctl;       // [0] intra row head, [1] timeout flag
-  unsigned *progress;  // per SB row intra wavefront progress
+  unsigned *progress;  // intra wavefront progress per (SB row, component)
+  int16_t *resid;      // intra residual planes (Y, U, V; int16), written by k_inter, read by k_intra
+  unsigned long long *dbg;  // optional per-row intra timing (debug)
+  int dbg_flags;
   int stop_stage;
   // optional per-stage timing (hipEvents on the decode stream)
   int timing;
@@ -144,6 +147,9 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->decode_count = 0;
   d->stop_stage = 2;
   d->progress = nullptr;
+  d->resid = nullptr;
+  d->dbg = nullptr;
+  d->dbg_flags = 0;
   d->timing = 0;
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
@@ -156,7 +162,8 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   ok = ok && hipMemset(d->cellmap, 0, ncell * sizeof(int32_t)) == hipSuccess;
   ok = ok && hipMemset(d->cellinfo, 0, ncell * sizeof(uint16_t)) == hipSuccess;
   ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
-  ok = ok && hipMalloc(&d->progress, (size_t)((H + 63) / 64 + 1) * sizeof(unsigned)) == hipSuccess;
+  ok = ok && hipMalloc(&d->resid, (size_t)W * H * 3) == hipSuccess;  // 1.5 px/luma px x 2 B
+  ok = ok && hipMalloc(&d->progress, (size_t)3 * ((H + 63) / 64 + 1) * sizeof(unsigned)) == hipSuccess;
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
   if (!ok) {
     thor_dec_destroy(d);
@@ -174,6 +181,7 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->cellmap) hipFree(d->cellmap);
   if (d->ctl) hipFree(d->ctl);
   if (d->progress) hipFree(d->progress);
+  if (d->resid) hipFree(d->resid);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
   if (d->own_stream) hipStreamDestroy(d->own_stream);
   delete d;
@@ -268,15 +276,19 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     int tiles_w = W / 16, tiles_h = (H + 15) / 16;
     int ntiles = tiles_w * tiles_h;
     StageMark m(d, ST_INTER);
-    k_inter<<<(ntiles + 3) / 4, 256, 0, st>>>(f, blocks, coeffs, d->cellmap, tiles_w, ntiles);
+    k_inter<<<(ntiles + 3) / 4, 256, 0, st>>>(f, blocks, coeffs, d->cellmap, tiles_w, ntiles, d->resid);
     HIPCHK(hipGetLastError());
   }
   if (n_intra > 0) {
     int nrows = (H + 63) / 64;
-    HIPCHK(hipMemsetAsync(d->progress, 0, (size_t)nrows * sizeof(unsigned), st));
+    HIPCHK(hipMemsetAsync(d->progress, 0, (size_t)3 * nrows * sizeof(unsigned), st));
     HIPCHK(hipMemsetAsync(d->ctl, 0, sizeof(unsigned), st));
     StageMark m(d, ST_INTRA);
-    k_intra<<<nrows, 256, 0, st>>>(f, blocks, coeffs, intra_list, n_intra, d->ctl, d->progress, nrows);
+    // full SB images only when inter CUs were reconstructed (their pixels are intra neighbours)
+    int full_sb = n_intra < nblocks;
+    // one 64-lane chain per (SB row, component)
+    k_intra<<<3 * nrows, 64, 0, st>>>(f, blocks, intra_list, n_intra, d->ctl, d->progress, nrows, d->dbg,
+                                      d->dbg_flags, full_sb, d->resid);
     HIPCHK(hipGetLastError());
   }
   if (d->stop_stage >= 1 && d->seq.deblocking) {
@@ -305,6 +317,15 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
   }
   d->slot_fnum[cur] = hdr->frame_num;
   d->slot_age[cur] = d->decode_count++;
+  return THOR_OK;
+}
+
+// Debug hook (not in the public header): per-row intra timing into a device
+// buffer of 4 u64 per SB row; flags bit0 ignores the wavefront waits.
+extern "C" int thor_dec_debug_intra(thor_dec_t *d, void *dev_buf, int flags) {
+  if (!d) return THOR_ERR_ARG;
+  d->dbg = (unsigned long long *)dev_buf;
+  d->dbg_flags = flags;
   return THOR_OK;
 }
 

@@ -4,45 +4,52 @@
 // Intra CUs read the pre-deblock reconstruction of their left / top / top-left
 // / top-right / bottom-left neighbours (make_top_and_left,
 // common/intra_prediction.c:57-143), so they form a dependency chain in
-// decode order.  The chain is walked as a wavefront over 64x64 SB rows (the
-// WPP pattern): one workgroup owns one SB row and reconstructs that row's
-// intra CUs in decode order; row k may work on SB l once row k-1 has
-// completed SBs 0..l+1 (the top-right neighbour is the furthest pixel read,
-// common/common_block.c:110-118; the bottom-left is never read across an SB
-// row, :120-129).  Row progress is published with an agent-scope release and
-// read with one relaxed poll + one agent-scope acquire per SB, never per CU.
+// decode order.  Y, U and V never read each other, so a frame's intra work is
+// 3 x (SB rows) independent chains.  Each chain is one wavefront (a 64-lane
+// workgroup): it owns one component of one 64x64 SB row and reconstructs that
+// row's intra CUs in decode order, with no workgroup barrier at all (LDS
+// ordering inside one wave is a wave-scope fence).  The rows of a component
+// form a wavefront (WPP pattern): row k may work on SB l once row k-1 of the
+// same component has completed SBs 0..l+1 (the top-right neighbour is the
+// furthest pixel read, common/common_block.c:110-118; the bottom-left is never
+// read across an SB row, :120-129).  Progress is published with an agent-scope
+// release and read with relaxed polls + one agent-scope acquire per SB.
 //
-// Inside a row the workgroup keeps the SB being reconstructed in LDS as a
-// padded image (the SB plus its left column and the row above), so every
-// neighbour read after the SB is loaded is an LDS read, global stores are
-// fire-and-forget, and the per-TU barriers wait on LDS only.  Rows are
-// dequeued in order (atomic head): every awaited row is held by a running
-// workgroup, so the grid always drains.
+// Per SB the chain stages, with every global load in flight at once, the
+// SB's pixel image (the row above, and in P frames the SB itself), the intra
+// residual k_inter computed for it and (per 128 CUs) the CU descriptors, so
+// every per-CU read is an LDS read and global stores are fire-and-forget.
+// Tasks (row, component) are dequeued in row order (atomic head): every
+// awaited chain is held by a running wave, so the grid always drains.
 #include "common.h"
 
-#define SBY_W 68  // luma SB image: rows -1..63, cols -1..64 (+pad), stride 68
-#define SBY_H 65
-#define SBC_W 36  // chroma: rows -1..31, cols -1..32 (+pad)
-#define SBC_H 33
+#define DESC_WIN 128  // CU descriptors staged in LDS per window load
+#define IMG_X0 4      // image column -4 at byte 0: rows are dword aligned
 
-struct IntraLds {
-  uint8_t img[SBY_H * SBY_W + 2 * SBC_H * SBC_W + 16];
-  uint8_t top[136], left[136], tF[136], lF[136];
-  int pT[64], pL[64];
-  int8_t M[32 * 32];
-  int16_t D[3][4 * 256];  // dequantised coefficients of the CU, per component (compact slots)
-  int16_t T[16][64];      // inverse transform pass 1
-  int tl, tlF, pTL, dc;
-  int row, i0, i1, seen, pub, cur_sb;
+template <int C>
+struct CompGeom {
+  static constexpr int SZ = C ? 32 : 64;      // SB size in this plane
+  static constexpr int IW = SZ + 8;           // image row: cols -4 .. SZ+3
+  static constexpr int IH = SZ + 1;           // image rows -1 .. SZ-1
+  static constexpr int DW = IW / 4;           // dwords per image row
 };
 
-__device__ __forceinline__ uint8_t *sb_img(IntraLds &L, int comp) {
-  return comp == 0 ? L.img : L.img + SBY_H * SBY_W + (comp - 1) * SBC_H * SBC_W;
-}
+struct IntraChain {
+  uint8_t img[65 * 72];          // SB image of this component
+  int16_t res[64 * 64];          // k_inter's intra residual over the SB
+  thor_block_t desc[DESC_WIN];   // intra CUs [dbase, dbase + DESC_WIN) of the row
+  uint8_t top[136], left[136];   // raw neighbours (make_top_and_left)
+  uint8_t ft[136], fl[136];      // 1-2-1 filtered top / left (over n or 2n, by mode)
+  int16_t p5t[64], p5l[64];      // planar 5-tap filtered edges
+  int tl, tlf, ptl, dcsum;
+  int task;
+};
 
-// Barrier for LDS traffic only: global stores stay in flight.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+// Ordering of this wave's LDS traffic (the only agent touching the chain's LDS).
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ int upright_available(int ypos, int xpos, int size, int width) {
@@ -61,267 +68,354 @@ __device__ __forceinline__ int downleft_available(int ypos, int xpos, int size, 
   return a;
 }
 
-__device__ __forceinline__ int f121(const uint8_t *a, int k, int len) {  // filter_121, intra_prediction.c:39-48
-  if (k == 0) return (3 * a[0] + a[1] + 2) >> 2;
-  if (k == len - 1) return (a[len - 2] + 3 * a[len - 1] + 2) >> 2;
-  return (a[k - 1] + 2 * a[k] + a[k + 1] + 2) >> 2;
+
+
+// Prediction of pixel (i, j) from the per-TU edge arrays phase A prepared:
+// the ten modes of intra_prediction.c:145-388 with every filter_121 /
+// 5-tap term looked up instead of recomputed.  ft/fl hold filter_121 over n
+// (modes 4, 7, 8) or over 2n (modes 5, 6 / 9), as get_intra_prediction
+// filters them (:250-388).
+__device__ __forceinline__ int intra_px2(const uint8_t *top, const uint8_t *left, const uint8_t *ft,
+                                         const uint8_t *fl, const int16_t *p5t, const int16_t *p5l, int tlF,
+                                         int pTL, int dc, int mode, int i, int j) {
+  switch (mode) {
+    case 1: return clip255((p5l[i] + p5t[j] - pTL + 4) / 8);  // planar, C division
+    case 2: return left[i];
+    case 3: return top[j];
+    case 4: {
+      int d = i - j;
+      return d > 0 ? fl[d - 1] : (d == 0 ? tlF : ft[-d - 1]);
+    }
+    case 5: return ft[i + j + 1];
+    case 6: {
+      int d = i + 2 * j;
+      return (d & 1) ? ft[(d + 1) >> 1] : (ft[d >> 1] + ft[(d >> 1) + 1]) >> 1;
+    }
+    case 7: {
+      int d = i - 2 * j;
+      if (d > 1) return fl[d - 2];
+      if (d == 1) return tlF;
+      if (d == 0) return (tlF + ft[0]) >> 1;
+      int h = (-d) >> 1;
+      return (d & 1) ? ft[h] : (ft[h] + ft[h - 1]) >> 1;
+    }
+    case 8: {
+      int d = 2 * i - j;
+      if (d < -1) return ft[-d - 2];
+      if (d == -1) return tlF;
+      if (d == 0) return (tlF + fl[0]) >> 1;
+      int h = d >> 1;
+      return (d & 1) ? fl[h] : (fl[h] + fl[h - 1]) >> 1;
+    }
+    case 9: {
+      int d = 2 * i + j;
+      return (d & 1) ? fl[(d + 1) >> 1] : (fl[d >> 1] + fl[(d >> 1) + 1]) >> 1;
+    }
+    default: return dc;
+  }
 }
 
-// One transform block.  (ypos, xpos): CU origin in plane coordinates;
-// (sy0, sx0): CU origin inside the SB image; (i0, j0): TU offset in the CU.
-// All 256 threads call it; three LDS-only barriers.
-__device__ void intra_tu(IntraLds &L, int comp, uint8_t *plane, int stride, int mode, int ypos, int xpos, int sy0,
-                         int sx0, int size, int i0, int j0, int tb, int ur_cb, int dl_cb, const int16_t *D,
-                         int has_coef) {
-  int tid = threadIdx.x;
-  int n = tb ? size >> 1 : size;
-  int len = 2 * n;
-  int iw = comp ? SBC_W : SBY_W;
-  uint8_t *img = sb_img(L, comp) + iw + 1;  // SB (0,0)
-  // ---- phase 1: make_top_and_left (intra_prediction.c:57-143) from the SB image ----
-  int dl, ur;
-  if (!tb) { dl = dl_cb; ur = ur_cb; }
+
+// Parameters of one transform block (uniform: scalar registers).
+struct TuP {
+  int active, n, lg, has, mode;
+  int iy, ix;           // TU origin inside the SB image
+  int toplen, leftlen, top_none, left_none;
+  int xnz, ynz;         // xnz bit0: TU x != 0 (DC selector, :366); bit1: CU x > 0 (top_left, :79/:96)
+  long long gofs;       // plane offset of the TU origin
+};
+
+// Component C's transform block of TU step t (intra_prediction.c:57-143 +
+// dec/decode_block.c:48-88: tb_split gives 4 raster sub-TUs; chroma of an
+// 8x8 CU is not split).
+template <int C>
+__device__ __forceinline__ TuP make_tup(int S, int tb, int y, int x, int mode, int cmask, int t, int ur_cb, int dl_cb,
+                                        int stride) {
+  TuP p;
+  int size = C ? S >> 1 : S;
+  int tbc = C ? (tb && S > 8) : tb;
+  p.active = t < (tbc ? 4 : 1);
+  int n = tbc ? size >> 1 : size;
+  int i0_ = tbc ? (t >> 1) * n : 0, j0_ = tbc ? (t & 1) * n : 0;
+  int yp = C ? y >> 1 : y, xp = C ? x >> 1 : x;
+  constexpr int sbm = CompGeom<C>::SZ - 1;
+  p.n = n;
+  p.lg = ilog2i(n);
+  p.has = (cmask >> C) & 1;
+  p.mode = mode;
+  p.iy = (yp & sbm) + i0_;
+  p.ix = (xp & sbm) + j0_;
+  int dl, ur;  // make_top_and_left availability (intra_prediction.c:70-76, :100-104)
+  if (!tbc) { dl = dl_cb; ur = ur_cb; }
   else {
-    dl = (j0 == 0 && (i0 == 0 || dl_cb)) ? 1 : 0;
-    ur = (j0 == 0 || (i0 == 0 && ur_cb)) ? 1 : 0;
+    dl = (j0_ == 0 && (i0_ == 0 || dl_cb)) ? 1 : 0;
+    ur = (j0_ == 0 || (i0_ == 0 && ur_cb)) ? 1 : 0;
   }
-  int toplen = ur ? n + 1 : n, leftlen = dl ? n + 1 : n;
-  bool top_none = (ypos + i0) == 0, left_none = (xpos + j0) == 0;
-  const uint8_t *trow = img + (sy0 + i0 - 1) * iw + sx0 + j0;
-  const uint8_t *lcol = img + (sy0 + i0) * iw + sx0 + j0 - 1;
-  if (tid < len) {
-    int k = tid;
-    L.top[k] = top_none ? 128 : trow[k < toplen ? k : toplen - 1];
-    L.left[k] = left_none ? 128 : lcol[(k < leftlen ? k : leftlen - 1) * iw];
-  }
-  if (tid == 255) {
-    int tl = top_none ? 128 : (xpos > 0 ? trow[-1] : trow[0]);
-    if (top_none) tl = left_none ? 128 : lcol[0];  // ypos+i==0: top_left = left[0]
-    L.tl = tl;
-  }
-  lds_barrier();
-  // ---- phase 2: edge filters / DC sum / inverse transform pass 1 ----
-  if (mode == 4 || mode == 7 || mode == 8) {
-    if (tid < n) {
-      L.tF[tid] = (uint8_t)f121(L.top, tid, n);
-      L.lF[tid] = (uint8_t)f121(L.left, tid, n);
-    }
-    if (tid == 64) L.tlF = (2 * L.tl + L.left[0] + L.top[0] + 2) >> 2;
-  } else if (mode == 5 || mode == 6) {
-    if (tid < 2 * n) L.tF[tid] = (uint8_t)f121(L.top, tid, 2 * n);
-  } else if (mode == 9) {
-    if (tid < 2 * n) L.lF[tid] = (uint8_t)f121(L.left, tid, 2 * n);
-  } else if (mode == 1) {  // planar 5-tap edges (intra_prediction.c:182-214)
-    if (tid < 2 * n) {
-      const uint8_t *a = tid < n ? L.top : L.left;
-      int j = tid < n ? tid : tid - n;
-      int v;
-      if (j == 0) v = 5 * a[0] + 2 * a[1] + a[2];
-      else if (j == 1) v = 3 * a[0] + 2 * a[1] + 2 * a[2] + a[3];
-      else if (j == n - 2) v = a[n - 4] + 2 * a[n - 3] + 2 * a[n - 2] + 3 * a[n - 1];
-      else if (j == n - 1) v = a[n - 3] + 2 * a[n - 2] + 5 * a[n - 1];
-      else v = a[j - 2] + 2 * a[j - 1] + 2 * a[j] + 2 * a[j + 1] + a[j + 2];
-      if (tid < n) L.pT[j] = v;
-      else L.pL[j] = v;
-    }
-    if (tid == 255) L.pTL = L.left[1] + 2 * L.left[0] + 2 * L.tl + 2 * L.top[0] + L.top[1];
-  } else if (mode == 0 || mode > 9) {
-    // DC: get_dc_pred(xpos!=0 ? left:top, ypos!=0 ? top:left), :145-160, :366
-    if (tid < 64) {
-      const uint8_t *a = (xpos + j0) != 0 ? L.left : L.top;
-      const uint8_t *c = (ypos + i0) != 0 ? L.top : L.left;
-      int s = tid < n ? a[tid] + c[tid] : 0;
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-      if (tid == 0) L.dc = (s + n) / (2 * n);
-    }
-  }
-  int q = n < 16 ? n : 16;
-  int nt = n == 64 ? 32 : n, rep = n == 64;
-  if (has_coef) {
-    int step = 32 / nt;
-    for (int it = tid; it < q * nt; it += 256) {
-      int k = it / nt, yp = it - k * nt;
-      int s = 0;
-      for (int m = 0; m < q; m++) s += (int)L.M[(m * step) * 32 + yp] * (int)D[m * q + k];
-      L.T[k][yp] = (int16_t)clip16((s + 64) >> 7);
-    }
-  }
-  lds_barrier();
-  // ---- phase 3: prediction + residual + reconstruction ----
-  uint8_t *dst = plane + (long long)(ypos + i0) * stride + xpos + j0;
-  uint8_t *idst = img + (sy0 + i0) * iw + sx0 + j0;
-  int step = 32 / nt;
-  int lg = ilog2i(n);
-  for (int p = tid; p < n * n; p += 256) {
-    int i = p >> lg, j = p & (n - 1);
-    int v;
-    switch (mode) {
-      case 1: v = clip255((L.pL[i] + L.pT[j] - L.pTL + 4) / 8); break;
-      case 2: v = L.left[i]; break;
-      case 3: v = L.top[j]; break;
-      case 4: { int d = i - j; v = d > 0 ? L.lF[d - 1] : (d == 0 ? L.tlF : L.tF[-d - 1]); } break;
-      case 5: v = L.tF[i + j + 1]; break;
-      case 6: { int d = i + 2 * j; v = (d & 1) ? L.tF[(d + 1) / 2] : (L.tF[d / 2] + L.tF[d / 2 + 1]) >> 1; } break;
-      case 7: {
-        int d = i - 2 * j;
-        if (d > 1) v = L.lF[d - 2];
-        else if (d == 1) v = L.tlF;
-        else if (d == 0) v = (L.tlF + L.tF[0]) >> 1;
-        else if (d & 1) v = L.tF[(-d) / 2];
-        else v = (L.tF[(-d) / 2] + L.tF[(-d) / 2 - 1]) >> 1;
-      } break;
-      case 8: {
-        int d = 2 * i - j;
-        if (d < -1) v = L.tF[-d - 2];
-        else if (d == -1) v = L.tlF;
-        else if (d == 0) v = (L.tlF + L.lF[0]) >> 1;
-        else if (d & 1) v = L.lF[d / 2];
-        else v = (L.lF[d / 2] + L.lF[d / 2 - 1]) >> 1;
-      } break;
-      case 9: { int d = 2 * i + j; v = (d & 1) ? L.lF[(d + 1) / 2] : (L.lF[d / 2] + L.lF[d / 2 + 1]) >> 1; } break;
-      default: v = L.dc; break;
-    }
-    if (has_coef) {
-      int xp = j >> rep, yp = i >> rep;
-      int s = 0;
-      for (int k = 0; k < q; k++) s += (int)L.M[(k * step) * 32 + xp] * (int)L.T[k][yp];
-      v = clip255(clip16((s + 2048) >> 12) + v);
-    }
-    idst[i * iw + j] = (uint8_t)v;
-    dst[(long long)i * stride + j] = (uint8_t)v;
-  }
-  lds_barrier();  // the next TU (tb-split raster order) / next CU reads these pixels from LDS
+  p.toplen = ur ? n + 1 : n;
+  p.leftlen = dl ? n + 1 : n;
+  p.top_none = (yp + i0_) == 0;
+  p.left_none = (xp + j0_) == 0;
+  p.xnz = ((xp + j0_) != 0) | ((xp > 0) << 1);
+  p.ynz = (yp + i0_) != 0;
+  p.gofs = (long long)(yp + i0_) * stride + xp + j0_;
+  return p;
 }
 
 __device__ __forceinline__ unsigned ld_progress(const unsigned *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Caller: every storing wave has passed a full __syncthreads() (vmcnt drained).
 __device__ __forceinline__ void publish_progress(unsigned *p, unsigned v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Load SB (k, l) with its left column and the row above (cols -1..64) from
-// the frame into the LDS image.
-__device__ void load_sb_image(IntraLds &L, const FrameCtx &f, int k, int l) {
-  int tid = threadIdx.x;
-  for (int comp = 0; comp < 3; comp++) {
-    int sz = comp ? 32 : 64, iw = comp ? SBC_W : SBY_W;
-    int W = comp ? f.W >> 1 : f.W, H = comp ? f.H >> 1 : f.H;
-    int stride = comp ? f.sc : f.sy;
-    const uint8_t *pl = comp == 0 ? f.cy : (comp == 1 ? f.cu : f.cv);
-    int y0 = k * sz, x0 = l * sz;
-    uint8_t *img = sb_img(L, comp);
-    int cols = sz + 2;
-    for (int p = tid; p < (sz + 1) * cols; p += 256) {
-      int r = p / cols, c = p - r * cols;  // image row r = frame row y0-1+r
-      int y = y0 - 1 + r, x = x0 - 1 + c;
-      uint8_t v = 0;
-      if (y >= 0 && y < H && x >= 0 && x < W + 64) v = pl[(long long)y * stride + x];  // padded slot: x<W+pad ok
-      img[r * iw + c] = v;
-    }
+// Stage SB (k, l) of component C in LDS: the pixel image and the residual.
+//  image: the row above (cols -4..SZ+3) always comes from the frame (written
+//  by row k-1, acquired).  With `full` (P frames: k_inter reconstructed the
+//  inter CUs) the SB interior and its left column come from the frame too;
+//  otherwise (every CU of the row is intra) the left column is the previous
+//  SB's last image column when that SB was this one's left neighbour, else
+//  the frame's.  Frame reads may fall in the slot's padding (row -1, columns
+//  past the right edge, rows past the bottom): those bytes are never used as
+//  neighbours (availability, common/common_block.c:100-129).
+//  residual: the SB's area of k_inter's intra residual plane.
+// Every global load is issued before the first LDS store.
+template <int C, bool FULL>
+__device__ void load_sb(IntraChain &L, const FrameCtx &f, const uint8_t *__restrict__ pl, int stride,
+                        const int16_t *__restrict__ rplane, int pw, int ph, int k, int l, bool from_prev) {
+  using G = CompGeom<C>;
+  const int lane = threadIdx.x;
+  uint8_t *img = L.img + G::IW + IMG_X0;  // image (0,0)
+  uint8_t keep = (from_prev && lane < G::SZ) ? img[lane * G::IW + G::SZ - 1] : 0;
+  // Buffer loads (range-checked, out-of-range reads return 0) keep every load
+  // unconditional, so all of them are in flight before the first wait.
+  const uint8_t *slot = f.cy - f.offy;  // the current frame's ring slot
+  __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc((void *)slot, 0, (int)f.slot_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)rplane, 0, 2 * pw * ph, 0x00020000);
+  const int pofs = (int)(pl - slot);
+  constexpr int NIMG = (FULL ? G::IH : 1) * G::DW;
+  constexpr int RI = (NIMG + 63) / 64;
+  uint32_t iv[RI];
+#pragma unroll
+  for (int r = 0; r < RI; r++) {
+    int q = lane + 64 * r;
+    int row = q / G::DW, col = q - row * G::DW;
+    int off = pofs + (k * G::SZ - 1 + row) * stride + l * G::SZ - IMG_X0 + 4 * col;
+    iv[r] = __builtin_amdgcn_raw_buffer_load_b32(fr, off, 0, 0);
   }
+  uint32_t lv = 0;
+  if (!FULL) lv = __builtin_amdgcn_raw_buffer_load_b8(fr, pofs + (k * G::SZ + (lane & (G::SZ - 1))) * stride + l * G::SZ - 1, 0, 0);
+  // residual, 4 int16 per item (rows past the plane read as 0)
+  constexpr int PER = G::SZ / 4, NR = G::SZ * PER, RR = NR / 64;
+  uint2 rv[RR];
+#pragma unroll
+  for (int r = 0; r < RR; r++) {
+    int q = lane + 64 * r;
+    int row = q / PER, x = l * G::SZ + 4 * (q - row * PER), y = k * G::SZ + row;
+    rv[r] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, 2 * (y * pw + x), 0, 0));
+  }
+  lds_order();  // `keep` read before the image is overwritten
+#pragma unroll
+  for (int r = 0; r < RI; r++) {
+    int q = lane + 64 * r;
+    int row = q / G::DW, col = q - row * G::DW;
+    if (q < NIMG) *(uint32_t *)(img + (row - 1) * G::IW - IMG_X0 + 4 * col) = iv[r];
+  }
+  if (!FULL && lane < G::SZ) img[lane * G::IW - 1] = from_prev ? keep : (uint8_t)lv;
+#pragma unroll
+  for (int r = 0; r < RR; r++) {
+    int q = lane + 64 * r;
+    int row = q / PER, col = 4 * (q - row * PER);
+    *(uint2 *)&L.res[row * G::SZ + col] = rv[r];
+  }
+  lds_order();
 }
 
-__global__ __launch_bounds__(256) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,
-                                               const int16_t *__restrict__ coeffs, const uint32_t *__restrict__ list,
-                                               int n_intra, unsigned *ctl, unsigned *progress, int nrows) {
-  __shared__ IntraLds L;
-  int tid = threadIdx.x;
-  for (int i = tid; i < 1024; i += 256) L.M[i] = (int8_t)dct32_entry(i >> 5, i & 31);
-  int nsbw = (f.W + 63) >> 6;
+// One transform block: phase A gathers the neighbours (make_top_and_left,
+// intra_prediction.c:57-143) and the edge filters the mode needs; phase C
+// predicts, adds the residual and stores to the LDS image and the frame.
+template <int C>
+__device__ void intra_tu(IntraChain &L, const TuP &p, uint8_t *__restrict__ plane, int stride, int dbg_flags) {
+  using G = CompGeom<C>;
+  const int lane = threadIdx.x;
+  uint8_t *img = L.img + G::IW + IMG_X0;
+  const int n = p.n, cnt = 2 * n, mode = p.mode;
+  const uint8_t *trow = img + (p.iy - 1) * G::IW + p.ix;
+  const uint8_t *lcol = img + p.iy * G::IW + p.ix - 1;
+  const bool dcm = mode == 0 || mode > 9;
+  int dcpart = 0;
+  for (int k = lane; k < cnt; k += 64) {
+    int T[5], Lf[5];
+#pragma unroll
+    for (int o = 0; o < 5; o++) {
+      int m = k - 2 + o;
+      m = m < 0 ? 0 : (m > cnt - 1 ? cnt - 1 : m);
+      T[o] = p.top_none ? 128 : trow[m < p.toplen ? m : p.toplen - 1];
+      Lf[o] = p.left_none ? 128 : lcol[(m < p.leftlen ? m : p.leftlen - 1) * G::IW];
+    }
+    L.top[k] = (uint8_t)T[2];
+    L.left[k] = (uint8_t)Lf[2];
+    if (mode == 4 || mode == 7 || mode == 8) {  // filter_121 over n (:39-48)
+      if (k < n) {
+        L.ft[k] = (uint8_t)(k == 0 ? (3 * T[2] + T[3] + 2) >> 2
+                                   : (k == n - 1 ? (T[1] + 3 * T[2] + 2) >> 2 : (T[1] + 2 * T[2] + T[3] + 2) >> 2));
+        L.fl[k] = (uint8_t)(k == 0 ? (3 * Lf[2] + Lf[3] + 2) >> 2
+                                   : (k == n - 1 ? (Lf[1] + 3 * Lf[2] + 2) >> 2 : (Lf[1] + 2 * Lf[2] + Lf[3] + 2) >> 2));
+      }
+    } else if (mode == 5 || mode == 6) {  // filter_121 of top over 2n
+      L.ft[k] = (uint8_t)(k == 0 ? (3 * T[2] + T[3] + 2) >> 2
+                                 : (k == cnt - 1 ? (T[1] + 3 * T[2] + 2) >> 2 : (T[1] + 2 * T[2] + T[3] + 2) >> 2));
+    } else if (mode == 9) {  // filter_121 of left over 2n
+      L.fl[k] = (uint8_t)(k == 0 ? (3 * Lf[2] + Lf[3] + 2) >> 2
+                                 : (k == cnt - 1 ? (Lf[1] + 3 * Lf[2] + 2) >> 2 : (Lf[1] + 2 * Lf[2] + Lf[3] + 2) >> 2));
+    } else if (mode == 1) {  // planar 5-tap (:190-204)
+      if (k < n) {
+        int t5, l5;
+        if (k == 0) { t5 = 5 * T[2] + 2 * T[3] + T[4]; l5 = 5 * Lf[2] + 2 * Lf[3] + Lf[4]; }
+        else if (k == 1) { t5 = 3 * T[1] + 2 * T[2] + 2 * T[3] + T[4]; l5 = 3 * Lf[1] + 2 * Lf[2] + 2 * Lf[3] + Lf[4]; }
+        else if (k == n - 2) { t5 = T[0] + 2 * T[1] + 2 * T[2] + 3 * T[3]; l5 = Lf[0] + 2 * Lf[1] + 2 * Lf[2] + 3 * Lf[3]; }
+        else if (k == n - 1) { t5 = T[0] + 2 * T[1] + 5 * T[2]; l5 = Lf[0] + 2 * Lf[1] + 5 * Lf[2]; }
+        else { t5 = T[0] + 2 * T[1] + 2 * T[2] + 2 * T[3] + T[4]; l5 = Lf[0] + 2 * Lf[1] + 2 * Lf[2] + 2 * Lf[3] + Lf[4]; }
+        L.p5t[k] = (int16_t)t5;
+        L.p5l[k] = (int16_t)l5;
+      }
+    } else if (dcm && k < n) {
+      // DC sum of get_dc_pred(xpos!=0 ? left:top, ypos!=0 ? top:left), :145-160, :366
+      int xs = p.xnz & 1;
+      dcpart += T[2] * ((!xs) + p.ynz) + Lf[2] * (xs + (!p.ynz));
+    }
+  }
+  int dc = 0;
+  if (dcm) {  // wave reduction of the DC sum
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dcpart += __shfl_xor(dcpart, o);
+    dc = (dcpart + n) / (2 * n);
+  }
+  // corner terms (uniform: every lane computes them)
+  int tl = p.top_none ? 128 : ((p.xnz & 2) ? trow[-1] : trow[0]);
+  if (p.top_none) tl = p.left_none ? 128 : lcol[0];  // ypos+i==0: top_left = left[0]
+  int t0 = p.top_none ? 128 : trow[0], t1 = p.top_none ? 128 : trow[1 < p.toplen ? 1 : p.toplen - 1];
+  int l0 = p.left_none ? 128 : lcol[0], l1 = p.left_none ? 128 : lcol[(1 < p.leftlen ? 1 : p.leftlen - 1) * G::IW];
+  int tlF = (2 * tl + l0 + t0 + 2) >> 2;
+  int pTL = l1 + 2 * l0 + 2 * tl + 2 * t0 + t1;
+  lds_order();
+  // phase C: 1x4 strips
+  const int strips = (n * n) >> 2;
+  for (int s = lane; s < strips; s += 64) {
+    int i = (s << 2) >> p.lg, j = (s << 2) & (n - 1);
+    uint2 cur = make_uint2(0, 0);
+    if (p.has) cur = *(const uint2 *)&L.res[(p.iy + i) * G::SZ + p.ix + j];
+    int rr[4] = {(int)(int16_t)(cur.x & 0xffff), (int)(int16_t)(cur.x >> 16), (int)(int16_t)(cur.y & 0xffff),
+                 (int)(int16_t)(cur.y >> 16)};
+    uint32_t w = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      w |= put_byte(clip255(intra_px2(L.top, L.left, L.ft, L.fl, L.p5t, L.p5l, tlF, pTL, dc, mode, i, j + u) + rr[u]), u);
+    *(uint32_t *)(img + (p.iy + i) * G::IW + p.ix + j) = w;
+    if (!(dbg_flags & 2)) *(uint32_t *)(plane + p.gofs + (long long)i * stride + j) = w;
+  }
+  lds_order();  // the next TU reads these pixels (and rewrites the edge arrays)
+}
+
+// One chain: component C of SB row `row`.
+template <int C>
+__device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, const thor_block_t *__restrict__ blk,
+                            const uint32_t *__restrict__ list, int i0, int i1, unsigned *ctl, unsigned *progress,
+                            int row, int full, const int16_t *__restrict__ resid, int dbg_flags, bool timed) {
+  unsigned long long tw = 0;  // ticks spent waiting on the row above (debug)
+  using G = CompGeom<C>;
+  const int lane = threadIdx.x;
+  uint8_t *const plane = C == 0 ? f.cy : (C == 1 ? f.cu : f.cv);
+  const int stride = C ? f.sc : f.sy;
+  const int pw = C ? f.W >> 1 : f.W, ph = C ? f.H >> 1 : f.H;
+  const int16_t *rplane = resid + (C == 0 ? 0 : (long long)f.W * f.H + (C == 2 ? (long long)pw * ph : 0));
+  const int nsbw = (f.W + 63) >> 6;
+  unsigned *my = progress + 3 * row + C;
+  const unsigned *above = progress + 3 * (row - 1) + C;
+  int seen = row == 0 ? 0x7fffffff : 0, pub = 0, cur_sb = -2;
+  int dbase = i0 - DESC_WIN;
+  for (int it = i0; it < i1; it++) {
+    if (it - dbase >= DESC_WIN) {  // stage the next window of CU descriptors
+      dbase = it;
+      lds_order();
+      for (int q = lane; q < DESC_WIN && it + q < i1; q += 64) L.desc[q] = blk[list[it + q]];
+      lds_order();
+    }
+    // descriptor fields are uniform: scalar registers
+    const thor_block_t &D = L.desc[it - dbase];
+    int y = __builtin_amdgcn_readfirstlane(D.ypos), x = __builtin_amdgcn_readfirstlane(D.xpos);
+    int S = __builtin_amdgcn_readfirstlane(D.size), tb = __builtin_amdgcn_readfirstlane(D.tb_split) != 0;
+    int mode = __builtin_amdgcn_readfirstlane(D.intra_mode), cmask = __builtin_amdgcn_readfirstlane(D.coeff_mask);
+    int l = x >> 6;
+    if (l != cur_sb) {
+      // SB transition: publish this chain's progress, acquire the row above, stage the SB
+      if (l > pub) {  // every SB of this row left of l is complete
+        publish_progress(my, (unsigned)l);
+        pub = l;
+      }
+      int need = l + 2 < nsbw ? l + 2 : nsbw;
+      if (dbg_flags & 1) need = 0;  // debug: ignore the wavefront dependency (wrong pixels)
+      if (seen < need) {
+        unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0;
+        unsigned v = ld_progress(above);
+        unsigned spins = 0;
+        while ((int)v < need) {
+          __builtin_amdgcn_s_sleep(1);
+          v = ld_progress(above);
+          if (++spins > (1u << 27)) { if (lane == 0) atomicOr(&ctl[1], 1u); break; }
+        }
+        seen = (int)v;
+        if (timed) tw += __builtin_amdgcn_s_memtime() - t0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      bool from_prev = !full && cur_sb == l - 1;
+      if (full) load_sb<C, true>(L, f, plane, stride, rplane, pw, ph, row, l, false);
+      else load_sb<C, false>(L, f, plane, stride, rplane, pw, ph, row, l, from_prev);
+      cur_sb = l;
+    }
+    int ur_cb = upright_available(y, x, S, f.W), dl_cb = downleft_available(y, x, S, f.H);
+    int nsteps = (C == 0 ? tb : (tb && S > 8)) ? 4 : 1;
+    for (int t = 0; t < nsteps; t++) {
+      TuP p = make_tup<C>(S, tb, y, x, mode, cmask, t, ur_cb, dl_cb, stride);
+      intra_tu<C>(L, p, plane, stride, dbg_flags);
+    }
+  }
+  publish_progress(my, 0x7fffffffu);
+  return tw;
+}
+
+__global__ __launch_bounds__(64) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,
+                                              const uint32_t *__restrict__ list, int n_intra, unsigned *ctl,
+                                              unsigned *progress, int nrows, unsigned long long *dbg, int dbg_flags,
+                                              int full_sb, const int16_t *__restrict__ resid) {
+  __shared__ IntraChain L;
+  const int lane = threadIdx.x;
   for (;;) {
-    __syncthreads();
-    if (tid == 0) {
-      int row = (int)atomicAdd(&ctl[0], 1u);
-      L.row = row;
-      if (row < nrows) {
-        // decode order is raster SB order: binary-search this row's segment
-        int lo = 0, hi = n_intra;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if ((blk[list[mid]].ypos >> 6) < row) lo = mid + 1; else hi = mid; }
-        L.i0 = lo;
-        hi = n_intra;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if ((blk[list[mid]].ypos >> 6) <= row) lo = mid + 1; else hi = mid; }
-        L.i1 = lo;
-        L.seen = row == 0 ? 0x7fffffff : 0;
-        L.pub = 0;
-        L.cur_sb = -1;
-      }
+    if (lane == 0) L.task = (int)atomicAdd(&ctl[0], 1u);
+    lds_order();
+    int task = __builtin_amdgcn_readfirstlane(L.task);
+    lds_order();
+    if (task >= 3 * nrows) return;
+    int row = task / 3, c = task - 3 * row;
+    // decode order is raster SB order: binary-search this row's segment
+    int lo = 0, hi = n_intra;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if ((blk[list[mid]].ypos >> 6) < row) lo = mid + 1; else hi = mid; }
+    int i0 = lo;
+    hi = n_intra;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if ((blk[list[mid]].ypos >> 6) <= row) lo = mid + 1; else hi = mid; }
+    int i1 = lo;
+    unsigned long long t0 = dbg ? __builtin_amdgcn_s_memtime() : 0, tw;
+    bool timed = dbg != nullptr;
+    if (c == 0) tw = intra_chain<0>(L, f, blk, list, i0, i1, ctl, progress, row, full_sb, resid, dbg_flags, timed);
+    else if (c == 1) tw = intra_chain<1>(L, f, blk, list, i0, i1, ctl, progress, row, full_sb, resid, dbg_flags, timed);
+    else tw = intra_chain<2>(L, f, blk, list, i0, i1, ctl, progress, row, full_sb, resid, dbg_flags, timed);
+    if (dbg && lane == 0) {
+      unsigned long long *o = dbg + 4 * task;
+      o[0] = t0;
+      o[1] = __builtin_amdgcn_s_memtime();
+      o[2] = tw;
+      o[3] = (unsigned long long)(i1 - i0);
     }
-    __syncthreads();
-    int row = L.row;
-    if (row >= nrows) return;
-    int i0 = L.i0, i1 = L.i1;
-    for (int it = i0; it < i1; it++) {
-      int b = (int)list[it];
-      thor_block_t B = blk[b];
-      int S = B.size, x = B.xpos, y = B.ypos;
-      int l = x >> 6;
-      if (l != L.cur_sb) {
-        // SB transition: drain this workgroup's stores, publish, acquire above row, load the new SB image
-        __syncthreads();
-        if (tid == 0) {
-          if (l > L.pub) {  // every SB of this row left of l is complete
-            publish_progress(&progress[row], (unsigned)l);
-            L.pub = l;
-          }
-          int need = l + 2 < nsbw ? l + 2 : nsbw;
-          if (L.seen < need) {
-            unsigned v = ld_progress(&progress[row - 1]);
-            unsigned spins = 0;
-            while ((int)v < need) {
-              __builtin_amdgcn_s_sleep(1);
-              v = ld_progress(&progress[row - 1]);
-              if (++spins > (1u << 27)) { atomicOr(&ctl[1], 1u); break; }
-            }
-            L.seen = (int)v;
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          L.cur_sb = l;
-        }
-        __syncthreads();
-        load_sb_image(L, f, row, l);
-        __syncthreads();
-      }
-      // stage this CU's dequantised coefficients (dequantize, common/common_block.c:132-146)
-      int tb = B.tb_split != 0;
-      for (int comp = 0; comp < 3; comp++) {
-        if (!((B.coeff_mask >> comp) & 1)) continue;
-        int size = comp ? S >> 1 : S;
-        int tbc = comp ? (tb && S > 8) : tb;
-        int n = tbc ? size >> 1 : size, q = n < 16 ? n : 16, ntu = tbc ? 4 : 1;
-        int qp = comp ? chroma_qp(B.qp) : B.qp;
-        int lshift = qp / 6, scale = dequant_scale(qp % 6);
-        int rshift = ilog2i(n) - 1, add = 1 << (rshift - 1);
-        const int16_t *cp = coeffs + B.coeff_off[comp];
-        for (int p = tid; p < ntu * q * q; p += 256)
-          L.D[comp][p] = (int16_t)wrap16(((cp[p] * scale) * (1 << lshift) + add) >> rshift);
-      }
-      lds_barrier();
-      int ur = upright_available(y, x, S, f.W), dl = downleft_available(y, x, S, f.H);
-      int mode = B.intra_mode;
-      for (int comp = 0; comp < 3; comp++) {
-        int size = comp ? S >> 1 : S;
-        int tbc = comp ? (tb && S > 8) : tb;
-        uint8_t *plane = comp == 0 ? f.cy : (comp == 1 ? f.cu : f.cv);
-        int stride = comp ? f.sc : f.sy;
-        int yp = comp ? y >> 1 : y, xp = comp ? x >> 1 : x;
-        int sbm = comp ? 31 : 63;
-        int has = (B.coeff_mask >> comp) & 1;
-        if (!tbc) {
-          intra_tu(L, comp, plane, stride, mode, yp, xp, yp & sbm, xp & sbm, size, 0, 0, 0, ur, dl, L.D[comp], has);
-        } else {
-          int h = size >> 1, qq = h < 16 ? h : 16;
-          for (int t = 0; t < 4; t++)
-            intra_tu(L, comp, plane, stride, mode, yp, xp, yp & sbm, xp & sbm, size, (t >> 1) * h, (t & 1) * h, 1, ur,
-                     dl, L.D[comp] + t * qq * qq, has);
-        }
-      }
-    }
-    __syncthreads();
-    if (tid == 0) publish_progress(&progress[row], 0x7fffffffu);
   }
 }

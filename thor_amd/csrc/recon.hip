@@ -215,12 +215,16 @@ __device__ __forceinline__ int it_pass2(const TuRef &t, const int8_t *M, int xp,
 // or four 8x8 CUs.  Restates decode_block for SKIP / MERGE / INTER / BIPRED
 // (dec/decode_block.c:213-451): MC per quarter MV (INTER/BIPRED predict four
 // size/2 quarters, :381-392), truncating bi-pred average (:272-283), then
-// decode_and_reconstruct_block_inter (:90-120).  Intra CUs are skipped here.
+// decode_and_reconstruct_block_inter (:90-120).  For intra CUs only the
+// residual (dequant + inverse transform, dec/decode_block.c:67-69,80-81) is
+// computed here -- it does not depend on neighbours -- and stored as int16
+// into `resid` for k_intra, which adds it to the prediction.
 // ---------------------------------------------------------------------------
 #define TILE_WAVES 4
 __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *__restrict__ blk,
                                                const int16_t *__restrict__ coeffs,
-                                               const int32_t *__restrict__ cellmap, int tiles_w, int ntiles) {
+                                               const int32_t *__restrict__ cellmap, int tiles_w, int ntiles,
+                                               int16_t *__restrict__ resid) {
   __shared__ int8_t Ms[32 * 32];
   __shared__ int16_t Tl[TILE_WAVES][64][16];
   for (int i = threadIdx.x; i < 1024; i += 256) Ms[i] = (int8_t)dct32_entry(i >> 5, i & 31);
@@ -240,6 +244,7 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
     int b = act ? cellmap[(y >> 2) * cs + (x >> 2)] : 0;
     const thor_block_t &B = blk[b];
     int mode = B.mode;
+    bool intra = act && mode == M_INTRA;
     act = act && mode != M_INTRA;
     if (mode == M_SKIP) act = act && (x < B.xpos + B.bwidth) && (y < B.ypos + B.bheight);
     int S = B.size;
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
         pred = (pred & p1) + (((pred ^ p1) >> 1) & 0x7f7f7f7fu);  // (p0+p1)>>1 per byte
       }
     }
-    bool res = act && mode != M_SKIP && (B.coeff_mask & 1);
+    bool res = (act || intra) && mode != M_SKIP && (B.coeff_mask & 1);
     uint32_t outv = pred;
     // residual (cooperative pass 1 over lanes sharing a TU row)
     TuRef t;
@@ -287,9 +292,16 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
     wave_lds_sync();
     if (res) {
       outv = 0;
+      int rr[4];
       for (int j = 0; j < 4; j++) {
-        int rr = it_pass2(t, Ms, (xin + j) >> t.rep, T[lane - lane % g]);
-        outv |= put_byte(clip255(rr + (int)byte_of(pred, j)), j);
+        rr[j] = it_pass2(t, Ms, (xin + j) >> t.rep, T[lane - lane % g]);
+        outv |= put_byte(clip255(rr[j] + (int)byte_of(pred, j)), j);
+      }
+      if (intra) {
+        uint2 w;
+        w.x = (uint32_t)(rr[0] & 0xffff) | ((uint32_t)rr[1] << 16);
+        w.y = (uint32_t)(rr[2] & 0xffff) | ((uint32_t)rr[3] << 16);
+        *(uint2 *)(resid + (long long)y * f.W + x) = w;
       }
     }
     if (act) *(uint32_t *)(f.cy + (long long)y * f.sy + x) = outv;
@@ -304,6 +316,7 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
     int b = act ? cellmap[((2 * y) >> 2) * cs + ((2 * x) >> 2)] : 0;
     const thor_block_t &B = blk[b];
     int mode = B.mode;
+    bool intra = act && mode == M_INTRA;
     act = act && mode != M_INTRA;
     if (mode == M_SKIP) act = act && (2 * x < B.xpos + B.bwidth) && (2 * y < B.ypos + B.bheight);
     int S = B.size, SC = S >> 1;
@@ -341,14 +354,21 @@ __global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *_
           pred = (pred + mc_chroma1(rp1, f.sc, ux & 7, uy & 7)) >> 1;
         }
       }
-      bool res = act && mode != M_SKIP && (B.coeff_mask & (1 << comp));
+      bool res = (act || intra) && mode != M_SKIP && (B.coeff_mask & (1 << comp));
       if (res) {
         t.coef = coeffs + B.coeff_off[comp] + ti * t.q * t.q;
         it_pass1(t, Ms, yin, lane % g, g, T[lane - lane % g]);
       }
       wave_lds_sync();
       int outv = pred;
-      if (res) outv = clip255(it_pass2(t, Ms, xin, T[lane - lane % g]) + pred);
+      if (res) {
+        int rr = it_pass2(t, Ms, xin, T[lane - lane % g]);
+        outv = clip255(rr + pred);
+        if (intra) {
+          long long cplane = (long long)f.W * f.H + (long long)(comp - 1) * (f.W >> 1) * (f.H >> 1);
+          resid[cplane + (long long)y * (f.W >> 1) + x] = (int16_t)rr;
+        }
+      }
       wave_lds_sync();
       if (act) (comp == 1 ? f.cu : f.cv)[(long long)y * f.sc + x] = (uint8_t)outv;
     }
