@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 databases written by tools/profile_round.sh into
+committed text/JSON under profiles/:
+
+  <tag>_rocprof_stats.txt   per-kernel calls / average / total duration
+                            (the --kernel-trace --stats pass)
+  <tag>_traffic.json        per-kernel HBM bytes per launch from the separate
+                            FETCH_SIZE and WRITE_SIZE --pmc passes
+
+HBM correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE
+reports half the bytes of a wide coalesced read, so fetched bytes are
+FETCH_SIZE(KiB) x 1024 x 2; WRITE_SIZE is taken as reported.
+
+usage: prof_summary.py <prof_dir> <tag>
+"""
+import json
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    return name.split("(")[0]
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    return rows
+
+
+def pmc(db, counter):
+    c = sqlite3.connect(db)
+    acc = defaultdict(list)
+    for name, val in c.execute("select kernel_name, value from counters_collection where counter_name=?", (counter,)):
+        acc[short(name)].append(float(val))
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = os.path.join(root, "profiles")
+    os.makedirs(out, exist_ok=True)
+    rows = kernel_stats(os.path.join(d, "trace", "run_results.db"))
+    lines = ["# rocprofv3 --kernel-trace --stats  (%s)" % tag,
+             "# command: rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline",
+             "%-24s %8s %14s %12s %8s" % ("kernel", "calls", "total_us", "avg_us", "pct")]
+    for name, calls, tot, avg, pct in rows:
+        lines.append("%-24s %8d %14.1f %12.3f %8.2f" % (short(name), calls, tot, avg, pct))
+    open(os.path.join(out, "%s_rocprof_stats.txt" % tag), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+    traffic = {"tag": tag, "correction": "fetch_bytes = FETCH_SIZE_KiB*1024*2 (gfx950 half-count); "
+                                         "write_bytes = WRITE_SIZE_KiB*1024", "kernels": {}}
+    f, nf = pmc(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
+    w, nw = pmc(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
+    for k in sorted(set(f) | set(w)):
+        fb = f.get(k, 0.0) * 1024 * 2
+        wb = w.get(k, 0.0) * 1024
+        traffic["kernels"][k] = {"fetch_kib_raw": round(f.get(k, 0.0), 1), "write_kib_raw": round(w.get(k, 0.0), 1),
+                                 "hbm_bytes_per_launch": round(fb + wb), "launches": nf.get(k, 0)}
+    if "k_inter" in traffic["kernels"]:
+        traffic["inter_hbm_bytes_per_launch"] = traffic["kernels"]["k_inter"]["hbm_bytes_per_launch"]
+    json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
