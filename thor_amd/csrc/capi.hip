@@ -15,7 +15,9 @@
 
 // kernels (recon.hip, intra.hip, loopfilter.hip)
 __global__ void k_prep(const thor_block_t *, int, uint16_t *, int32_t *, int);
-__global__ void k_inter(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int, int, int16_t *);
+__global__ void k_resid(const thor_block_t *, const int16_t *, int16_t *, int, int);
+__global__ void k_recon(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int16_t *,
+                        unsigned long long *);
 __global__ void k_intra(FrameCtx, const thor_block_t *, const uint32_t *, int, unsigned *, unsigned *, int,
                         unsigned long long *, int, int, const int16_t *);
 __global__ void k_deblock_luma_v(uint8_t *, int, int, int, const uint16_t *, int);
@@ -59,6 +61,7 @@ struct thor_dec {
   unsigned *progress;  // intra wavefront progress per (SB row, component)
   int16_t *resid;      // intra residual planes (Y, U, V; int16), written by k_inter, read by k_intra
   unsigned long long *dbg;  // optional per-row intra timing (debug)
+  unsigned long long *dbg_recon;  // optional k_recon phase stamps (debug)
   int dbg_flags;
   int stop_stage;
   // optional per-stage timing (hipEvents on the decode stream)
@@ -141,6 +144,10 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->offu = ybytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
   d->offv = ybytes + cbytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
   d->slot_bytes = ybytes + 2 * cbytes + 256;
+  if (d->slot_bytes * num_slots >= (1LL << 31)) {  // k_recon addresses the ring with 32-bit buffer offsets
+    delete d;
+    return nullptr;
+  }
   d->nslots = num_slots;
   d->slot_fnum.assign(num_slots, -1);
   d->slot_age.assign(num_slots, -1);
@@ -149,6 +156,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->progress = nullptr;
   d->resid = nullptr;
   d->dbg = nullptr;
+  d->dbg_recon = nullptr;
   d->dbg_flags = 0;
   d->timing = 0;
   d->ev_used = 0;
@@ -238,6 +246,7 @@ static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
   f.cv = cur + d->offv;
   f.slots = d->slots;
   f.slot_bytes = d->slot_bytes;
+  f.ring_bytes = d->slot_bytes * d->nslots;
   f.offy = d->offy;
   f.offu = d->offu;
   f.offv = d->offv;
@@ -254,6 +263,10 @@ static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
     f.ref_slot[f.nref] = s;
     f.nref++;
   }
+  int8_t lut[128];
+  memset(lut, -1, sizeof(lut));
+  for (int r = 0; r < f.nref; r++) lut[f.ref_fnum[r] & 127] = (int8_t)f.ref_slot[r];
+  memcpy(f.slot_lut, lut, sizeof(lut));
   return f;
 }
 
@@ -265,6 +278,11 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
   int W = d->seq.width, H = d->seq.height;
   int cur = pick_slot(d, hdr->frame_num);
   FrameCtx f = make_ctx(d, cur, hdr->frame_num);
+  // k_recon resolves references through a 128-entry table keyed by
+  // frame_num & 127: resident frame numbers must be distinct modulo 128
+  for (int a = 0; a < f.nref; a++)
+    for (int b = a + 1; b < f.nref; b++)
+      if (((f.ref_fnum[a] ^ f.ref_fnum[b]) & 127) == 0) return THOR_ERR_REF;
   int cs = W / 4;
   hipStream_t st = d->stream;
   if (nblocks > 0) {
@@ -273,10 +291,11 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     k_prep<<<(nblocks + 3) / 4, 256, 0, st>>>(blocks, nblocks, d->cellinfo, d->cellmap, cs);
     HIPCHK(hipGetLastError());
     }
-    int tiles_w = W / 16, tiles_h = (H + 15) / 16;
-    int ntiles = tiles_w * tiles_h;
+    int nsb = ((W + 63) / 64) * ((H + 63) / 64);
     StageMark m(d, ST_INTER);
-    k_inter<<<(ntiles + 3) / 4, 256, 0, st>>>(f, blocks, coeffs, d->cellmap, tiles_w, ntiles, d->resid);
+    k_resid<<<dim3(nblocks, 3), 64, 0, st>>>(blocks, coeffs, d->resid, W, H);
+    HIPCHK(hipGetLastError());
+    k_recon<<<8 * ((nsb + 7) / 8), 64, 0, st>>>(f, blocks, coeffs, d->cellmap, d->resid, d->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   if (n_intra > 0) {
@@ -326,6 +345,13 @@ extern "C" int thor_dec_debug_intra(thor_dec_t *d, void *dev_buf, int flags) {
   if (!d) return THOR_ERR_ARG;
   d->dbg = (unsigned long long *)dev_buf;
   d->dbg_flags = flags;
+  return THOR_OK;
+}
+
+// Debug hook (not in the public header): k_recon phase stamps, 8 u64 per wave.
+extern "C" int thor_dec_debug_recon(thor_dec_t *d, void *dev_buf) {
+  if (!d) return THOR_ERR_ARG;
+  d->dbg_recon = (unsigned long long *)dev_buf;
   return THOR_OK;
 }
 

@@ -18,6 +18,7 @@ struct FrameCtx {
   uint8_t *cy, *cu, *cv;  // current frame, interior (0,0)
   const uint8_t *slots;   // base of the reference ring
   long long slot_bytes;   // bytes per slot
+  long long ring_bytes;   // bytes of the whole ring (slot_bytes x slots, < 2 GiB)
   long long offy, offu, offv;  // interior (0,0) offsets inside a slot
   int sy, sc;             // luma / chroma stride (create_yuv_frame, common/common_frame.c:331-332)
   int W, H;
@@ -26,6 +27,7 @@ struct FrameCtx {
   int nref;
   int ref_fnum[THOR_MAX_SLOTS];
   int ref_slot[THOR_MAX_SLOTS];
+  int slot_lut[32];       // frame_num & 127 -> slot (int8, -1 none), 4 per word
 };
 
 // Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits

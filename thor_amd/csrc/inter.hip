@@ -1,0 +1,539 @@
+// k_recon: inter reconstruction of one 64x64 superblock per wavefront (gfx950).
+//
+// Restates, for every non-intra CU of a frame, decode_block's prediction
+// (dec/decode_block.c:213-451: SKIP / MERGE / INTER / BIPRED; INTER and BIPRED
+// predict four size/2 quarters with mv_arr[i], :381-392; truncating bi-pred
+// average, :272-283) through get_inter_prediction_luma/chroma
+// (common/inter_prediction.c:72-180), then reconstruct_block
+// (common/common_block.c:148-156) with the residual k_resid (resid.hip) left in
+// the int16 residual planes (dequantize + inverse_transform, :90-120).
+//
+// One wave per SB, SBs mapped XCD-major (a band of consecutive SBs per XCD, so
+// neighbouring SBs share their reference rows in that XCD's L2).
+//  P0  lane = 8x8 unit: resolve its four 4x4 cells' MC parameters -- quarter MV
+//      with the `sign` negation (inter_prediction.c:78-79, :125-126),
+//      reference slot, bi-pred, coded residual per component -- into LDS.
+//  P1  the SB is two jobs (rows 0-31, 32-63; x2 with a bi-pred second pass).
+//      Work item = (lane, segment): lane = 4-px luma column x 8 rows + 2-px
+//      chroma column x 4 rows per plane; segment = one 4x4 cell row (the MV may
+//      change every 4 luma rows: 8x8 INTER quarters).  A job takes the distinct
+//      (mv, slot) keys of its items one at a time (one key per job in the
+//      common case): that key's displaced reference window (37 x 96 B luma,
+//      2 x 19 x 64 B chroma) is staged HBM -> LDS with 16-byte loads, all in
+//      flight at once, biased (^0x80) on the way; the next job's first window
+//      is already in flight while this job filters (double-buffered).
+//      Horizontal taps: v_dot4_i32_i8 on the (p - 128) bytes (the bias folds
+//      into the rounding constant); vertical taps: v_dot2_i32_i16 on pairs of
+//      rows of the int16 horizontal sums.  Taps are uniform per key.  The (2,2)
+//      centre filter (inter_prediction.c:145-157) is the sum of two separable
+//      filters, [0 1 1 0]x[1 1 1 1] + [1 1 1 1]x[0 1 1 0].
+//  P2  per half: residual add where the cell's CU carries coefficients, then
+//      the lane's rows go to the frame (64 contiguous bytes per 16 lanes/row).
+//
+// Separable order: the reference computes the vertical taps first into int32
+// and the horizontal second; the sum is the same exact integer either way.
+#include <stddef.h>
+
+#include "common.h"
+
+#define SB_CELLS 256
+#define CELL_ACT 0x10000u
+#define CELL_BI 0x20000u
+#define CELL_RES(c) (0x40000u << (c))  // inter cell with a coded residual in component c
+
+// reference window for one (mv, slot) key and one half SB
+#define WL_P 96  // luma pitch: 64 + 5 taps + 15 alignment, rounded to 16 B
+#define WL_R 37  // 32 rows + 5
+#define WC_P 64  // chroma pitch: 32 + 3 + 15 -> 64
+#define WC_R 19  // 16 rows + 3
+#define WL_CH (WL_R * WL_P / 16)  // 16-byte chunks: 222
+#define WC_CH (WC_R * WC_P / 16)  // 76 per plane
+#define WIN_LOADS 6               // ceil((222 + 2 * 76) / 64)
+struct RefWin {
+  uint8_t y[WL_R * WL_P];
+  uint8_t u[WC_R * WC_P];
+  uint8_t v[WC_R * WC_P];
+};
+
+struct ReconLds {
+  RefWin win[2];            // double buffer
+  int mv0[SB_CELLS];        // per 4x4 cell: (mvx, mvy) int16 pair, sign applied
+  int mv1[SB_CELLS];
+  unsigned meta[SB_CELLS];  // slot0 | slot1 << 8 | ACT | BI | RES(c)
+  int8_t lut[128];          // display frame number & 127 -> ring slot
+};
+
+__device__ __forceinline__ int tap8(int w, int i) { return __builtin_amdgcn_sbfe(w, 8 * i, 8); }
+
+// Filter tables (common/inter_prediction.c:47-70) as packed int8 words:
+// luma word0 = taps 0..3, word1 = taps 4,5 (uni table, then the sequence-level
+// bipred table); chroma = 4 taps.  Indexed by uniform fractions: scalar loads.
+struct TapTables {
+  int luma[2][4][2];
+  int chroma[8];
+  constexpr TapTables() : luma(), chroma() {
+    const int t[2][4][6] = {{{0, 0, 64, 0, 0, 0}, {1, -7, 55, 19, -5, 1}, {1, -7, 38, 38, -7, 1}, {1, -5, 19, 55, -7, 1}},
+                            {{0, 0, 64, 0, 0, 0}, {2, -10, 59, 17, -5, 1}, {1, -8, 39, 39, -8, 1}, {1, -5, 17, 59, -10, 2}}};
+    const int c[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-4, 44, 28, -4},
+                         {-4, 36, 36, -4}, {-4, 28, 44, -4}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+    for (int b = 0; b < 2; b++)
+      for (int f = 0; f < 4; f++) {
+        luma[b][f][0] = (t[b][f][0] & 255) | ((t[b][f][1] & 255) << 8) | ((t[b][f][2] & 255) << 16) |
+                        (int)((unsigned)(t[b][f][3] & 255) << 24);
+        luma[b][f][1] = (t[b][f][4] & 255) | ((t[b][f][5] & 255) << 8);
+      }
+    for (int f = 0; f < 8; f++)
+      chroma[f] = (c[f][0] & 255) | ((c[f][1] & 255) << 8) | ((c[f][2] & 255) << 16) | (int)((unsigned)(c[f][3] & 255) << 24);
+  }
+};
+__constant__ TapTables g_taps = TapTables();
+
+// Centre (2,2) terms as 6-tap words, scaled by 16 so that the product of the
+// two 1-D sums is 256 * the 4x4 kernel weight: (S + 8) >> 4 == (256 S + 2048) >> 12.
+#define CTR_A0 0x10101000  // [0,16,16,16 | 16,0]
+#define CTR_A1 0x00000010
+#define CTR_B0 0x10100000  // [0,0,16,16 | 0,0]
+#define CTR_B1 0x00000000
+
+// Rounding constant of the 2-D filters with the (p - 128) bias folded in:
+// 2048 + 128 * 64 * 64 (every tap set sums to 64; for the centre, 64*32 + 32*64).
+#define MC_RND (2048 + 524288)
+
+// Horizontal sums H' = sum t_k (p_k - 128) fit int16 (|H'| <= 128 * 94 for
+// every luma table, 128 * 64 for the scaled centre terms, 128 * 72 chroma), so
+// the vertical pass runs on pairs of rows packed as int16x2 with
+// v_dot2_i32_i16: P(r) = (H'[r], H'[r+1]) per pixel, three dot2 per luma
+// pixel (taps (t0,t1) (t2,t3) (t4,t5)), two per chroma pixel.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int dot2(uint32_t pair, int taps, int acc) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pair), __builtin_bit_cast(s16x2, taps), acc, false);
+}
+__device__ __forceinline__ int dot4(uint32_t a, int taps, int acc) {
+  return __builtin_amdgcn_sdot4((int)a, taps, acc, false);
+}
+__device__ __forceinline__ int dot4z(uint32_t a, int taps) { return dot4(a, taps, 0); }
+__device__ __forceinline__ uint32_t pack_lo16(int lo, int hi) {  // (lo & 0xffff) | hi << 16
+  return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+// packed int16 pairs of a 6-tap word (t0,t1), (t2,t3), (t4,t5)
+__device__ __forceinline__ void tap_pairs6(int w0, int w1, int &p01, int &p23, int &p45) {
+  p01 = (tap8(w0, 0) & 0xffff) | (tap8(w0, 1) << 16);
+  p23 = (tap8(w0, 2) & 0xffff) | (tap8(w0, 3) << 16);
+  p45 = (tap8(w1, 0) & 0xffff) | (tap8(w1, 1) << 16);
+}
+
+// Four horizontal 6-tap sums from the 12 bytes d0..d2 (window bytes are stored ^ 0x80),
+// starting `sh` bytes in (the byte 2 left of the lane's first pixel).
+__device__ __forceinline__ void luma_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t sh, int tw0, int tw1,
+                                        int h[4]) {
+  const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t e1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t e2 = __builtin_amdgcn_alignbyte(d2, d2, sh);  // byte 0 = byte 8 of the window
+  h[0] = dot4(e1, tw1, dot4z(e0, tw0));
+#pragma unroll
+  for (int j = 1; j < 4; j++) {
+    const uint32_t lo = __builtin_amdgcn_alignbyte(e1, e0, j), hi = __builtin_amdgcn_alignbyte(e2, e1, j);
+    h[j] = dot4(hi, tw1, dot4z(lo, tw0));
+  }
+}
+
+__device__ __forceinline__ uint32_t mc_pack(int v, int j) { return put_byte(clip255(v >> 12), j); }  // v includes MC_RND
+__device__ __forceinline__ uint32_t avg_bytes(uint32_t a, uint32_t b) {  // (p0 + p1) >> 1 per byte
+  return (a & b) + (((a ^ b) >> 1) & 0x7f7f7f7fu);
+}
+
+
+// Luma rows R0 .. R0+N-1 of the lane's 8-row strip from the staged window.
+// `wrow` = window row of strip row -2, `wb` = window byte of column -2.
+// Vertical taps as int16 pairs v01/v23/v45; CTR adds the centre's term B
+// (horizontal [0,0,16,16,0,0], vertical [0,16,16,16,16,0]).
+template <int R0, int N, bool CTR>
+__device__ __forceinline__ void luma_rows(const uint8_t *__restrict__ win, int wrow, int wb, int tw0, int tw1, int v01,
+                                          int v23, int v45, uint32_t out[8]) {
+  int ha[6][4], hb[6][4];   // H' of the last rows (ring by strip row)
+  uint32_t pa[6][4], pb[6][4];  // P(r) = (H'[r], H'[r+1])
+  const uint32_t sh = (uint32_t)(wb & 3);
+  const uint8_t *base = win + (wb & ~3);
+  auto hrow = [&](int r) {  // strip row r -> ring, and P(r-1)
+    const uint32_t *p = (const uint32_t *)(base + (wrow + r + 2) * WL_P);
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+    luma_h4(d0, d1, d2, sh, tw0, tw1, ha[(r + 6) % 6]);
+    if (CTR) luma_h4(d0, d1, d2, sh, CTR_B0, CTR_B1, hb[(r + 6) % 6]);
+    if (r > R0 - 2) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        pa[(r + 5) % 6][j] = pack_lo16(ha[(r + 5) % 6][j], ha[(r + 6) % 6][j]);
+        if (CTR) pb[(r + 5) % 6][j] = pack_lo16(hb[(r + 5) % 6][j], hb[(r + 6) % 6][j]);
+      }
+    }
+  };
+#pragma unroll
+  for (int r = R0 - 2; r <= R0 + 2; r++) hrow(r);
+#pragma unroll
+  for (int i = R0; i < R0 + N; i++) {
+    hrow(i + 3);
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int acc = dot2(pa[(i - 2 + 6) % 6][j], v01, MC_RND);
+      acc = dot2(pa[(i + 6) % 6][j], v23, acc);
+      acc = dot2(pa[(i + 2 + 6) % 6][j], v45, acc);
+      if (CTR) {
+        acc = dot2(pb[(i - 2 + 6) % 6][j], 16 << 16, acc);
+        acc = dot2(pb[(i + 6) % 6][j], 16 | (16 << 16), acc);
+        acc = dot2(pb[(i + 2 + 6) % 6][j], 16, acc);
+      }
+      o |= mc_pack(acc, j);
+    }
+    out[i] = o;
+  }
+}
+
+// Chroma rows R0 .. R0+N-1 (of 4) of the lane's 2-px column, U and V.
+template <int R0, int N>
+__device__ __forceinline__ void chroma_rows(const RefWin &w, int wrow, int wb, int tw, int v01, int v23,
+                                            uint32_t out[4]) {
+  int hu[4][2], hv[4][2];
+  uint32_t pu[4][2], pv[4][2];
+  const uint32_t sh = (uint32_t)(wb & 3);
+  auto h2 = [&](const uint8_t *p, int h[2]) {
+    const uint32_t d0 = ((const uint32_t *)p)[0], d1 = ((const uint32_t *)p)[1];
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t e1 = sh == 3 ? d1 : __builtin_amdgcn_alignbyte(d1, d0, sh + 1);
+    h[0] = dot4z(e0, tw);
+    h[1] = dot4z(e1, tw);
+  };
+  auto hrow = [&](int r) {
+    const int o = (wrow + r + 1) * WC_P + (wb & ~3);
+    h2(w.u + o, hu[(r + 4) % 4]);
+    h2(w.v + o, hv[(r + 4) % 4]);
+    if (r > R0 - 1) {
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        pu[(r + 3) % 4][j] = pack_lo16(hu[(r + 3) % 4][j], hu[(r + 4) % 4][j]);
+        pv[(r + 3) % 4][j] = pack_lo16(hv[(r + 3) % 4][j], hv[(r + 4) % 4][j]);
+      }
+    }
+  };
+#pragma unroll
+  for (int r = R0 - 1; r <= R0 + 1; r++) hrow(r);
+#pragma unroll
+  for (int i = R0; i < R0 + N; i++) {
+    hrow(i + 2);
+    uint32_t ou = 0, ov = 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int au = dot2(pu[(i + 1) % 4][j], v23, dot2(pu[(i + 3) % 4][j], v01, MC_RND));
+      const int av = dot2(pv[(i + 1) % 4][j], v23, dot2(pv[(i + 3) % 4][j], v01, MC_RND));
+      ou |= mc_pack(au, j);
+      ov |= mc_pack(av, j);
+    }
+    out[i] = ou | (ov << 16);  // U in the low half, V in the high half
+  }
+}
+
+// The uniform filter of one key.
+struct Key {
+  int mv, slot;
+  int fx, fy, cfx, cfy;  // luma quarter / chroma eighth fractions
+  int dx, dy, cdx, cdy;  // integer displacements
+};
+__device__ __forceinline__ Key make_key(int mv, int slot) {
+  Key K;
+  K.mv = mv;
+  K.slot = slot;
+  const int mvx = (int)(int16_t)(mv & 0xffff), mvy = mv >> 16;
+  K.fx = mvx & 3; K.fy = mvy & 3; K.dx = mvx >> 2; K.dy = mvy >> 2;      // quarter-pel luma
+  K.cfx = mvx & 7; K.cfy = mvy & 7; K.cdx = mvx >> 3; K.cdy = mvy >> 3;  // the same value as 1/8-pel chroma, :80-83
+  return K;
+}
+
+// Window loads of key K for the half SB whose luma origin is (x0, y0): every
+// byte a matching item reads lies inside.  Rows / columns outside the slot's
+// padding only occur for non-conformant MVs and then read other ring memory
+// or (past the ring) zeros through the buffer descriptor -- never out of bounds.
+struct WinLoad {
+  uint4 v[WIN_LOADS];
+  int dst[WIN_LOADS];
+};
+__device__ __forceinline__ void win_issue(WinLoad &W, const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, const Key &K,
+                                          int x0, int y0) {
+  const int lane = threadIdx.x;
+  const long long sbase = (long long)K.slot * f.slot_bytes;
+  const int cx0 = x0 >> 1, cy0 = y0 >> 1;
+  const int ly = (int)(sbase + f.offy + (long long)(y0 - 2 + K.dy) * f.sy + ((x0 - 2 + K.dx) & ~15));
+  const int cu = (int)(sbase + f.offu + (long long)(cy0 - 1 + K.cdy) * f.sc + ((cx0 - 1 + K.cdx) & ~15));
+  const int uvd = (int)(f.offv - f.offu);
+#pragma unroll
+  for (int i = 0; i < WIN_LOADS; i++) {
+    const int q = lane + 64 * i;
+    int off, d;
+    if (q < WL_CH) {
+      const int r = q / (WL_P / 16), c = q - r * (WL_P / 16);
+      off = ly + r * f.sy + 16 * c;
+      d = r * WL_P + 16 * c;
+    } else {
+      const int q2 = q - WL_CH, pl = q2 >= WC_CH, q3 = q2 - pl * WC_CH;
+      const int r = q3 / (WC_P / 16), c = q3 - r * (WC_P / 16);
+      off = cu + pl * uvd + r * f.sc + 16 * c;
+      d = WL_R * WL_P + pl * (WC_R * WC_P) + r * WC_P + 16 * c;
+    }
+    W.dst[i] = q < WL_CH + 2 * WC_CH ? d : -1;
+    W.v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ring, off, 0, 0));
+  }
+}
+__device__ __forceinline__ void win_commit(const WinLoad &W, RefWin &w) {
+#pragma unroll
+  for (int i = 0; i < WIN_LOADS; i++)
+    if (W.dst[i] >= 0) {
+      uint4 v = W.v[i];
+      v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+      *(uint4 *)(w.y + W.dst[i]) = v;
+    }
+}
+
+// A job's items of this lane: segment s of half h (cell rows 8h + 2gr + s).
+struct Items {
+  unsigned pend;
+  int mv[2], slot[2];
+};
+__device__ __forceinline__ Items job_items(const ReconLds &L, int h, int pass) {
+  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  Items it;
+  it.pend = 0;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const int cell = (8 * h + 2 * gr + s) * 16 + cc;
+    const unsigned meta = L.meta[cell];
+    const bool act = (meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI));
+    it.mv[s] = pass ? L.mv1[cell] : L.mv0[cell];
+    it.slot[s] = pass ? (int)((meta >> 8) & 255) : (int)(meta & 255);
+    it.pend |= act ? (1u << s) : 0u;
+  }
+  return it;
+}
+// The first pending key of a job (uniform); false if the job has no items.
+__device__ __forceinline__ bool first_key(const Items &it, Key &K) {
+  const unsigned long long bal = __ballot(it.pend != 0);
+  if (!bal) return false;
+  const int ln = __builtin_ctzll(bal);
+  const int s1 = (it.pend & 1) ? 0 : 1;
+  K = make_key(__builtin_amdgcn_readlane(s1 ? it.mv[1] : it.mv[0], ln),
+               __builtin_amdgcn_readlane(s1 ? it.slot[1] : it.slot[0], ln));
+  return true;
+}
+
+// Filter every pending item whose key is K from the staged window; clears them.
+__device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bipred, int x0, Items &it, uint32_t ty[8],
+                                           uint32_t tc[4]) {
+  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const bool m0 = (it.pend & 1) && it.mv[0] == K.mv && it.slot[0] == K.slot;
+  const bool m1 = (it.pend & 2) && it.mv[1] == K.mv && it.slot[1] == K.slot;
+  const bool ctr = K.fx == 2 && K.fy == 2;
+  const int tw0 = ctr ? CTR_A0 : g_taps.luma[bipred][K.fx][0], tw1 = ctr ? CTR_A1 : g_taps.luma[bipred][K.fx][1];
+  int v01, v23, v45;
+  tap_pairs6(ctr ? CTR_B0 : g_taps.luma[bipred][K.fy][0], ctr ? CTR_B1 : g_taps.luma[bipred][K.fy][1], v01, v23, v45);
+  const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
+  const int lwr = 8 * gr;
+  if (ctr) {
+    if (m0 && m1) luma_rows<0, 8, true>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
+    else {
+      if (m0) luma_rows<0, 4, true>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
+      if (m1) luma_rows<4, 4, true>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
+    }
+  } else {
+    if (m0 && m1) luma_rows<0, 8, false>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
+    else {
+      if (m0) luma_rows<0, 4, false>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
+      if (m1) luma_rows<4, 4, false>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
+    }
+  }
+  const int ctw = g_taps.chroma[K.cfx], cvt = g_taps.chroma[K.cfy];
+  const int c01 = (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16), c23 = (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16);
+  const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
+  const int cwr = 4 * gr;
+  if (m0 && m1) chroma_rows<0, 4>(w, cwr, cwb, ctw, c01, c23, tc);
+  else {
+    if (m0) chroma_rows<0, 2>(w, cwr, cwb, ctw, c01, c23, tc);
+    if (m1) chroma_rows<2, 2>(w, cwr, cwb, ctw, c01, c23, tc);
+  }
+  it.pend &= ~((m0 ? 1u : 0u) | (m1 ? 2u : 0u));
+}
+
+__device__ __forceinline__ uint32_t add_res4(uint32_t p, const int16_t *__restrict__ r) {
+  const uint2 a = *(const uint2 *)r;
+  const int e[4] = {(int)(int16_t)(a.x & 0xffff), (int)(int16_t)(a.x >> 16), (int)(int16_t)(a.y & 0xffff),
+                    (int)(int16_t)(a.y >> 16)};
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) o |= put_byte(clip255((int)((p >> (8 * j)) & 255) + e[j]), j);
+  return o;
+}
+__device__ __forceinline__ uint32_t add_res2(uint32_t p, const int16_t *__restrict__ r) {
+  const uint32_t a = *(const uint32_t *)r;
+  return put_byte(clip255((int)(p & 255) + (int)(int16_t)(a & 0xffff)), 0) |
+         put_byte(clip255((int)((p >> 8) & 255) + (int)(int16_t)(a >> 16)), 1);
+}
+
+__global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__restrict__ blk,
+                                              const int16_t *__restrict__ coeffs,
+                                              const int32_t *__restrict__ cellmap, int16_t *__restrict__ resid,
+                                              unsigned long long *__restrict__ dbg) {
+  __shared__ ReconLds L;
+  const int lane = threadIdx.x;
+  // debug only (null in the product path): s_memrealtime stamps, 8 u64 per wave
+  unsigned long long *stamp = dbg ? dbg + blockIdx.x * 8 : nullptr;
+#define STAMP(i) \
+  if (stamp && lane == 0) stamp[i] = __builtin_amdgcn_s_memrealtime();
+  STAMP(0);
+  if (stamp && lane == 0) {  // placement: HW_ID (wave, simd, cu, sh, se) | XCC_ID << 32
+    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    stamp[7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+  }
+  const int sbw = (f.W + 63) >> 6, sbh = (f.H + 63) >> 6, nsb = sbw * sbh;
+  // XCD-major SB order: workgroup b runs on XCD b % 8 (round-robin dispatch);
+  // give each XCD a contiguous band of SBs.  Speed only, never correctness.
+  const int per = (nsb + 7) >> 3;
+  const int sb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (sb >= nsb) return;
+  const int sby = sb / sbw, sbx = sb - sby * sbw;
+  const int cs = f.W >> 2;
+
+  // reference lookup table, straight from the kernel argument (packed by the host)
+  if (lane < 32)
+    *(int *)&L.lut[4 * lane] =
+        ((const int *)((const char *)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(FrameCtx, slot_lut)))[lane];
+
+  // ---- P0: lane = 8x8 unit ----
+  const int ur = lane >> 3, uc = lane & 7;
+  const int uy = sby * 64 + 8 * ur, ux = sbx * 64 + 8 * uc;
+  int b = -1;
+  if (uy < f.H && ux < f.W) b = cellmap[(uy >> 2) * cs + (ux >> 2)];
+  bool inter = false, bi_any = false;
+  wave_lds_sync();  // lut
+  if (b >= 0) {
+    const thor_block_t &B = blk[b];
+    const int mode = B.mode, S = B.size, by = B.ypos, bx = B.xpos;
+    const unsigned resbits = mode == M_SKIP ? 0u : ((unsigned)(B.coeff_mask & 7) << 18);
+    const bool bi = mode == M_BIPRED || ((mode == M_SKIP || mode == M_MERGE) && B.dir == 2);
+    const int ref0 = B.ref0, ref1 = B.ref1;
+    const int sg0 = bi ? (ref0 >= f.frame_num) : (ref0 > f.frame_num);
+    const int sg1 = ref1 >= f.frame_num;
+    const int s0 = L.lut[ref0 & 127], s1 = bi ? L.lut[ref1 & 127] : 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int cy = uy + 4 * (c >> 1), cx = ux + 4 * (c & 1);
+      bool act = mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0);
+      if (mode == M_SKIP) act = act && cx < bx + B.bwidth && cy < by + B.bheight;
+      const int q = (mode == M_INTER || mode == M_BIPRED) ? 2 * (cy - by >= (S >> 1)) + (cx - bx >= (S >> 1)) : 0;
+      int m0x = B.mv0[2 * q], m0y = B.mv0[2 * q + 1], m1x = B.mv1[2 * q], m1y = B.mv1[2 * q + 1];
+      if (sg0) { m0x = -m0x; m0y = -m0y; }
+      if (sg1) { m1x = -m1x; m1y = -m1y; }
+      const int cell = (2 * ur + (c >> 1)) * 16 + 2 * uc + (c & 1);
+      L.mv0[cell] = (m0x & 0xffff) | (m0y << 16);
+      L.mv1[cell] = bi ? ((m1x & 0xffff) | (m1y << 16)) : 0;
+      L.meta[cell] = act ? ((unsigned)s0 | ((unsigned)(bi ? s1 : 0) << 8) | CELL_ACT | (bi ? CELL_BI : 0u) | resbits)
+                         : 0u;
+      inter |= act;
+      bi_any |= act && bi;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; c++) L.meta[(2 * ur + (c >> 1)) * 16 + 2 * uc + (c & 1)] = 0;
+  }
+  const bool any_inter = __ballot(inter) != 0, any_bi = __ballot(bi_any) != 0;
+  wave_lds_sync();
+  STAMP(2);
+  if (!any_inter) {
+    STAMP(5);
+    return;
+  }
+
+  // ---- P1 + P2: jobs (half h, pass p), the next job's first window in flight ----
+  const __amdgpu_buffer_rsrc_t ring =  // one descriptor over the whole ring (< 2 GiB: 32-bit offsets)
+      __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
+  const int npass = any_bi ? 2 : 1, njobs = 2 * npass;
+  const int x0 = sbx * 64, cc = lane & 15, gr = lane >> 4;
+  const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
+  Items it = job_items(L, 0, 0);
+  Key K;
+  bool have = first_key(it, K);
+  WinLoad cur;
+  if (have) win_issue(cur, f, ring, K, x0, sby * 64);
+  uint32_t ly[8], lc[4], ty[8], tc[4];
+  for (int j = 0; j < njobs; j++) {
+    const int h = j / npass, pass = j % npass;
+    const int y0 = sby * 64 + 32 * h;
+    RefWin &w = L.win[j & 1];
+    // next job's first window: issued before this job filters
+    Items nit;
+    Key NK;
+    bool nhave = false;
+    WinLoad nxt;
+    if (j + 1 < njobs) {
+      nit = job_items(L, (j + 1) / npass, (j + 1) % npass);
+      nhave = first_key(nit, NK);
+      if (nhave) win_issue(nxt, f, ring, NK, x0, sby * 64 + 32 * ((j + 1) / npass));
+    }
+    if (have) {
+      win_commit(cur, w);
+      wave_lds_sync();
+      if (j == 0) STAMP(4);
+      filter_key(w, K, f.bipred, x0, it, ty, tc);
+      // further keys of this job (rare: CU edges and 8x8 INTER quarters inside the half)
+      Key K2;
+      while (first_key(it, K2)) {
+        wave_lds_sync();  // everyone is done reading the window
+        WinLoad tmp;
+        win_issue(tmp, f, ring, K2, x0, y0);
+        win_commit(tmp, w);
+        wave_lds_sync();
+        filter_key(w, K2, f.bipred, x0, it, ty, tc);
+      }
+      // merge: pass 0 result, or the truncating bi-pred average
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const unsigned meta = L.meta[(8 * h + 2 * gr + s) * 16 + cc];
+        if (!((meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI)))) continue;
+#pragma unroll
+        for (int i = 4 * s; i < 4 * s + 4; i++) ly[i] = pass ? avg_bytes(ly[i], ty[i]) : ty[i];
+#pragma unroll
+        for (int i = 2 * s; i < 2 * s + 2; i++) lc[i] = pass ? avg_bytes(lc[i], tc[i]) : tc[i];
+      }
+    }
+    if (pass == npass - 1) {  // P2: residual + store of half h
+      const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
+      const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const unsigned meta = L.meta[(8 * h + 2 * gr + s) * 16 + cc];
+        if (!(meta & CELL_ACT)) continue;
+#pragma unroll
+        for (int i = 4 * s; i < 4 * s + 4; i++) {
+          const int y = yb + i;
+          uint32_t v = ly[i];
+          if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
+          *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
+        }
+#pragma unroll
+        for (int i = 2 * s; i < 2 * s + 2; i++) {
+          const int y = ycb + i;
+          uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
+          if (meta & CELL_RES(1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
+          if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
+          *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
+          *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
+        }
+      }
+    }
+    wave_lds_sync();  // window j & 1 is rewritten by job j + 2
+    it = nit;
+    K = NK;
+    have = nhave;
+    cur = nxt;
+  }
+  STAMP(3);
+  STAMP(5);
+#undef STAMP
+}

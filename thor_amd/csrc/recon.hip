@@ -166,212 +166,3 @@ __device__ int mc_chroma1(const uint8_t *src, int stride, int fx, int fy) {
   }
   return clip255((s + 2048) >> 12);
 }
-
-// ---------------------------------------------------------------------------
-// Residual: dequantize (common/common_block.c:132-146) + inverse transform
-// (common/transform.c:432-518) restricted to the pixels a lane owns.
-//   T[k][y'] = clip16((sum_m M[m][y'] * D[m][k] + 64) >> 7)     pass 1
-//   r[y][x]  = clip16((sum_k M[k][x'] * T[k][y'] + 2048) >> 12) pass 2
-// with m, k < q = min(N,16) (only the low-frequency corner is coded), M the
-// N-point basis (N = 32 and x' = x/2, y' = y/2 for 64x64 TUs: 32-point IT
-// then 2x2 replication, transform.c:496-517).  Pass 1 is shared by the `g`
-// lanes that own the same TU row: lane `member` computes k = member, member+g..
-// ---------------------------------------------------------------------------
-struct TuRef {
-  const int16_t *coef;  // compact q x q slots
-  int ntu;              // TU size as coded (4..64): dequant shift
-  int n;                // transform size (ntu, or 32 for 64)
-  int q;                // min(n, 16)
-  int qp;
-  int rep;              // 1 for 64x64 TUs
-};
-
-__device__ __forceinline__ int dq(int c, int scale, int lshift, int add, int rshift) {
-  return wrap16(((c * scale) * (1 << lshift) + add) >> rshift);
-}
-
-// pass 1 for IT row yp: this lane's share of T[k], written to lds[k]
-__device__ __forceinline__ void it_pass1(const TuRef &t, const int8_t *M, int yp, int member, int g, int16_t *lds) {
-  int lshift = t.qp / 6, scale = dequant_scale(t.qp % 6);
-  int rshift = ilog2i(t.ntu) - 1, add = 1 << (rshift - 1);
-  int step = 32 / t.n;
-  for (int k = member; k < t.q; k += g) {
-    int s = 0;
-    for (int m = 0; m < t.q; m++) s += (int)M[(m * step) * 32 + yp] * dq(t.coef[m * t.q + k], scale, lshift, add, rshift);
-    lds[k] = (int16_t)clip16((s + 64) >> 7);
-  }
-}
-__device__ __forceinline__ int it_pass2(const TuRef &t, const int8_t *M, int xp, const int16_t *T) {
-  int step = 32 / t.n;
-  int s = 0;
-  for (int k = 0; k < t.q; k++) s += (int)M[(k * step) * 32 + xp] * (int)T[k];
-  return clip16((s + 2048) >> 12);
-}
-
-// ---------------------------------------------------------------------------
-// k_inter: one wavefront per 16x16 luma tile (+ its 8x8 U and V tiles).
-// Each lane owns a 1x4 luma strip and one pixel of each chroma plane; the CU
-// covering a lane comes from the cell map, so a tile may hold one CU (>= 16)
-// or four 8x8 CUs.  Restates decode_block for SKIP / MERGE / INTER / BIPRED
-// (dec/decode_block.c:213-451): MC per quarter MV (INTER/BIPRED predict four
-// size/2 quarters, :381-392), truncating bi-pred average (:272-283), then
-// decode_and_reconstruct_block_inter (:90-120).  For intra CUs only the
-// residual (dequant + inverse transform, dec/decode_block.c:67-69,80-81) is
-// computed here -- it does not depend on neighbours -- and stored as int16
-// into `resid` for k_intra, which adds it to the prediction.
-// ---------------------------------------------------------------------------
-#define TILE_WAVES 4
-__global__ __launch_bounds__(256) void k_inter(FrameCtx f, const thor_block_t *__restrict__ blk,
-                                               const int16_t *__restrict__ coeffs,
-                                               const int32_t *__restrict__ cellmap, int tiles_w, int ntiles,
-                                               int16_t *__restrict__ resid) {
-  __shared__ int8_t Ms[32 * 32];
-  __shared__ int16_t Tl[TILE_WAVES][64][16];
-  for (int i = threadIdx.x; i < 1024; i += 256) Ms[i] = (int8_t)dct32_entry(i >> 5, i & 31);
-  __syncthreads();
-  int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int tile = blockIdx.x * TILE_WAVES + wave;
-  if (tile >= ntiles) return;
-  int ty = tile / tiles_w, tx = tile - ty * tiles_w;
-  int cs = f.W >> 2;
-  int16_t(*T)[16] = Tl[wave];
-
-  // ---------------- luma: lane -> row r, columns c0..c0+3 ----------------
-  {
-    int r = lane >> 2, c0 = (lane & 3) * 4;
-    int y = ty * 16 + r, x = tx * 16 + c0;
-    bool act = y < f.H;
-    int b = act ? cellmap[(y >> 2) * cs + (x >> 2)] : 0;
-    const thor_block_t &B = blk[b];
-    int mode = B.mode;
-    bool intra = act && mode == M_INTRA;
-    act = act && mode != M_INTRA;
-    if (mode == M_SKIP) act = act && (x < B.xpos + B.bwidth) && (y < B.ypos + B.bheight);
-    int S = B.size;
-    int xc = x - B.xpos, yc = y - B.ypos;
-    uint32_t pred = 0;
-    if (act) {
-      int q = (mode == M_INTER || mode == M_BIPRED) ? (2 * (yc >= (S >> 1)) + (xc >= (S >> 1))) : 0;
-      bool bi = mode == M_BIPRED || ((mode == M_SKIP || mode == M_MERGE) && B.dir == 2);
-      int mvx = B.mv0[2 * q], mvy = B.mv0[2 * q + 1];
-      int sg = bi ? (B.ref0 >= f.frame_num) : (B.ref0 > f.frame_num);
-      if (sg) { mvx = -mvx; mvy = -mvy; }
-      int sl = find_slot(f, B.ref0);
-      const uint8_t *rp = slot_plane(f, sl < 0 ? 0 : sl, 0) + (long long)ry_clamp(y + (mvy >> 2), f.H) * f.sy +
-                          rx_clamp(x + (mvx >> 2), f.W);
-      pred = mc_luma4(rp, f.sy, mvx & 3, mvy & 3, f.bipred);
-      if (bi) {
-        int ux = B.mv1[2 * q], uy = B.mv1[2 * q + 1];
-        if (B.ref1 >= f.frame_num) { ux = -ux; uy = -uy; }
-        int s1 = find_slot(f, B.ref1);
-        const uint8_t *rp1 = slot_plane(f, s1 < 0 ? 0 : s1, 0) + (long long)ry_clamp(y + (uy >> 2), f.H) * f.sy +
-                             rx_clamp(x + (ux >> 2), f.W);
-        uint32_t p1 = mc_luma4(rp1, f.sy, ux & 3, uy & 3, f.bipred);
-        pred = (pred & p1) + (((pred ^ p1) >> 1) & 0x7f7f7f7fu);  // (p0+p1)>>1 per byte
-      }
-    }
-    bool res = (act || intra) && mode != M_SKIP && (B.coeff_mask & 1);
-    uint32_t outv = pred;
-    // residual (cooperative pass 1 over lanes sharing a TU row)
-    TuRef t;
-    int xin = 0, yin = 0, g = 1;
-    if (res) {
-      int tb = B.tb_split != 0;
-      t.ntu = tb ? S >> 1 : S;
-      t.rep = t.ntu == 64;
-      t.n = t.rep ? 32 : t.ntu;
-      t.q = t.n < 16 ? t.n : 16;
-      t.qp = B.qp;
-      int ti = tb ? (2 * (yc >= t.ntu) + (xc >= t.ntu)) : 0;
-      t.coef = coeffs + B.coeff_off[0] + ti * t.q * t.q;
-      xin = xc - (tb ? (xc >= t.ntu) * t.ntu : 0);
-      yin = yc - (tb ? (yc >= t.ntu) * t.ntu : 0);
-      g = t.ntu >= 16 ? 4 : (t.ntu >> 2);
-    }
-    if (res) it_pass1(t, Ms, yin >> t.rep, lane % g, g, T[lane - lane % g]);
-    wave_lds_sync();
-    if (res) {
-      outv = 0;
-      int rr[4];
-      for (int j = 0; j < 4; j++) {
-        rr[j] = it_pass2(t, Ms, (xin + j) >> t.rep, T[lane - lane % g]);
-        outv |= put_byte(clip255(rr[j] + (int)byte_of(pred, j)), j);
-      }
-      if (intra) {
-        uint2 w;
-        w.x = (uint32_t)(rr[0] & 0xffff) | ((uint32_t)rr[1] << 16);
-        w.y = (uint32_t)(rr[2] & 0xffff) | ((uint32_t)rr[3] << 16);
-        *(uint2 *)(resid + (long long)y * f.W + x) = w;
-      }
-    }
-    if (act) *(uint32_t *)(f.cy + (long long)y * f.sy + x) = outv;
-  }
-  wave_lds_sync();
-
-  // ---------------- chroma: lane -> one pixel of each plane ----------------
-  {
-    int r = lane >> 3, c = lane & 7;
-    int y = ty * 8 + r, x = tx * 8 + c;  // chroma coordinates
-    bool act = y < (f.H >> 1);
-    int b = act ? cellmap[((2 * y) >> 2) * cs + ((2 * x) >> 2)] : 0;
-    const thor_block_t &B = blk[b];
-    int mode = B.mode;
-    bool intra = act && mode == M_INTRA;
-    act = act && mode != M_INTRA;
-    if (mode == M_SKIP) act = act && (2 * x < B.xpos + B.bwidth) && (2 * y < B.ypos + B.bheight);
-    int S = B.size, SC = S >> 1;
-    int xc = x - (B.xpos >> 1), yc = y - (B.ypos >> 1);
-    int q = (mode == M_INTER || mode == M_BIPRED) ? (2 * (yc >= (SC >> 1)) + (xc >= (SC >> 1))) : 0;
-    bool bi = mode == M_BIPRED || ((mode == M_SKIP || mode == M_MERGE) && B.dir == 2);
-    int mvx = B.mv0[2 * q], mvy = B.mv0[2 * q + 1];
-    if (bi ? (B.ref0 >= f.frame_num) : (B.ref0 > f.frame_num)) { mvx = -mvx; mvy = -mvy; }
-    int ux = B.mv1[2 * q], uy = B.mv1[2 * q + 1];
-    if (B.ref1 >= f.frame_num) { ux = -ux; uy = -uy; }
-    int sl0 = act ? find_slot(f, B.ref0) : 0, sl1 = (act && bi) ? find_slot(f, B.ref1) : 0;
-    sl0 = sl0 < 0 ? 0 : sl0;
-    sl1 = sl1 < 0 ? 0 : sl1;
-    int tbc = B.tb_split && S > 8;  // dec/decode_block.c:449-450
-    TuRef t;
-    int xin = 0, yin = 0, g = 1;
-    t.ntu = tbc ? SC >> 1 : SC;
-    t.rep = 0;
-    t.n = t.ntu;
-    t.q = t.n < 16 ? t.n : 16;
-    t.qp = chroma_qp(B.qp);
-    int ti = tbc ? (2 * (yc >= t.ntu) + (xc >= t.ntu)) : 0;
-    xin = xc - (tbc ? (xc >= t.ntu) * t.ntu : 0);
-    yin = yc - (tbc ? (yc >= t.ntu) * t.ntu : 0);
-    g = t.ntu >= 8 ? 8 : t.ntu;
-    for (int comp = 1; comp <= 2; comp++) {
-      int pred = 0;
-      if (act) {
-        const uint8_t *rp = slot_plane(f, sl0, comp) + (long long)ry_clamp_c(y + (mvy >> 3), f.H >> 1) * f.sc +
-                            rx_clamp_c(x + (mvx >> 3), f.W >> 1);
-        pred = mc_chroma1(rp, f.sc, mvx & 7, mvy & 7);
-        if (bi) {
-          const uint8_t *rp1 = slot_plane(f, sl1, comp) + (long long)ry_clamp_c(y + (uy >> 3), f.H >> 1) * f.sc +
-                               rx_clamp_c(x + (ux >> 3), f.W >> 1);
-          pred = (pred + mc_chroma1(rp1, f.sc, ux & 7, uy & 7)) >> 1;
-        }
-      }
-      bool res = (act || intra) && mode != M_SKIP && (B.coeff_mask & (1 << comp));
-      if (res) {
-        t.coef = coeffs + B.coeff_off[comp] + ti * t.q * t.q;
-        it_pass1(t, Ms, yin, lane % g, g, T[lane - lane % g]);
-      }
-      wave_lds_sync();
-      int outv = pred;
-      if (res) {
-        int rr = it_pass2(t, Ms, xin, T[lane - lane % g]);
-        outv = clip255(rr + pred);
-        if (intra) {
-          long long cplane = (long long)f.W * f.H + (long long)(comp - 1) * (f.W >> 1) * (f.H >> 1);
-          resid[cplane + (long long)y * (f.W >> 1) + x] = (int16_t)rr;
-        }
-      }
-      wave_lds_sync();
-      if (act) (comp == 1 ? f.cu : f.cv)[(long long)y * f.sc + x] = (uint8_t)outv;
-    }
-  }
-}
-

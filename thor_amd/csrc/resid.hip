@@ -1,0 +1,118 @@
+// k_resid: residual of every coded transform block of a frame (gfx950).
+//
+// Restates the residual half of decode_and_reconstruct_block_inter / _intra
+// (dec/decode_block.c:48-120): dequantize (common/common_block.c:132-146),
+// then the 2-D inverse transform (common/transform.c:432-518: pass 1 over the
+// coded columns with clip16((s + 64) >> 7) between passes, pass 2 with
+// clip16((s + 2048) >> 12); 64x64 = 32-point transform + 2x2 replication,
+// :496-517).  The residual does not depend on any neighbour, so it runs for
+// the whole frame before prediction: one 64-lane workgroup per (CU,
+// component); the result goes to the frame's int16 residual planes (Y W x H,
+// then U and V W/2 x H/2), where k_recon adds it to inter predictions and
+// k_intra to intra ones.
+//
+// Only the low-frequency q x q corner (q = min(N,16)) can be coded
+// (common/transform.c:309-327), so pass 1 runs over q columns and pass 2 over
+// q terms: the coded tile is the whole input.
+#include "common.h"
+
+// 32-point basis (g*mat_hevc, common/transform.c:41-245) as a constant table.
+struct Dct32Table {
+  int8_t v[1024];
+  constexpr Dct32Table() : v() {
+    const int c[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                       61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+    for (int k = 0; k < 32; k++)
+      for (int n = 0; n < 32; n++) {
+        int e;
+        if (k == 0) e = 64;
+        else {
+          int t = (k * (2 * n + 1)) & 127;
+          e = t <= 32 ? c[t] : (t <= 64 ? -c[64 - t] : (t <= 96 ? -c[t - 64] : c[128 - t]));
+        }
+        v[k * 32 + n] = (int8_t)e;
+      }
+  }
+};
+__constant__ Dct32Table g_dct32 = Dct32Table();
+
+struct ResidLds {
+  int8_t M[1024];
+  int16_t D[256];      // dequantised q x q tile
+  int16_t T[16 * 32];  // pass-1 output [k][y']
+};
+
+__device__ __forceinline__ int sx8(int w, int i) { return __builtin_amdgcn_sbfe(w, 8 * i, 8); }
+
+// One TU across the wave; writes the n x n (x2 replicated for 64) residual
+// at `out` (row stride `ostride` int16).
+__device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int ntu, int qp, int16_t *__restrict__ out,
+                           int ostride) {
+  const int lane = threadIdx.x;
+  const int rep = ntu == 64, n = rep ? 32 : ntu, q = n < 16 ? n : 16;
+  const int step = 32 / n;
+  const int lshift = qp / 6, scale = dequant_scale(qp % 6);
+  const int rshift = ilog2i(ntu) - 1, add = 1 << (rshift - 1);
+  for (int e = lane; e < q * q; e += 64)
+    L.D[e] = (int16_t)wrap16(((coef[e] * scale) * (1 << lshift) + add) >> rshift);  // int16 store, :143
+  wave_lds_sync();
+  for (int e = lane; e < q * n; e += 64) {  // pass 1, transform.c:455-463
+    const int k = e / n, yp = e - k * n;
+    int s = 0;
+    for (int m = 0; m < q; m++) s += (int)L.M[(m * step) * 32 + yp] * (int)L.D[m * q + k];
+    L.T[k * n + yp] = (int16_t)clip16((s + 64) >> 7);
+  }
+  wave_lds_sync();
+  for (int e = lane; e < (n * n) >> 2; e += 64) {  // pass 2, four columns per lane, :466-484
+    const int yp = (e << 2) / n, xp = (e << 2) - yp * n;
+    int r[4] = {0, 0, 0, 0};
+    for (int k = 0; k < q; k++) {
+      const int t = L.T[k * n + yp];
+      const int mw = *(const int *)&L.M[(k * step) * 32 + xp];
+#pragma unroll
+      for (int j = 0; j < 4; j++) r[j] += sx8(mw, j) * t;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) r[j] = clip16((r[j] + 2048) >> 12);
+    if (rep) {  // 2x2 replication
+      uint4 w;
+      w.x = (uint32_t)(r[0] & 0xffff) * 0x10001u;
+      w.y = (uint32_t)(r[1] & 0xffff) * 0x10001u;
+      w.z = (uint32_t)(r[2] & 0xffff) * 0x10001u;
+      w.w = (uint32_t)(r[3] & 0xffff) * 0x10001u;
+      *(uint4 *)(out + (long long)(2 * yp) * ostride + 2 * xp) = w;
+      *(uint4 *)(out + (long long)(2 * yp + 1) * ostride + 2 * xp) = w;
+    } else {
+      uint2 w;
+      w.x = (uint32_t)(r[0] & 0xffff) | ((uint32_t)r[1] << 16);
+      w.y = (uint32_t)(r[2] & 0xffff) | ((uint32_t)r[3] << 16);
+      *(uint2 *)(out + (long long)yp * ostride + xp) = w;
+    }
+  }
+  wave_lds_sync();  // the next TU rewrites D and T
+}
+
+__global__ __launch_bounds__(64) void k_resid(const thor_block_t *__restrict__ blk, const int16_t *__restrict__ coeffs,
+                                              int16_t *__restrict__ resid, int W, int H) {
+  __shared__ ResidLds L;
+  const int lane = threadIdx.x;
+  const thor_block_t &B = blk[blockIdx.x];
+  const int c = blockIdx.y;
+  const int mode = B.mode, cmask = B.coeff_mask;
+  if (mode == M_SKIP || !((cmask >> c) & 1)) return;
+  *(uint4 *)&L.M[16 * lane] = *(const uint4 *)&g_dct32.v[16 * lane];
+  const int S = B.size, tb = B.tb_split != 0;
+  const int size = c ? S >> 1 : S;
+  const int tbc = c ? (tb && S > 8) : tb;  // chroma of an 8x8 CU is not split, dec/decode_block.c:449-450
+  const int ntu = tbc ? size >> 1 : size;
+  const int nt = ntu == 64 ? 32 : ntu, q = nt < 16 ? nt : 16;
+  const int qp = c ? chroma_qp(B.qp) : B.qp;
+  const int pw = c ? W >> 1 : W;
+  const int py = c ? B.ypos >> 1 : B.ypos, px = c ? B.xpos >> 1 : B.xpos;
+  int16_t *plane = resid + (c == 0 ? 0 : (long long)W * H + (c == 2 ? (long long)(W >> 1) * (H >> 1) : 0));
+  wave_lds_sync();
+  for (int t = 0; t < (tbc ? 4 : 1); t++) {  // tb-split quarters in raster order, :101-102
+    const int oy = (t >> 1) * ntu, ox = (t & 1) * ntu;
+    tu_inverse(L, coeffs + B.coeff_off[c] + t * q * q, ntu, qp, plane + (long long)(py + oy) * pw + px + ox, pw);
+  }
+}

@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libthor_amd.so")
+LIB_PATH = os.environ.get("THOR_AMD_LIB") or os.path.join(HERE, "libthor_amd.so")
 
 _lib = None
 

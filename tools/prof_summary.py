@@ -49,6 +49,13 @@ def main():
              "%-24s %8s %14s %12s %8s" % ("kernel", "calls", "total_us", "avg_us", "pct")]
     for name, calls, tot, avg, pct in rows:
         lines.append("%-24s %8d %14.1f %12.3f %8.2f" % (short(name), calls, tot, avg, pct))
+    # per-dispatch durations of the last step (one launch per frame, 8 frames)
+    c = sqlite3.connect(os.path.join(d, "trace", "run_results.db"))
+    seq = [(short(n), dur / 1e3) for n, dur in c.execute("select name, duration from kernels order by start")]
+    lines.append("# last step, per frame (us): I P P P P P P P")
+    for k in sorted({n for n, _ in seq if n.startswith("k_")}):
+        ds = [v for n, v in seq if n == k][-8:]
+        lines.append("%-24s %s" % (k, " ".join("%8.1f" % v for v in ds)))
     open(os.path.join(out, "%s_rocprof_stats.txt" % tag), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
     traffic = {"tag": tag, "correction": "fetch_bytes = FETCH_SIZE_KiB*1024*2 (gfx950 half-count); "
