@@ -295,7 +295,7 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     StageMark m(d, ST_INTER);
     k_resid<<<dim3(nblocks, 3), 64, 0, st>>>(blocks, coeffs, d->resid, W, H);
     HIPCHK(hipGetLastError());
-    k_recon<<<8 * ((nsb + 7) / 8), 64, 0, st>>>(f, blocks, coeffs, d->cellmap, d->resid, d->dbg_recon);
+    k_recon<<<8 * ((2 * nsb + 7) / 8), 64, 0, st>>>(f, blocks, coeffs, d->cellmap, d->resid, d->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   if (n_intra > 0) {

@@ -1,4 +1,4 @@
-// k_recon: inter reconstruction of one 64x64 superblock per wavefront (gfx950).
+// k_recon: inter reconstruction, one wavefront per half (64x32) superblock (gfx950).
 //
 // Restates, for every non-intra CU of a frame, decode_block's prediction
 // (dec/decode_block.c:213-451: SKIP / MERGE / INTER / BIPRED; INTER and BIPRED
@@ -8,31 +8,33 @@
 // (common/common_block.c:148-156) with the residual k_resid (resid.hip) left in
 // the int16 residual planes (dequantize + inverse_transform, :90-120).
 //
-// One wave per SB, SBs mapped XCD-major (a band of consecutive SBs per XCD, so
-// neighbouring SBs share their reference rows in that XCD's L2).
-//  P0  lane = 8x8 unit: resolve its four 4x4 cells' MC parameters -- quarter MV
+// One wave per half SB (rows 0-31 or 32-63), mapped XCD-major (a band of
+// consecutive half SBs per XCD, so neighbours share their reference rows in
+// that XCD's L2).
+//  P0  lane = one 4-row half of an 8x8 unit: resolve its 4x4 cells' MC parameters -- quarter MV
 //      with the `sign` negation (inter_prediction.c:78-79, :125-126),
 //      reference slot, bi-pred, coded residual per component -- into LDS.
-//  P1  the SB is two jobs (rows 0-31, 32-63; x2 with a bi-pred second pass).
+//  P1  one pass (two with bi-pred: mv1 / slot1 of the bi-pred cells).
 //      Work item = (lane, segment): lane = 4-px luma column x 8 rows + 2-px
 //      chroma column x 4 rows per plane; segment = one 4x4 cell row (the MV may
 //      change every 4 luma rows: 8x8 INTER quarters).  A job takes the distinct
 //      (mv, slot) keys of its items one at a time (one key per job in the
 //      common case): that key's displaced reference window (37 x 96 B luma,
 //      2 x 19 x 64 B chroma) is staged HBM -> LDS with 16-byte loads, all in
-//      flight at once, biased (^0x80) on the way; the next job's first window
-//      is already in flight while this job filters (double-buffered).
+//      flight at once, biased (^0x80) on the way.
 //      Horizontal taps: v_dot4_i32_i8 on the (p - 128) bytes (the bias folds
 //      into the rounding constant); vertical taps: v_dot2_i32_i16 on pairs of
 //      rows of the int16 horizontal sums.  Taps are uniform per key.  The (2,2)
-//      centre filter (inter_prediction.c:145-157) is the sum of two separable
-//      filters, [0 1 1 0]x[1 1 1 1] + [1 1 1 1]x[0 1 1 0].
-//  P2  per half: residual add where the cell's CU carries coefficients, then
+//      centre filter (inter_prediction.c:145-157) is u_i + u_j, u = [0 1 1 0]:
+//      a 4-tap and a 2-tap horizontal sum per row, packed, four v_dot2 down.
+//  P2  residual add where the cell's CU carries coefficients, then
 //      the lane's rows go to the frame (64 contiguous bytes per 16 lanes/row).
 //
 // Separable order: the reference computes the vertical taps first into int32
 // and the horizontal second; the sum is the same exact integer either way.
 #include <stddef.h>
+
+#include <type_traits>
 
 #include "common.h"
 
@@ -55,12 +57,13 @@ struct RefWin {
   uint8_t v[WC_R * WC_P];
 };
 
+#define HALF_CELLS 128  // 8 cell rows x 16 cells: one half SB
 struct ReconLds {
-  RefWin win[2];            // double buffer
-  int mv0[SB_CELLS];        // per 4x4 cell: (mvx, mvy) int16 pair, sign applied
-  int mv1[SB_CELLS];
-  unsigned meta[SB_CELLS];  // slot0 | slot1 << 8 | ACT | BI | RES(c)
-  int8_t lut[128];          // display frame number & 127 -> ring slot
+  RefWin win;
+  int mv0[HALF_CELLS];        // per 4x4 cell: (mvx, mvy) int16 pair, sign applied
+  int mv1[HALF_CELLS];
+  unsigned meta[HALF_CELLS];  // slot0 | slot1 << 8 | ACT | BI | RES(c)
+  int8_t lut[128];            // display frame number & 127 -> ring slot
 };
 
 __device__ __forceinline__ int tap8(int w, int i) { return __builtin_amdgcn_sbfe(w, 8 * i, 8); }
@@ -88,15 +91,8 @@ struct TapTables {
 };
 __constant__ TapTables g_taps = TapTables();
 
-// Centre (2,2) terms as 6-tap words, scaled by 16 so that the product of the
-// two 1-D sums is 256 * the 4x4 kernel weight: (S + 8) >> 4 == (256 S + 2048) >> 12.
-#define CTR_A0 0x10101000  // [0,16,16,16 | 16,0]
-#define CTR_A1 0x00000010
-#define CTR_B0 0x10100000  // [0,0,16,16 | 0,0]
-#define CTR_B1 0x00000000
-
 // Rounding constant of the 2-D filters with the (p - 128) bias folded in:
-// 2048 + 128 * 64 * 64 (every tap set sums to 64; for the centre, 64*32 + 32*64).
+// 2048 + 128 * 64 * 64 (every tap set sums to 64).
 #define MC_RND (2048 + 524288)
 
 // Horizontal sums H' = sum t_k (p_k - 128) fit int16 (|H'| <= 128 * 94 for
@@ -143,28 +139,74 @@ __device__ __forceinline__ uint32_t avg_bytes(uint32_t a, uint32_t b) {  // (p0 
 }
 
 
-// Luma rows R0 .. R0+N-1 of the lane's 8-row strip from the staged window.
-// `wrow` = window row of strip row -2, `wb` = window byte of column -2.
-// Vertical taps as int16 pairs v01/v23/v45; CTR adds the centre's term B
-// (horizontal [0,0,16,16,0,0], vertical [0,16,16,16,16,0]).
-template <int R0, int N, bool CTR>
-__device__ __forceinline__ void luma_rows(const uint8_t *__restrict__ win, int wrow, int wb, int tw0, int tw1, int v01,
-                                          int v23, int v45, uint32_t out[8]) {
-  int ha[6][4], hb[6][4];   // H' of the last rows (ring by strip row)
-  uint32_t pa[6][4], pb[6][4];  // P(r) = (H'[r], H'[r+1])
-  const uint32_t sh = (uint32_t)(wb & 3);
-  const uint8_t *base = win + (wb & ~3);
-  auto hrow = [&](int r) {  // strip row r -> ring, and P(r-1)
-    const uint32_t *p = (const uint32_t *)(base + (wrow + r + 2) * WL_P);
-    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
-    luma_h4(d0, d1, d2, sh, tw0, tw1, ha[(r + 6) % 6]);
-    if (CTR) luma_h4(d0, d1, d2, sh, CTR_B0, CTR_B1, hb[(r + 6) % 6]);
-    if (r > R0 - 2) {
+// The uniform filter of one key.
+struct Key {
+  int mv, slot;
+  int fx, fy, cfx, cfy;  // luma quarter / chroma eighth fractions
+  int dx, dy, cdx, cdy;  // integer displacements
+};
+// Row sources.  A staged LDS window (bytes already biased ^0x80), or the
+// reference ring directly (waves whose items need more than one window): the
+// direct source prefetches every row of a call before any arithmetic.
+struct LdsLuma {
+  static constexpr bool PF = false;
+  const uint8_t *base;  // window byte of strip row -2, column -2 (dword aligned)
+  __device__ __forceinline__ void get(int r, uint32_t d[3]) const {
+    const uint32_t *p = (const uint32_t *)(base + (r + 2) * WL_P);
+    d[0] = p[0]; d[1] = p[1]; d[2] = p[2];
+  }
+};
+struct GlobLuma {
+  static constexpr bool PF = true;
+  __amdgpu_buffer_rsrc_t ring;
+  int o, stride;  // ring offset of strip row 0, column -2 (dword aligned)
+  __device__ __forceinline__ void get(int r, uint32_t d[3]) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(ring, o + r * stride, 0, 0);
+    d[0] = v[0] ^ 0x80808080u; d[1] = v[1] ^ 0x80808080u; d[2] = v[2] ^ 0x80808080u;
+  }
+};
+struct LdsChroma {
+  static constexpr bool PF = false;
+  const uint8_t *u, *v;  // window byte of strip row -1, column -1 (dword aligned)
+  __device__ __forceinline__ void get(int r, uint32_t du[2], uint32_t dv[2]) const {
+    const uint32_t *pu = (const uint32_t *)(u + (r + 1) * WC_P), *pv = (const uint32_t *)(v + (r + 1) * WC_P);
+    du[0] = pu[0]; du[1] = pu[1]; dv[0] = pv[0]; dv[1] = pv[1];
+  }
+};
+struct GlobChroma {
+  static constexpr bool PF = true;
+  __amdgpu_buffer_rsrc_t ring;
+  int o, uvd, stride;  // ring offset (U) of strip row 0, column -1 (dword aligned)
+  __device__ __forceinline__ void get(int r, uint32_t du[2], uint32_t dv[2]) const {
+    const auto a = __builtin_amdgcn_raw_buffer_load_b64(ring, o + r * stride, 0, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b64(ring, o + uvd + r * stride, 0, 0);
+    du[0] = a[0] ^ 0x80808080u; du[1] = a[1] ^ 0x80808080u; dv[0] = b[0] ^ 0x80808080u; dv[1] = b[1] ^ 0x80808080u;
+  }
+};
+
+// Luma rows R0 .. R0+N-1 of the lane's 8-row strip; `sh` = byte offset of
+// column -2 inside the fetched dwords.  Vertical taps as int16 pairs.
+template <int R0, int N, class Src>
+__device__ __forceinline__ void luma_rows(const Src &src, uint32_t sh, int tw0, int tw1, int v01, int v23, int v45,
+                                          uint32_t out[8]) {
+  constexpr int NR = N + 5;
+  uint32_t pre[Src::PF ? NR : 1][3];
+  if (Src::PF) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        pa[(r + 5) % 6][j] = pack_lo16(ha[(r + 5) % 6][j], ha[(r + 6) % 6][j]);
-        if (CTR) pb[(r + 5) % 6][j] = pack_lo16(hb[(r + 5) % 6][j], hb[(r + 6) % 6][j]);
-      }
+    for (int k = 0; k < NR; k++) src.get(R0 - 2 + k, pre[Src::PF ? k : 0]);
+  }
+  int hp[4];                // H' of the previous row
+  uint32_t pa[6][4];        // P(r) = (H'[r], H'[r+1]), ring by strip row
+  auto hrow = [&](int r) {  // strip row r -> P(r-1)
+    uint32_t d[3];
+    if (Src::PF) { d[0] = pre[Src::PF ? r - R0 + 2 : 0][0]; d[1] = pre[Src::PF ? r - R0 + 2 : 0][1]; d[2] = pre[Src::PF ? r - R0 + 2 : 0][2]; }
+    else src.get(r, d);
+    int hc[4];
+    luma_h4(d[0], d[1], d[2], sh, tw0, tw1, hc);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (r > R0 - 2) pa[(r + 5) % 6][j] = pack_lo16(hp[j], hc[j]);
+      hp[j] = hc[j];
     }
   };
 #pragma unroll
@@ -178,41 +220,93 @@ __device__ __forceinline__ void luma_rows(const uint8_t *__restrict__ win, int w
       int acc = dot2(pa[(i - 2 + 6) % 6][j], v01, MC_RND);
       acc = dot2(pa[(i + 6) % 6][j], v23, acc);
       acc = dot2(pa[(i + 2 + 6) % 6][j], v45, acc);
-      if (CTR) {
-        acc = dot2(pb[(i - 2 + 6) % 6][j], 16 << 16, acc);
-        acc = dot2(pb[(i + 6) % 6][j], 16 | (16 << 16), acc);
-        acc = dot2(pb[(i + 2 + 6) % 6][j], 16, acc);
-      }
       o |= mc_pack(acc, j);
     }
     out[i] = o;
   }
 }
 
+// The (2,2) centre position (inter_prediction.c:145-157): kernel
+// K[i][j] = u_i + u_j over rows / columns -1..2, u = [0 1 1 0], so per output
+// row o: S = Hv(o) + Hv(o+1) + Hu(o-1) + Hu(o) + Hu(o+1) + Hu(o+2) with Hv the
+// 4-tap [1 1 1 1] and Hu the 2-tap [1 1] horizontal sums.  Q(r) = (Hv, Hu)
+// packed int16 -> four v_dot2 per pixel; (S + 8) >> 4 with the bias
+// 128 * 16 = 2048 folded in.
+template <int R0, int N, class Src>
+__device__ __forceinline__ void luma_rows_ctr(const Src &src, uint32_t sh, uint32_t out[8]) {
+  constexpr int NR = N + 3;
+  uint32_t pre[Src::PF ? NR : 1][3];
+  if (Src::PF) {
+#pragma unroll
+    for (int k = 0; k < NR; k++) src.get(R0 - 1 + k, pre[Src::PF ? k : 0]);
+  }
+  uint32_t q[6][4];
+  auto hrow = [&](int r) {
+    uint32_t d[3];
+    if (Src::PF) { d[0] = pre[Src::PF ? r - R0 + 1 : 0][0]; d[1] = pre[Src::PF ? r - R0 + 1 : 0][1]; d[2] = pre[Src::PF ? r - R0 + 1 : 0][2]; }
+    else src.get(r, d);
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh), e1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t lo = j ? __builtin_amdgcn_alignbyte(e1, e0, j) : e0;  // bytes at offsets -2..1
+      const uint32_t hi = j ? __builtin_amdgcn_alignbyte(e1, e1, j) : e1;  // byte 0 at offset 2
+      const int hv = dot4(hi, 0x00000001, dot4z(lo, 0x01010100));
+      const int hu = dot4z(lo, 0x01010000);
+      q[(r + 6) % 6][j] = pack_lo16(hv, hu);
+    }
+  };
+#pragma unroll
+  for (int r = R0 - 1; r <= R0 + 2; r++) hrow(r);
+#pragma unroll
+  for (int i = R0; i < R0 + N; i++) {
+    if (i > R0) hrow(i + 2);
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int acc = dot2(q[(i - 1 + 6) % 6][j], 0x00010000, 2048 + 8);
+      acc = dot2(q[(i + 6) % 6][j], 0x00010001, acc);
+      acc = dot2(q[(i + 1 + 6) % 6][j], 0x00010001, acc);
+      acc = dot2(q[(i + 2 + 6) % 6][j], 0x00010000, acc);
+      o |= put_byte(clip255(acc >> 4), j);
+    }
+    out[i] = o;
+  }
+}
+
 // Chroma rows R0 .. R0+N-1 (of 4) of the lane's 2-px column, U and V.
-template <int R0, int N>
-__device__ __forceinline__ void chroma_rows(const RefWin &w, int wrow, int wb, int tw, int v01, int v23,
-                                            uint32_t out[4]) {
-  int hu[4][2], hv[4][2];
-  uint32_t pu[4][2], pv[4][2];
-  const uint32_t sh = (uint32_t)(wb & 3);
-  auto h2 = [&](const uint8_t *p, int h[2]) {
-    const uint32_t d0 = ((const uint32_t *)p)[0], d1 = ((const uint32_t *)p)[1];
-    const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    const uint32_t e1 = sh == 3 ? d1 : __builtin_amdgcn_alignbyte(d1, d0, sh + 1);
+template <int R0, int N, class Src>
+__device__ __forceinline__ void chroma_rows(const Src &src, uint32_t sh, int tw, int v01, int v23, uint32_t out[4]) {
+  constexpr int NR = N + 3;
+  uint32_t preu[Src::PF ? NR : 1][2], prev_[Src::PF ? NR : 1][2];
+  if (Src::PF) {
+#pragma unroll
+    for (int k = 0; k < NR; k++) src.get(R0 - 1 + k, preu[Src::PF ? k : 0], prev_[Src::PF ? k : 0]);
+  }
+  int pu_prev[2], pv_prev[2];
+  uint32_t pu[4][2], pv[4][2];  // P(r) = (H'[r], H'[r+1]) per plane
+  auto h2 = [&](const uint32_t d[2], int h[2]) {
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+    const uint32_t e1 = sh == 3 ? d[1] : __builtin_amdgcn_alignbyte(d[1], d[0], sh + 1);
     h[0] = dot4z(e0, tw);
     h[1] = dot4z(e1, tw);
   };
   auto hrow = [&](int r) {
-    const int o = (wrow + r + 1) * WC_P + (wb & ~3);
-    h2(w.u + o, hu[(r + 4) % 4]);
-    h2(w.v + o, hv[(r + 4) % 4]);
-    if (r > R0 - 1) {
+    uint32_t du[2], dv[2];
+    if (Src::PF) {
+      const int k = Src::PF ? r - R0 + 1 : 0;
+      du[0] = preu[k][0]; du[1] = preu[k][1]; dv[0] = prev_[k][0]; dv[1] = prev_[k][1];
+    } else src.get(r, du, dv);
+    int hu[2], hv[2];
+    h2(du, hu);
+    h2(dv, hv);
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
-        pu[(r + 3) % 4][j] = pack_lo16(hu[(r + 3) % 4][j], hu[(r + 4) % 4][j]);
-        pv[(r + 3) % 4][j] = pack_lo16(hv[(r + 3) % 4][j], hv[(r + 4) % 4][j]);
+    for (int j = 0; j < 2; j++) {
+      if (r > R0 - 1) {
+        pu[(r + 3) % 4][j] = pack_lo16(pu_prev[j], hu[j]);
+        pv[(r + 3) % 4][j] = pack_lo16(pv_prev[j], hv[j]);
       }
+      pu_prev[j] = hu[j];
+      pv_prev[j] = hv[j];
     }
   };
 #pragma unroll
@@ -232,12 +326,41 @@ __device__ __forceinline__ void chroma_rows(const RefWin &w, int wrow, int wb, i
   }
 }
 
-// The uniform filter of one key.
-struct Key {
-  int mv, slot;
-  int fx, fy, cfx, cfy;  // luma quarter / chroma eighth fractions
-  int dx, dy, cdx, cdy;  // integer displacements
-};
+// The luma / chroma calls of one segment set: both segments (rows 0-7 / 0-3)
+// when they share the key, else each on its own.
+template <class LSrc, class CSrc>
+__device__ __forceinline__ void filter_items(bool m0, bool m1, const LSrc &l0, const LSrc &l1, uint32_t lsh0, uint32_t lsh1,
+                                             const CSrc &c0, const CSrc &c1, uint32_t csh0, uint32_t csh1,
+                                             const Key &K0, const Key &K1, bool same, int bipred, uint32_t ty[8],
+                                             uint32_t tc[4]) {
+  auto luma = [&](auto r0c, auto nc, const LSrc &src, uint32_t sh, const Key &K) {
+    constexpr int R0 = decltype(r0c)::value, N = decltype(nc)::value;
+    if (K.fx == 2 && K.fy == 2) luma_rows_ctr<R0, N>(src, sh, ty);
+    else {
+      int v01, v23, v45;
+      tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45);
+      luma_rows<R0, N>(src, sh, g_taps.luma[bipred][K.fx][0], g_taps.luma[bipred][K.fx][1], v01, v23, v45, ty);
+    }
+  };
+  auto chroma = [&](auto r0c, auto nc, const CSrc &src, uint32_t sh, const Key &K) {
+    constexpr int R0 = decltype(r0c)::value, N = decltype(nc)::value;
+    const int cvt = g_taps.chroma[K.cfy];
+    chroma_rows<R0, N>(src, sh, g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
+                       (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  if (m0 && m1 && same) {
+    luma(I0{}, I8{}, l0, lsh0, K0);
+    chroma(I0{}, I4{}, c0, csh0, K0);
+  } else {
+    if (m0) { luma(I0{}, I4{}, l0, lsh0, K0); chroma(I0{}, I2{}, c0, csh0, K0); }
+    if (m1) { luma(I4{}, I4{}, l1, lsh1, K1); chroma(I2{}, I2{}, c1, csh1, K1); }
+  }
+}
+
 __device__ __forceinline__ Key make_key(int mv, int slot) {
   Key K;
   K.mv = mv;
@@ -292,18 +415,18 @@ __device__ __forceinline__ void win_commit(const WinLoad &W, RefWin &w) {
     }
 }
 
-// A job's items of this lane: segment s of half h (cell rows 8h + 2gr + s).
+// A pass's items of this lane: segment s (cell row 2gr + s of the half).
 struct Items {
   unsigned pend;
   int mv[2], slot[2];
 };
-__device__ __forceinline__ Items job_items(const ReconLds &L, int h, int pass) {
+__device__ __forceinline__ Items job_items(const ReconLds &L, int pass) {
   const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
   Items it;
   it.pend = 0;
 #pragma unroll
   for (int s = 0; s < 2; s++) {
-    const int cell = (8 * h + 2 * gr + s) * 16 + cc;
+    const int cell = (2 * gr + s) * 16 + cc;
     const unsigned meta = L.meta[cell];
     const bool act = (meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI));
     it.mv[s] = pass ? L.mv1[cell] : L.mv0[cell];
@@ -329,35 +452,37 @@ __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bi
   const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
   const bool m0 = (it.pend & 1) && it.mv[0] == K.mv && it.slot[0] == K.slot;
   const bool m1 = (it.pend & 2) && it.mv[1] == K.mv && it.slot[1] == K.slot;
-  const bool ctr = K.fx == 2 && K.fy == 2;
-  const int tw0 = ctr ? CTR_A0 : g_taps.luma[bipred][K.fx][0], tw1 = ctr ? CTR_A1 : g_taps.luma[bipred][K.fx][1];
-  int v01, v23, v45;
-  tap_pairs6(ctr ? CTR_B0 : g_taps.luma[bipred][K.fy][0], ctr ? CTR_B1 : g_taps.luma[bipred][K.fy][1], v01, v23, v45);
   const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
-  const int lwr = 8 * gr;
-  if (ctr) {
-    if (m0 && m1) luma_rows<0, 8, true>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
-    else {
-      if (m0) luma_rows<0, 4, true>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
-      if (m1) luma_rows<4, 4, true>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
-    }
-  } else {
-    if (m0 && m1) luma_rows<0, 8, false>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
-    else {
-      if (m0) luma_rows<0, 4, false>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
-      if (m1) luma_rows<4, 4, false>(w.y, lwr, lwb, tw0, tw1, v01, v23, v45, ty);
-    }
-  }
-  const int ctw = g_taps.chroma[K.cfx], cvt = g_taps.chroma[K.cfy];
-  const int c01 = (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16), c23 = (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16);
   const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
-  const int cwr = 4 * gr;
-  if (m0 && m1) chroma_rows<0, 4>(w, cwr, cwb, ctw, c01, c23, tc);
-  else {
-    if (m0) chroma_rows<0, 2>(w, cwr, cwb, ctw, c01, c23, tc);
-    if (m1) chroma_rows<2, 2>(w, cwr, cwb, ctw, c01, c23, tc);
-  }
+  const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
+  const LdsChroma c{w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3)};
+  filter_items(m0, m1, l, l, (uint32_t)(lwb & 3), (uint32_t)(lwb & 3), c, c, (uint32_t)(cwb & 3), (uint32_t)(cwb & 3),
+               K, K, true, bipred, ty, tc);
   it.pend &= ~((m0 ? 1u : 0u) | (m1 ? 2u : 0u));
+}
+
+// Waves whose items need several keys: every item straight from the ring,
+// per-lane keys (one pass, no per-key staging round trips).
+__device__ __forceinline__ void filter_direct(const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, int bipred, int x0,
+                                              int y0, Items &it, uint32_t ty[8], uint32_t tc[4]) {
+  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const Key K0 = make_key(it.mv[0], it.slot[0]), K1 = make_key(it.mv[1], it.slot[1]);
+  const bool m0 = it.pend & 1, m1 = (it.pend >> 1) & 1;
+  const bool same = it.mv[0] == it.mv[1] && it.slot[0] == it.slot[1];
+  const int uvd = (int)(f.offv - f.offu);
+  auto lo = [&](const Key &K) {
+    return (int)((long long)K.slot * f.slot_bytes + f.offy + (long long)(y0 + 8 * gr + K.dy) * f.sy + x0 + 4 * cc - 2 + K.dx);
+  };
+  auto co = [&](const Key &K) {
+    return (int)((long long)K.slot * f.slot_bytes + f.offu + (long long)((y0 >> 1) + 4 * gr + K.cdy) * f.sc +
+                 (x0 >> 1) + 2 * cc - 1 + K.cdx);
+  };
+  const int l0 = lo(K0), l1 = lo(K1), c0 = co(K0), c1 = co(K1);
+  const GlobLuma g0{ring, l0 & ~3, f.sy}, g1{ring, l1 & ~3, f.sy};
+  const GlobChroma h0{ring, c0 & ~3, uvd, f.sc}, h1{ring, c1 & ~3, uvd, f.sc};
+  filter_items(m0, m1, g0, g1, (uint32_t)(l0 & 3), (uint32_t)(l1 & 3), h0, h1, (uint32_t)(c0 & 3), (uint32_t)(c1 & 3), K0,
+               K1, same, bipred, ty, tc);
+  it.pend = 0;
 }
 
 __device__ __forceinline__ uint32_t add_res4(uint32_t p, const int16_t *__restrict__ r) {
@@ -391,12 +516,13 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
     const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
     stamp[7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
   }
-  const int sbw = (f.W + 63) >> 6, sbh = (f.H + 63) >> 6, nsb = sbw * sbh;
-  // XCD-major SB order: workgroup b runs on XCD b % 8 (round-robin dispatch);
-  // give each XCD a contiguous band of SBs.  Speed only, never correctness.
-  const int per = (nsb + 7) >> 3;
-  const int sb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (sb >= nsb) return;
+  const int sbw = (f.W + 63) >> 6, sbh = (f.H + 63) >> 6, nh = 2 * sbw * sbh;
+  // XCD-major order of half SBs: workgroup b runs on XCD b % 8 (round-robin
+  // dispatch); each XCD gets a contiguous band.  Speed only, never correctness.
+  const int per = (nh + 7) >> 3;
+  const int hsb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (hsb >= nh) return;
+  const int sb = hsb >> 1, h = hsb & 1;
   const int sby = sb / sbw, sbx = sb - sby * sbw;
   const int cs = f.W >> 2;
 
@@ -405,13 +531,15 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
     *(int *)&L.lut[4 * lane] =
         ((const int *)((const char *)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(FrameCtx, slot_lut)))[lane];
 
-  // ---- P0: lane = 8x8 unit ----
-  const int ur = lane >> 3, uc = lane & 7;
-  const int uy = sby * 64 + 8 * ur, ux = sbx * 64 + 8 * uc;
+  // ---- P0: lane = cell row cr of 8x8 unit uu of the half ----
+  const int uu = lane >> 1, cr = lane & 1;
+  const int ur = uu >> 3, uc = uu & 7;
+  const int uy = sby * 64 + 32 * h + 8 * ur, ux = sbx * 64 + 8 * uc;
   int b = -1;
   if (uy < f.H && ux < f.W) b = cellmap[(uy >> 2) * cs + (ux >> 2)];
   bool inter = false, bi_any = false;
   wave_lds_sync();  // lut
+  const int lrow = 2 * ur + cr;  // cell row inside the half
   if (b >= 0) {
     const thor_block_t &B = blk[b];
     const int mode = B.mode, S = B.size, by = B.ypos, bx = B.xpos;
@@ -422,15 +550,15 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
     const int sg1 = ref1 >= f.frame_num;
     const int s0 = L.lut[ref0 & 127], s1 = bi ? L.lut[ref1 & 127] : 0;
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int cy = uy + 4 * (c >> 1), cx = ux + 4 * (c & 1);
+    for (int c = 0; c < 2; c++) {
+      const int cy = uy + 4 * cr, cx = ux + 4 * c;
       bool act = mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0);
       if (mode == M_SKIP) act = act && cx < bx + B.bwidth && cy < by + B.bheight;
       const int q = (mode == M_INTER || mode == M_BIPRED) ? 2 * (cy - by >= (S >> 1)) + (cx - bx >= (S >> 1)) : 0;
       int m0x = B.mv0[2 * q], m0y = B.mv0[2 * q + 1], m1x = B.mv1[2 * q], m1y = B.mv1[2 * q + 1];
       if (sg0) { m0x = -m0x; m0y = -m0y; }
       if (sg1) { m1x = -m1x; m1y = -m1y; }
-      const int cell = (2 * ur + (c >> 1)) * 16 + 2 * uc + (c & 1);
+      const int cell = lrow * 16 + 2 * uc + c;
       L.mv0[cell] = (m0x & 0xffff) | (m0y << 16);
       L.mv1[cell] = bi ? ((m1x & 0xffff) | (m1y << 16)) : 0;
       L.meta[cell] = act ? ((unsigned)s0 | ((unsigned)(bi ? s1 : 0) << 8) | CELL_ACT | (bi ? CELL_BI : 0u) | resbits)
@@ -439,8 +567,8 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
       bi_any |= act && bi;
     }
   } else {
-#pragma unroll
-    for (int c = 0; c < 4; c++) L.meta[(2 * ur + (c >> 1)) * 16 + 2 * uc + (c & 1)] = 0;
+    L.meta[lrow * 16 + 2 * uc] = 0;
+    L.meta[lrow * 16 + 2 * uc + 1] = 0;
   }
   const bool any_inter = __ballot(inter) != 0, any_bi = __ballot(bi_any) != 0;
   wave_lds_sync();
@@ -450,90 +578,68 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
     return;
   }
 
-  // ---- P1 + P2: jobs (half h, pass p), the next job's first window in flight ----
+  // ---- P1: prediction (pass 0: mv0; pass 1: mv1 of the bi-pred cells) ----
   const __amdgpu_buffer_rsrc_t ring =  // one descriptor over the whole ring (< 2 GiB: 32-bit offsets)
       __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
-  const int npass = any_bi ? 2 : 1, njobs = 2 * npass;
-  const int x0 = sbx * 64, cc = lane & 15, gr = lane >> 4;
-  const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
-  Items it = job_items(L, 0, 0);
-  Key K;
-  bool have = first_key(it, K);
-  WinLoad cur;
-  if (have) win_issue(cur, f, ring, K, x0, sby * 64);
+  const int x0 = sbx * 64, y0 = sby * 64 + 32 * h, cc = lane & 15, gr = lane >> 4;
   uint32_t ly[8], lc[4], ty[8], tc[4];
-  for (int j = 0; j < njobs; j++) {
-    const int h = j / npass, pass = j % npass;
-    const int y0 = sby * 64 + 32 * h;
-    RefWin &w = L.win[j & 1];
-    // next job's first window: issued before this job filters
-    Items nit;
-    Key NK;
-    bool nhave = false;
-    WinLoad nxt;
-    if (j + 1 < njobs) {
-      nit = job_items(L, (j + 1) / npass, (j + 1) % npass);
-      nhave = first_key(nit, NK);
-      if (nhave) win_issue(nxt, f, ring, NK, x0, sby * 64 + 32 * ((j + 1) / npass));
-    }
-    if (have) {
-      win_commit(cur, w);
-      wave_lds_sync();
-      if (j == 0) STAMP(4);
-      filter_key(w, K, f.bipred, x0, it, ty, tc);
-      // further keys of this job (rare: CU edges and 8x8 INTER quarters inside the half)
-      Key K2;
-      while (first_key(it, K2)) {
-        wave_lds_sync();  // everyone is done reading the window
-        WinLoad tmp;
-        win_issue(tmp, f, ring, K2, x0, y0);
-        win_commit(tmp, w);
+  for (int pass = 0; pass <= (int)any_bi; pass++) {
+    Items it = job_items(L, pass);
+    Key K;
+    if (first_key(it, K)) {
+      const bool m0 = (it.pend & 1) && it.mv[0] == K.mv && it.slot[0] == K.slot;
+      const bool m1 = (it.pend & 2) && it.mv[1] == K.mv && it.slot[1] == K.slot;
+      if (__ballot(it.pend != ((m0 ? 1u : 0u) | (m1 ? 2u : 0u))) == 0) {  // one key: one staged window
+        WinLoad W;
+        win_issue(W, f, ring, K, x0, y0);
+        win_commit(W, L.win);
         wave_lds_sync();
-        filter_key(w, K2, f.bipred, x0, it, ty, tc);
-      }
-      // merge: pass 0 result, or the truncating bi-pred average
-#pragma unroll
-      for (int s = 0; s < 2; s++) {
-        const unsigned meta = L.meta[(8 * h + 2 * gr + s) * 16 + cc];
-        if (!((meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI)))) continue;
-#pragma unroll
-        for (int i = 4 * s; i < 4 * s + 4; i++) ly[i] = pass ? avg_bytes(ly[i], ty[i]) : ty[i];
-#pragma unroll
-        for (int i = 2 * s; i < 2 * s + 2; i++) lc[i] = pass ? avg_bytes(lc[i], tc[i]) : tc[i];
+        if (pass == 0) STAMP(4);
+        filter_key(L.win, K, f.bipred, x0, it, ty, tc);
+      } else {
+        if (pass == 0) STAMP(4);
+        filter_direct(f, ring, f.bipred, x0, y0, it, ty, tc);
       }
     }
-    if (pass == npass - 1) {  // P2: residual + store of half h
-      const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
-      const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
+    // merge: pass 0 result, or the truncating bi-pred average
 #pragma unroll
-      for (int s = 0; s < 2; s++) {
-        const unsigned meta = L.meta[(8 * h + 2 * gr + s) * 16 + cc];
-        if (!(meta & CELL_ACT)) continue;
+    for (int s = 0; s < 2; s++) {
+      const unsigned meta = L.meta[(2 * gr + s) * 16 + cc];
+      if (!((meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI)))) continue;
 #pragma unroll
-        for (int i = 4 * s; i < 4 * s + 4; i++) {
-          const int y = yb + i;
-          uint32_t v = ly[i];
-          if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
-          *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
-        }
+      for (int i = 4 * s; i < 4 * s + 4; i++) ly[i] = pass ? avg_bytes(ly[i], ty[i]) : ty[i];
 #pragma unroll
-        for (int i = 2 * s; i < 2 * s + 2; i++) {
-          const int y = ycb + i;
-          uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
-          if (meta & CELL_RES(1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
-          if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
-          *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
-          *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
-        }
-      }
+      for (int i = 2 * s; i < 2 * s + 2; i++) lc[i] = pass ? avg_bytes(lc[i], tc[i]) : tc[i];
     }
-    wave_lds_sync();  // window j & 1 is rewritten by job j + 2
-    it = nit;
-    K = NK;
-    have = nhave;
-    cur = nxt;
+    wave_lds_sync();
   }
   STAMP(3);
+
+  // ---- P2: residual + store ----
+  const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
+  const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
+  const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const unsigned meta = L.meta[(2 * gr + s) * 16 + cc];
+    if (!(meta & CELL_ACT)) continue;
+#pragma unroll
+    for (int i = 4 * s; i < 4 * s + 4; i++) {
+      const int y = yb + i;
+      uint32_t v = ly[i];
+      if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
+      *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
+    }
+#pragma unroll
+    for (int i = 2 * s; i < 2 * s + 2; i++) {
+      const int y = ycb + i;
+      uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
+      if (meta & CELL_RES(1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
+      if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
+      *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
+      *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
+    }
+  }
   STAMP(5);
 #undef STAMP
 }

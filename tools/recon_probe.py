@@ -16,7 +16,7 @@ dec = GpuDecoder(seq)
 lib = L.load()
 lib.thor_dec_debug_recon.argtypes = [C.c_void_p, C.c_void_p]
 nsb = ((seq.width + 63) // 64) * ((seq.height + 63) // 64)
-nwg = 8 * ((nsb + 7) // 8)
+nwg = 8 * ((2 * nsb + 7) // 8)
 nbytes = nwg * 8 * 8
 buf = lib.thor_dev_alloc(nbytes)
 devs = [dec.upload(fr) for fr in frames]
@@ -58,6 +58,17 @@ for i, d in enumerate(devs):
     load = np.array([len(per[int(k)]) for k in key])
     for n in sorted(set(load.tolist())):
         print("     simds with %d waves: end p50 %.2f max %.2f (%d waves)" % (n, np.median(rel[load == n, 5]), rel[load == n, 5].max(), (load == n).sum()))
+    idx = np.nonzero(ok)[0]
+    per_x = (2 * nsb + 7) // 8
+    hsb = (idx & 7) * per_x + (idx >> 3)
+    sbw = (seq.width + 63) // 64
+    st = rel[:, 4] - rel[:, 2]
+    order = np.argsort(-st)[:12]
+    print("   slowest staging: (stage us, sby, sbx, half, xcc, end)",
+          [(round(st[k], 1), int(hsb[k] >> 1) // sbw, int(hsb[k] >> 1) % sbw, int(hsb[k] & 1), int(xcc[k]), round(rel[k, 5], 1)) for k in order])
+    order = np.argsort(-rel[:, 5])[:12]
+    print("   latest end: (end, sby, sbx, half, stage, filt)",
+          [(round(rel[k, 5], 1), int(hsb[k] >> 1) // sbw, int(hsb[k] >> 1) % sbw, int(hsb[k] & 1), round(st[k], 1), round(rel[k, 3] - rel[k, 4], 1)) for k in order])
     late = rel[:, 5] > np.percentile(rel[:, 5], 95)
     print("   late 5%%: xcc histogram %s" % np.bincount(xcc[late].astype(np.int64), minlength=8).tolist())
     if i >= 2:
