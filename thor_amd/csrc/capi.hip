@@ -306,7 +306,7 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     // full SB images only when inter CUs were reconstructed (their pixels are intra neighbours)
     int full_sb = n_intra < nblocks;
     // one 64-lane chain per (SB row, component)
-    k_intra<<<3 * nrows, 64, 0, st>>>(f, blocks, intra_list, n_intra, d->ctl, d->progress, nrows, d->dbg,
+    k_intra<<<3 * nrows, 256, 0, st>>>(f, blocks, intra_list, n_intra, d->ctl, d->progress, nrows, d->dbg,
                                       d->dbg_flags, full_sb, d->resid);
     HIPCHK(hipGetLastError());
   }
