@@ -59,7 +59,9 @@ struct thor_dec {
   int32_t *cellmap;
   unsigned *ctl;       // [0] intra row head, [1] timeout flag
   unsigned *progress;  // intra wavefront progress per (SB row, component)
-  int16_t *resid;      // intra residual planes (Y, U, V; int16), written by k_inter, read by k_intra
+  int16_t *resid;      // residual planes (Y, U, V; int16), written by k_resid, read by k_recon / k_intra
+  uint8_t *edge;       // SB-row edge rows (FrameCtx::edge)
+  int ewy, ewc;
   unsigned long long *dbg;  // optional per-row intra timing (debug)
   unsigned long long *dbg_recon;  // optional k_recon phase stamps (debug)
   int dbg_flags;
@@ -155,6 +157,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->stop_stage = 2;
   d->progress = nullptr;
   d->resid = nullptr;
+  d->edge = nullptr;
   d->dbg = nullptr;
   d->dbg_recon = nullptr;
   d->dbg_flags = 0;
@@ -172,6 +175,9 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
   ok = ok && hipMalloc(&d->resid, (size_t)W * H * 3) == hipSuccess;  // 1.5 px/luma px x 2 B
   ok = ok && hipMalloc(&d->progress, (size_t)3 * ((H + 63) / 64 + 1) * sizeof(unsigned)) == hipSuccess;
+  d->ewy = (W + 2 * EDGE_MARGIN + 15) & ~15;
+  d->ewc = (W / 2 + 2 * EDGE_MARGIN + 15) & ~15;
+  ok = ok && hipMalloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc)) == hipSuccess;
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
   if (!ok) {
     thor_dec_destroy(d);
@@ -182,16 +188,17 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
 
 void thor_dec_destroy(thor_dec_t *d) {
   if (!d) return;
-  hipSetDevice(d->device);
-  if (d->own_stream) hipStreamSynchronize(d->own_stream);
-  if (d->slots) hipFree(d->slots);
-  if (d->cellinfo) hipFree(d->cellinfo);
-  if (d->cellmap) hipFree(d->cellmap);
-  if (d->ctl) hipFree(d->ctl);
-  if (d->progress) hipFree(d->progress);
-  if (d->resid) hipFree(d->resid);
+  (void)hipSetDevice(d->device);
+  if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
+  if (d->slots) (void)hipFree(d->slots);
+  if (d->cellinfo) (void)hipFree(d->cellinfo);
+  if (d->cellmap) (void)hipFree(d->cellmap);
+  if (d->ctl) (void)hipFree(d->ctl);
+  if (d->progress) (void)hipFree(d->progress);
+  if (d->resid) (void)hipFree(d->resid);
+  if (d->edge) (void)hipFree(d->edge);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
-  if (d->own_stream) hipStreamDestroy(d->own_stream);
+  if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
   delete d;
 }
 
@@ -263,6 +270,10 @@ static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
     f.ref_slot[f.nref] = s;
     f.nref++;
   }
+  f.edge = d->edge;
+  f.ewy = d->ewy;
+  f.ewc = d->ewc;
+  f.nsbrows = (d->seq.height + 63) / 64;
   int8_t lut[128];
   memset(lut, -1, sizeof(lut));
   for (int r = 0; r < f.nref; r++) lut[f.ref_fnum[r] & 127] = (int8_t)f.ref_slot[r];
@@ -306,7 +317,7 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     // full SB images only when inter CUs were reconstructed (their pixels are intra neighbours)
     int full_sb = n_intra < nblocks;
     // one 64-lane chain per (SB row, component)
-    k_intra<<<3 * nrows, 256, 0, st>>>(f, blocks, intra_list, n_intra, d->ctl, d->progress, nrows, d->dbg,
+    k_intra<<<3 * nrows, INTRA_THREADS, 0, st>>>(f, blocks, intra_list, n_intra, d->ctl, d->progress, nrows, d->dbg,
                                       d->dbg_flags, full_sb, d->resid);
     HIPCHK(hipGetLastError());
   }

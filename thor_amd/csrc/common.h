@@ -28,7 +28,13 @@ struct FrameCtx {
   int ref_fnum[THOR_MAX_SLOTS];
   int ref_slot[THOR_MAX_SLOTS];
   int slot_lut[32];       // frame_num & 127 -> slot (int8, -1 none), 4 per word
+  // Edge rows: the bottom pixel row of every SB row, per component (the only
+  // pixels one intra chain hands to the next).  Y rows of ewy bytes, then U
+  // and V rows of ewc bytes; column x at byte EDGE_MARGIN + x.
+  uint8_t *edge;
+  int ewy, ewc, nsbrows;
 };
+#define EDGE_MARGIN 32
 
 // Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits
 // (replaces the 44-byte deblock_data_t, common/types.h:127-135):

@@ -629,6 +629,8 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
       uint32_t v = ly[i];
       if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
       *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
+      if (i == 7 && h == 1 && gr == 3)  // SB row 63: the edge row k_intra's next SB row reads
+        *(uint32_t *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + x) = v;
     }
 #pragma unroll
     for (int i = 2 * s; i < 2 * s + 2; i++) {
@@ -638,6 +640,11 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
       if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
       *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
       *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
+      if (i == 3 && h == 1 && gr == 3) {  // chroma SB row 31
+        uint8_t *e = f.edge + (long long)f.nsbrows * f.ewy + (long long)sby * f.ewc + EDGE_MARGIN + xc;
+        *(uint16_t *)e = (uint16_t)vu;
+        *(uint16_t *)(e + (long long)f.nsbrows * f.ewc) = (uint16_t)vv;
+      }
     }
   }
   STAMP(5);

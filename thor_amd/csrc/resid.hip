@@ -24,7 +24,7 @@ struct Dct32Table {
                        61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
     for (int k = 0; k < 32; k++)
       for (int n = 0; n < 32; n++) {
-        int e;
+        int e = 0;
         if (k == 0) e = 64;
         else {
           int t = (k * (2 * n + 1)) & 127;
