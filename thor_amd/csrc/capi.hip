@@ -18,7 +18,8 @@ __global__ void k_prep(const thor_block_t *, int, uint16_t *, int32_t *, int);
 __global__ void k_resid(const thor_block_t *, const int16_t *, int16_t *, int, int);
 __global__ void k_recon(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int16_t *,
                         unsigned long long *);
-__global__ void k_intra(FrameCtx, const thor_block_t *, const uint32_t *, int, unsigned *, unsigned *, int,
+__global__ void k_intra_setup(const thor_block_t *, const uint32_t *, int, unsigned *, unsigned *, int *, int);
+__global__ void k_intra(FrameCtx, const thor_block_t *, const uint32_t *, const int *, unsigned *, unsigned *, int,
                         unsigned long long *, int, int, const int16_t *);
 __global__ void k_deblock_luma_v(uint8_t *, int, int, int, const uint16_t *, int);
 __global__ void k_deblock_luma_h(uint8_t *, int, int, int, const uint16_t *, int);
@@ -174,11 +175,18 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   ok = ok && hipMemset(d->cellinfo, 0, ncell * sizeof(uint16_t)) == hipSuccess;
   ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
   ok = ok && hipMalloc(&d->resid, (size_t)W * H * 3) == hipSuccess;  // 1.5 px/luma px x 2 B
-  ok = ok && hipMalloc(&d->progress, (size_t)3 * ((H + 63) / 64 + 1) * sizeof(unsigned)) == hipSuccess;
+  // intra progress words (3 per SB row), then the rows' intra-list segments (nrows + 1)
+  ok = ok && hipMalloc(&d->progress, (size_t)4 * ((H + 63) / 64 + 2) * sizeof(unsigned)) == hipSuccess;
   d->ewy = (W + 2 * EDGE_MARGIN + 15) & ~15;
   d->ewc = (W / 2 + 2 * EDGE_MARGIN + 15) & ~15;
   ok = ok && hipMalloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc)) == hipSuccess;
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
+  {  // k_intra stages a row's CU words in LDS (up to (W/8) x 8 CUs)
+    size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
+    if (lds > 48 * 1024)
+      ok = ok && hipFuncSetAttribute((const void *)k_intra, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+                     hipSuccess;
+  }
   if (!ok) {
     thor_dec_destroy(d);
     return nullptr;
@@ -311,14 +319,16 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
   }
   if (n_intra > 0) {
     int nrows = (H + 63) / 64;
-    HIPCHK(hipMemsetAsync(d->progress, 0, (size_t)3 * nrows * sizeof(unsigned), st));
-    HIPCHK(hipMemsetAsync(d->ctl, 0, sizeof(unsigned), st));
     StageMark m(d, ST_INTRA);
+    int *rowstart = (int *)(d->progress + 3 * (nrows + 1));
+    k_intra_setup<<<1, 64, 0, st>>>(blocks, intra_list, n_intra, d->ctl, d->progress, rowstart, nrows);
+    HIPCHK(hipGetLastError());
     // full SB images only when inter CUs were reconstructed (their pixels are intra neighbours)
     int full_sb = n_intra < nblocks;
-    // one 64-lane chain per (SB row, component)
-    k_intra<<<3 * nrows, INTRA_THREADS, 0, st>>>(f, blocks, intra_list, n_intra, d->ctl, d->progress, nrows, d->dbg,
-                                      d->dbg_flags, full_sb, d->resid);
+    // one single-wave chain per (SB row, component); LDS holds the row's CU words
+    size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
+    k_intra<<<3 * nrows, 64, lds, st>>>(f, blocks, intra_list, rowstart, d->ctl, d->progress, nrows, d->dbg,
+                                        d->dbg_flags, full_sb, d->resid);
     HIPCHK(hipGetLastError());
   }
   if (d->stop_stage >= 1 && d->seq.deblocking) {

@@ -5,56 +5,53 @@
 // / top-right / bottom-left neighbours (make_top_and_left,
 // common/intra_prediction.c:57-143), so they form a dependency chain in
 // decode order.  Y, U and V never read each other, so a frame's intra work is
-// 3 x (SB rows) independent chains.  Each chain is one 256-lane workgroup: it
-// owns one component of one 64x64 SB row and reconstructs that row's intra
-// CUs in decode order, one transform block at a time: the lanes build the
-// neighbour arrays the mode needs (one edge sample per lane), then predict one
-// pixel each (1024 lanes = 16 waves, so LDS latency hides).  The rows of a
-// component form a wavefront (WPP pattern): row k may work on SB l once row
-// k-1 of the same component has completed SBs 0..l+1 (the top-right neighbour
-// is the furthest pixel read, common/common_block.c:110-118; the bottom-left
-// is never read across an SB row, :120-129).
+// 3 x (SB rows) independent chains.  Each chain is ONE wave: it owns one
+// component of one 64x64 SB row and reconstructs that row's intra CUs in
+// decode order, one transform block at a time.  A chain is a latency chain,
+// not a throughput problem, so a single wave is the fast shape: its LDS
+// operations complete in order (no barriers between building a block's
+// neighbour arrays and predicting from them), its uniform block parameters
+// are computed once (not once per wave of a workgroup, on the CU's one scalar
+// unit), and the DC sum is a DPP reduction.  The rows of a component form a
+// wavefront (WPP pattern): row k may work on SB l once row k-1 of the same
+// component has completed SBs 0..l+1 (the top-right neighbour is the furthest
+// pixel read, common/common_block.c:110-118; the bottom-left is never read
+// across an SB row, :120-129).
 //
 // Transform blocks reconstruct into the SB's LDS image only.  When a chain
 // leaves an SB it stores the SB's bottom pixel row -- the only pixels the
 // next chain reads -- to an edge-row buffer, then the whole image to the
 // frame.  Hand-off without agent-scope fences (cdna_hip_programming.md
 // Guideline 16, form R1): the edge store is write-through (sc1) and waited for
-// alone, the workgroup meets at a barrier and one lane publishes the progress
-// word with a relaxed agent-scope atomic; the consumer polls that word relaxed
-// and reads the edge row with sc1 loads (which bypass its L1), so no acquire
-// is needed.  Everything else a chain reads comes from earlier launches
-// (residual, k_recon's pixels) and is issued before the poll, so its latency
-// hides behind the wait.  Tasks (row,
-// component) are dequeued in row order (atomic head): every awaited chain is
-// held by a running workgroup, so the grid always drains.
+// alone, then one lane publishes the progress word with a relaxed agent-scope
+// atomic; the consumer polls that word relaxed and reads the edge row with
+// sc1 loads (which bypass its L1), so no acquire is needed.  Everything else
+// a chain reads comes from earlier launches (residual, k_recon's pixels, the
+// CU descriptors) and is issued before the poll, so its latency hides behind
+// the wait.  Tasks (row, component) are dequeued in row order (atomic head):
+// every awaited chain is held by a running workgroup, so the grid drains.
 #include "common.h"
 
-#define DESC_WIN 128  // CU descriptors staged in LDS per window load
-#define IMG_X0 4      // image column -4 at byte 0: rows are dword aligned
-#ifndef INTRA_THREADS
-#define INTRA_THREADS 1024
-#endif
-#define SC1 16        // buffer instruction aux: sc1 (write-through store / L1-bypassing load)
+#define IMG_X0 4  // image column -4 at byte 0: rows are dword aligned
+#define SC1 16    // buffer instruction aux: sc1 (write-through store / L1-bypassing load)
 
 template <int C>
 struct CompGeom {
-  static constexpr int SZ = C ? 32 : 64;      // SB size in this plane
-  static constexpr int IW = SZ + 8;           // image row: cols -4 .. SZ+3
-  static constexpr int IH = SZ + 1;           // image rows -1 .. SZ-1
-  static constexpr int DW = IW / 4;           // dwords per image row
+  static constexpr int SZ = C ? 32 : 64;  // SB size in this plane
+  static constexpr int IW = SZ + 8;       // image row: cols -4 .. SZ+3
+  static constexpr int IH = SZ + 1;       // image rows -1 .. SZ-1
+  static constexpr int DW = IW / 4;       // dwords per image row
 };
 
 struct IntraChain {
-  uint8_t img[65 * 72];          // SB image of this component
-  int16_t res[64 * 64];          // k_resid's residual over the SB
-  thor_block_t desc[DESC_WIN];   // intra CUs [dbase, dbase + DESC_WIN) of the row
-  uint8_t raw[256];              // neighbours of the current TU: top at 0, left at 128 (make_top_and_left)
-  uint8_t flt[256];              // 1-2-1 filtered top / left, over n or 2n by mode
-  int16_t p5[128];               // planar 5-tap filtered edges: top at 0, left at 64
-  int dcsum[2], tlF, pTL;      // DC sums double-buffered by TU parity
-  int task, seen;
+  int16_t res[64 * 64];  // k_resid's residual over the SB (16-B aligned rows)
+  uint8_t img[65 * 72];  // SB image of this component
+  uint8_t raw[256];      // neighbours of the current TU: top at 0, left at 128 (make_top_and_left)
+  uint8_t flt[256];      // 1-2-1 filtered top / left, over n or 2n by mode
+  int16_t p5[128];       // planar 5-tap filtered edges: top at 0, left at 64
 };
+// Dynamic LDS: two words per intra CU of the chain's row (cu_words).
+extern __shared__ uint2 g_cuw[];
 
 __device__ __forceinline__ int upright_available(int ypos, int xpos, int size, int width) {
   int a = (ypos > 0) && (xpos + size < width);  // common/common_block.c:110-118
@@ -72,28 +69,37 @@ __device__ __forceinline__ int downleft_available(int ypos, int xpos, int size, 
   return a;
 }
 
+// An intra CU as two words (built lane-parallel once per chain, read back
+// uniformly): w0 = ypos | xpos << 16; w1 = size | mode << 8 | tb_split << 12 |
+// coeff_mask << 13 | up-right available << 16 | down-left available << 17.
+// Modes past the last intra mode predict DC (get_intra_prediction's default).
+__device__ __forceinline__ uint2 cu_words(const thor_block_t &D, int W, int H) {
+  const int y = D.ypos, x = D.xpos, S = D.size;
+  const int m = D.intra_mode > 9 ? 0 : D.intra_mode;
+  const uint32_t w1 = (uint32_t)S | (uint32_t)m << 8 | (uint32_t)(D.tb_split != 0) << 12 |
+                      (uint32_t)(D.coeff_mask & 7) << 13 | (uint32_t)upright_available(y, x, S, W) << 16 |
+                      (uint32_t)downleft_available(y, x, S, H) << 17;
+  return make_uint2((uint32_t)y | (uint32_t)x << 16, w1);
+}
+
 // Parameters of one transform block (uniform: scalar registers).
 struct TuP {
-  int active, n, lg, has, mode;
-  int iy, ix;           // TU origin inside the SB image
+  int n, lg, has, mode;
+  int iy, ix;  // TU origin inside the SB image
   int toplen, leftlen, top_none, left_none;
-  int xnz, ynz;         // xnz bit0: TU x != 0 (DC selector, :366); bit1: CU x > 0 (top_left, :79/:96)
-  long long gofs;       // plane offset of the TU origin
+  int xnz, ynz;  // xnz bit0: TU x != 0 (DC selector, :366); bit1: CU x > 0 (top_left, :79/:96)
 };
 
 // Component C's transform block of TU step t (intra_prediction.c:57-143 +
 // dec/decode_block.c:48-88: tb_split gives 4 raster sub-TUs; chroma of an
 // 8x8 CU is not split).
 template <int C>
-__device__ __forceinline__ TuP make_tup(int S, int tb, int y, int x, int mode, int cmask, int t, int ur_cb, int dl_cb,
-                                        int stride) {
+__device__ __forceinline__ TuP make_tup(int S, int tbc, int y, int x, int mode, int cmask, int t, int ur_cb, int dl_cb) {
   TuP p;
-  int size = C ? S >> 1 : S;
-  int tbc = C ? (tb && S > 8) : tb;
-  p.active = t < (tbc ? 4 : 1);
-  int n = tbc ? size >> 1 : size;
-  int i0_ = tbc ? (t >> 1) * n : 0, j0_ = tbc ? (t & 1) * n : 0;
-  int yp = C ? y >> 1 : y, xp = C ? x >> 1 : x;
+  const int size = C ? S >> 1 : S;
+  const int n = tbc ? size >> 1 : size;
+  const int i0_ = tbc ? (t >> 1) * n : 0, j0_ = tbc ? (t & 1) * n : 0;
+  const int yp = C ? y >> 1 : y, xp = C ? x >> 1 : x;
   constexpr int sbm = CompGeom<C>::SZ - 1;
   p.n = n;
   p.lg = ilog2i(n);
@@ -113,35 +119,44 @@ __device__ __forceinline__ TuP make_tup(int S, int tb, int y, int x, int mode, i
   p.left_none = (xp + j0_) == 0;
   p.xnz = ((xp + j0_) != 0) | ((xp > 0) << 1);
   p.ynz = (yp + i0_) != 0;
-  p.gofs = (long long)(yp + i0_) * stride + xp + j0_;
   return p;
 }
 
 __device__ __forceinline__ unsigned ld_progress(const unsigned *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Residual of SB (k, l), 4 int16 per item, plain loads (written by k_resid in
+
+// Sum over the wave (every lane active): DPP within rows of 16, then the four
+// row sums through readlane.  Uniform result.
+__device__ __forceinline__ int wave_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, true);  // row_half_mirror
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, true);  // row_mirror
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+
+// Residual of SB (k, l), 8 int16 per item, plain loads (written by k_resid in
 // an earlier launch; rows past the plane read as 0).
 template <int C>
 struct ResLoad {
-  static constexpr int SZ = CompGeom<C>::SZ, PER = SZ / 4, NR = SZ * PER;
-  static constexpr int RR = (NR + INTRA_THREADS - 1) / INTRA_THREADS;
-  uint2 v[RR];
+  static constexpr int SZ = CompGeom<C>::SZ, PER = SZ / 8, NR = SZ * PER, RR = NR / 64;
+  uint4 v[RR];
   __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rr, int pw, int k, int l) {
 #pragma unroll
     for (int r = 0; r < RR; r++) {
-      const int q = threadIdx.x + INTRA_THREADS * r;
-      const int row = q / PER, x = l * SZ + 4 * (q - row * PER), y = k * SZ + row;
-      v[r] = q < NR ? __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, 2 * (y * pw + x), 0, 0))
-                    : make_uint2(0, 0);
+      const int q = threadIdx.x + 64 * r;
+      const int row = q / PER, x = l * SZ + 8 * (q - row * PER), y = k * SZ + row;
+      v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr, 2 * (y * pw + x), 0, 0));
     }
   }
   __device__ __forceinline__ void commit(IntraChain &L) const {
 #pragma unroll
     for (int r = 0; r < RR; r++) {
-      const int q = threadIdx.x + INTRA_THREADS * r;
-      const int row = q / PER, col = 4 * (q - row * PER);
-      if (q < NR) *(uint2 *)&L.res[row * SZ + col] = v[r];
+      const int q = threadIdx.x + 64 * r;
+      const int row = q / PER, col = 8 * (q - row * PER);
+      *(uint4 *)&L.res[row * SZ + col] = v[r];
     }
   }
 };
@@ -152,71 +167,76 @@ struct ResLoad {
 // frames: k_recon reconstructed the inter CUs) rows 0..SZ-1 come from the
 // frame, issued before the poll (nothing this launch writes them).  The left
 // column is the previous SB's last image column when the chain just left that
-// SB, else the frame's (k_recon's pixels, or outside the frame).  Bytes past
-// the frame's right / bottom edge are never used as neighbours
-// (availability, common_block.c:100-129).
+// SB, else the frame's (k_recon's pixels; without FULL every CU is intra, so
+// the chain visits every SB and only SB 0 lacks a previous one -- its left
+// column is outside the frame and never read).  Bytes past the frame's right
+// / bottom edge are never used as neighbours (availability,
+// common_block.c:100-129).
 template <int C, bool FULL>
 struct ImgLoad {
   using G = CompGeom<C>;
-  static constexpr int NIMG = FULL ? G::SZ * G::DW : 0;
-  static constexpr int RI = (NIMG + INTRA_THREADS - 1) / INTRA_THREADS;
-  uint32_t iv[RI > 0 ? RI : 1];
+  static constexpr int PER = G::SZ / 16;                  // 16-B pieces per interior row
+  static constexpr int RI = FULL ? G::SZ * PER / 64 : 0;  // per lane
+  uint4 iv[RI > 0 ? RI : 1];
   uint32_t ev, lv;
   __device__ __forceinline__ void issue_interior(__amdgpu_buffer_rsrc_t fr, int pofs, int stride, int k, int l,
                                                  bool from_prev) {
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
 #pragma unroll
     for (int r = 0; r < RI; r++) {
-      const int q = tid + INTRA_THREADS * r;
-      const int row = q / G::DW, col = q - row * G::DW;
-      iv[r] = q < NIMG ? __builtin_amdgcn_raw_buffer_load_b32(
-                             fr, pofs + (k * G::SZ + row) * stride + l * G::SZ - IMG_X0 + 4 * col, 0, 0)
-                       : 0u;
+      const int q = lane + 64 * r;
+      const int row = q / PER, col = 16 * (q - row * PER);
+      iv[r] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(fr, pofs + (k * G::SZ + row) * stride + l * G::SZ + col, 0, 0));
     }
     lv = 0;
-    if (!FULL && !from_prev && tid < G::SZ)
-      lv = __builtin_amdgcn_raw_buffer_load_b8(fr, pofs + (k * G::SZ + tid) * stride + l * G::SZ - 1, 0, 0);
+    if (FULL && !from_prev && lane < G::SZ)
+      lv = __builtin_amdgcn_raw_buffer_load_b8(fr, pofs + (k * G::SZ + lane) * stride + l * G::SZ - 1, 0, 0);
   }
   __device__ __forceinline__ void issue_edge(__amdgpu_buffer_rsrc_t eb, int ew, int k, int l) {
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     ev = 0;
-    if (tid < G::DW)
-      ev = __builtin_amdgcn_raw_buffer_load_b32(eb, (k - 1) * ew + EDGE_MARGIN + l * G::SZ - IMG_X0 + 4 * tid, 0, SC1);
+    if (lane < G::DW)
+      ev = __builtin_amdgcn_raw_buffer_load_b32(eb, (k - 1) * ew + EDGE_MARGIN + l * G::SZ - IMG_X0 + 4 * lane, 0, SC1);
   }
+  // LDS operations of one wave complete in order: the left column of the
+  // SB left behind is read before the new image overwrites it.
   __device__ __forceinline__ void commit(IntraChain &L, bool from_prev) const {
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     uint8_t *img = L.img + G::IW + IMG_X0;  // image (0,0)
-    const uint8_t keep = (from_prev && tid < G::SZ) ? img[tid * G::IW + G::SZ - 1] : 0;
-    __syncthreads();  // `keep` read everywhere before the image is overwritten
+    const uint8_t keep = (from_prev && lane < G::SZ) ? img[lane * G::IW + G::SZ - 1] : 0;
 #pragma unroll
     for (int r = 0; r < RI; r++) {
-      const int q = tid + INTRA_THREADS * r;
-      const int row = q / G::DW, col = q - row * G::DW;
-      if (q < NIMG) *(uint32_t *)(img + row * G::IW - IMG_X0 + 4 * col) = iv[r];
+      const int q = lane + 64 * r;
+      const int row = q / PER, col = 16 * (q - row * PER);
+      uint32_t *d = (uint32_t *)(img + row * G::IW + col);
+      d[0] = iv[r].x;
+      d[1] = iv[r].y;
+      d[2] = iv[r].z;
+      d[3] = iv[r].w;
     }
-    if (tid < G::DW) *(uint32_t *)(img - G::IW - IMG_X0 + 4 * tid) = ev;
-    if (tid < G::SZ) {
-      if (from_prev) img[tid * G::IW - 1] = keep;
-      else if (!FULL) img[tid * G::IW - 1] = (uint8_t)lv;
+    if (lane < G::DW) *(uint32_t *)(img - G::IW - IMG_X0 + 4 * lane) = ev;
+    if (lane < G::SZ) {
+      if (from_prev) img[lane * G::IW - 1] = keep;
+      else if (FULL) img[lane * G::IW - 1] = (uint8_t)lv;
     }
   }
 };
 
 // The chain leaves SB (k, l): its edge row goes out write-through (sc1) and is
-// waited for (nothing else of this wave's is in flight then), the workgroup
-// meets, one lane publishes "SBs < next are done" (form R1).
+// waited for (nothing else of the wave's is in flight then), then one lane
+// publishes "SBs < next are done" (form R1).
 template <int C>
 __device__ __forceinline__ void publish_sb(IntraChain &L, __amdgpu_buffer_rsrc_t eb, int ew, int k, int l, unsigned *my,
                                            unsigned next) {
   using G = CompGeom<C>;
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const uint8_t *img = L.img + G::IW + IMG_X0;
-  if (tid < G::SZ / 4)
-    __builtin_amdgcn_raw_buffer_store_b32(*(const uint32_t *)(img + (G::SZ - 1) * G::IW + 4 * tid), eb,
-                                          k * ew + EDGE_MARGIN + l * G::SZ + 4 * tid, 0, SC1);
+  if (lane < G::SZ / 4)
+    __builtin_amdgcn_raw_buffer_store_b32(*(const uint32_t *)(img + (G::SZ - 1) * G::IW + 4 * lane), eb,
+                                          k * ew + EDGE_MARGIN + l * G::SZ + 4 * lane, 0, SC1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) __hip_atomic_store(my, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store(my, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // ... then the whole SB image goes to the frame (plain stores: only later
 // launches read it).  Rows / columns past the frame edge land in the slot's
@@ -225,41 +245,20 @@ template <int C>
 __device__ __forceinline__ void store_sb(const IntraChain &L, __amdgpu_buffer_rsrc_t fr, int pofs, int stride, int k,
                                          int l) {
   using G = CompGeom<C>;
-  const int tid = threadIdx.x;
+  constexpr int PER = G::SZ / 16, NR = G::SZ * PER;
   const uint8_t *img = L.img + G::IW + IMG_X0;
-  if (tid >= 256) return;
-  if (C == 0) {  // 64 rows x 64 B: 16 B per lane
-    const int row = tid >> 2, col = (tid & 3) * 16;
-    const uint32_t *q = (const uint32_t *)(img + row * G::IW + col);
+#pragma unroll
+  for (int r = 0; r < NR / 64; r++) {
+    const int q = threadIdx.x + 64 * r;
+    const int row = q / PER, col = 16 * (q - row * PER);
+    const uint32_t *s = (const uint32_t *)(img + row * G::IW + col);
     __builtin_amdgcn_raw_buffer_store_b128(
-        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, make_uint4(q[0], q[1], q[2], q[3])), fr,
+        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, make_uint4(s[0], s[1], s[2], s[3])), fr,
         pofs + (k * G::SZ + row) * stride + l * G::SZ + col, 0, 0);
-  } else {  // 32 rows x 32 B: 4 B per lane
-    const int row = tid >> 3, col = (tid & 7) * 4;
-    __builtin_amdgcn_raw_buffer_store_b32(*(const uint32_t *)(img + row * G::IW + col), fr,
-                                          pofs + (k * G::SZ + row) * stride + l * G::SZ + col, 0, 0);
   }
 }
 
-// Neighbours of one transform block inside the SB image, with
-// make_top_and_left's rules (intra_prediction.c:57-143): 128 outside the
-// frame, the last available sample repeated past the up-right / down-left
-// availability (toplen / leftlen), indices clamped to the 2n edge.
-template <int C>
-struct Nb {
-  const uint8_t *trow, *lcol;  // image row -1 at the TU's x, image column -1 at its y
-  int cnt, toplen, leftlen, top_none, left_none;
-  __device__ __forceinline__ int T(int m) const {
-    m = m < 0 ? 0 : (m > cnt - 1 ? cnt - 1 : m);
-    return top_none ? 128 : trow[m < toplen ? m : toplen - 1];
-  }
-  __device__ __forceinline__ int Lf(int m) const {
-    m = m < 0 ? 0 : (m > cnt - 1 ? cnt - 1 : m);
-    return left_none ? 128 : lcol[(m < leftlen ? m : leftlen - 1) * CompGeom<C>::IW];
-  }
-};
-
-// filter_121 of one edge sample over len (:39-48); v[] = samples k-1, k, k+1
+// filter_121 of one edge sample over len (:39-48); a, b, c = samples k-1, k, k+1
 __device__ __forceinline__ int f121(int k, int len, int a, int b, int c) {
   return k == 0 ? (3 * b + c + 2) >> 2 : (k == len - 1 ? (a + 3 * b + 2) >> 2 : (a + 2 * b + c + 2) >> 2);
 }
@@ -313,45 +312,50 @@ __device__ __forceinline__ int intra_px(const IntraChain &L, int tlF, int pTL, i
   return dc;
 }
 
-// Phase C: one pixel per lane (4 for 64x64 blocks): prediction + residual.
+// Phase C: four horizontally adjacent pixels per lane and step: prediction +
+// residual, one dword into the image.
 template <int M, int C>
-__device__ __forceinline__ void intra_pred_px(IntraChain &L, const TuP &p, int par) {
+__device__ __forceinline__ void intra_pred(IntraChain &L, const TuP &p, int tlF, int pTL, int dc) {
   using G = CompGeom<C>;
   uint8_t *img = L.img + G::IW + IMG_X0;
-  const int n = p.n;
-  const int tlF = L.tlF, pTL = L.pTL, dc = M == 0 ? (L.dcsum[par] + n) / (2 * n) : 0;
-  for (int q = threadIdx.x; q < n * n; q += INTRA_THREADS) {
-    const int i = q >> p.lg, j = q & (n - 1);
-    const int r = p.has ? (int)L.res[(p.iy + i) * G::SZ + p.ix + j] : 0;
-    img[(p.iy + i) * G::IW + p.ix + j] = (uint8_t)clip255(intra_px<M>(L, tlF, pTL, dc, i, j) + r);
+  const int n = p.n, lgq = p.lg - 2, ng = (n * n) >> 2;
+  for (int g = threadIdx.x; g < ng; g += 64) {
+    const int i = g >> lgq, j = (g & ((n >> 2) - 1)) << 2;
+    uint2 rw = make_uint2(0, 0);
+    if (p.has) rw = *(const uint2 *)&L.res[(p.iy + i) * G::SZ + p.ix + j];
+    const int r[4] = {(int)(int16_t)(rw.x & 0xffff), (int)(int16_t)(rw.x >> 16), (int)(int16_t)(rw.y & 0xffff),
+                      (int)(int16_t)(rw.y >> 16)};
+    uint32_t o = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) o |= put_byte(clip255(intra_px<M>(L, tlF, pTL, dc, i, j + e) + r[e]), e);
+    *(uint32_t *)(img + (p.iy + i) * G::IW + p.ix + j) = o;
   }
 }
 
-// One transform block: phase A builds the neighbour arrays the mode needs,
-// one sample per lane (lanes 0..2n-1 the top edge, 2n..4n-1 the left edge)
-// and the DC sum by LDS atomics; phase C predicts every pixel.  Two barriers.
-// The SB reaches the frame once, when the chain leaves it.
+// One transform block.  Phase A builds the neighbour arrays the mode needs,
+// one edge sample per lane and step (samples 0..2n-1 the top edge, 2n..4n-1
+// the left edge, make_top_and_left's rules: 128 outside the frame, the last
+// available sample repeated past the up-right / down-left availability,
+// indices clamped to the 2n edge), the corner terms uniformly and the DC sum
+// by DPP; phase C predicts every pixel.  The SB reaches the frame once, when
+// the chain leaves it.
 template <int C>
-__device__ __forceinline__ void intra_tu(IntraChain &L, const TuP &p, int par) {
+__device__ __forceinline__ void intra_tu(IntraChain &L, const TuP &p) {
   using G = CompGeom<C>;
-  const int tid = threadIdx.x;
-  uint8_t *img = L.img + G::IW + IMG_X0;
-  Nb<C> b;
-  b.trow = img + (p.iy - 1) * G::IW + p.ix;
-  b.lcol = img + p.iy * G::IW + p.ix - 1;
-  b.cnt = 2 * p.n;
-  b.toplen = p.toplen;
-  b.leftlen = p.leftlen;
-  b.top_none = p.top_none;
-  b.left_none = p.left_none;
+  const int lane = threadIdx.x;
+  const uint8_t *img = L.img + G::IW + IMG_X0;
+  const uint8_t *trow = img + (p.iy - 1) * G::IW + p.ix, *lcol = img + p.iy * G::IW + p.ix - 1;
   const int n = p.n, cnt = 2 * n, mode = p.mode;
-#ifndef INTRA_PROBE_SKIP_A
-  if (tid < 2 * cnt) {  // ---- phase A: lanes 0..2n-1 the top edge, 2n..4n-1 the left edge, selects only ----
-    const int side = tid >= cnt;
-    const int k = tid - side * cnt;
+  const bool is_dc = mode == 0;
+  const int flen = (mode == 5 || mode == 6 || mode == 9) ? cnt : n;
+  const int tbase = (int)(trow - L.img), lbase = (int)(lcol - L.img);
+  int dcacc = 0;
+  for (int q = lane; q < 2 * cnt; q += 64) {
+    const int side = q >= cnt;
+    const int k = q - side * cnt;
     const int len = side ? p.leftlen : p.toplen, none = side ? p.left_none : p.top_none;
     const int step = side ? G::IW : 1;
-    const int base = (int)((side ? b.lcol : b.trow) - L.img);
+    const int base = side ? lbase : tbase;
     int v[5];
 #pragma unroll
     for (int o = 0; o < 5; o++) {
@@ -364,58 +368,51 @@ __device__ __forceinline__ void intra_tu(IntraChain &L, const TuP &p, int par) {
     L.raw[128 * side + k] = (uint8_t)v[2];
     // the one pre-filter this mode reads: 1-2-1 over n (4, 7, 8), over 2n of
     // the top (5, 6) or of the left (9); planar 5-tap; DC sum
-    const int flen = (mode == 5 || mode == 6 || mode == 9) ? cnt : n;
     const bool want_f = (mode == 4 || mode == 7 || mode == 8) ? k < n
                         : ((mode == 5 || mode == 6) ? !side : (mode == 9 ? (bool)side : false));
     if (want_f) L.flt[128 * side + k] = (uint8_t)f121(k, flen, v[1], v[2], v[3]);
     if (mode == 1 && k < n) L.p5[64 * side + k] = (int16_t)p5f(k, n, v[0], v[1], v[2], v[3], v[4]);
-    if ((mode == 0 || mode > 9) && k < n) {
+    if (is_dc && k < n) {
       // DC sum of get_dc_pred(xpos!=0 ? left:top, ypos!=0 ? top:left), :145-160, :366
       const int xs = p.xnz & 1;
       const int w = side ? xs + (!p.ynz) : (!xs) + p.ynz;
-      if (w) atomicAdd(&L.dcsum[par], v[2] * w);
-    }
-    if (tid == 0) {  // corner terms (:77-99, :186-189)
-      int tl = p.top_none ? 128 : ((p.xnz & 2) ? b.trow[-1] : b.trow[0]);
-      if (p.top_none) tl = p.left_none ? 128 : b.lcol[0];  // ypos+i==0: top_left = left[0]
-      const int t0 = b.T(0), l0 = b.Lf(0);
-      L.tlF = (2 * tl + l0 + t0 + 2) >> 2;
-      L.pTL = b.Lf(1) + 2 * l0 + 2 * tl + 2 * t0 + b.T(1);
+      dcacc += v[2] * w;
     }
   }
-#endif
-  __syncthreads();
-  if (tid == 0) L.dcsum[par ^ 1] = 0;  // the next TU's sum (last read before this TU's first barrier)
-#if defined(INTRA_PROBE_SKIP_C)
-  if (0)
-#elif defined(INTRA_PROBE_ONE_MODE)
-  intra_pred_px<0, C>(L, p, par);
-  if (0)
-#endif
+  int tlF = 0, pTL = 0, dc = 0;
+  if (mode == 1 || mode == 4 || mode == 7 || mode == 8) {  // corner terms (:77-99, :186-189), uniform
+    auto T = [&](int m) { return p.top_none ? 128 : (int)trow[m < p.toplen ? m : p.toplen - 1]; };
+    auto Lf = [&](int m) { return p.left_none ? 128 : (int)lcol[(m < p.leftlen ? m : p.leftlen - 1) * G::IW]; };
+    int tl = p.top_none ? 128 : ((p.xnz & 2) ? trow[-1] : trow[0]);
+    if (p.top_none) tl = p.left_none ? 128 : lcol[0];  // ypos+i==0: top_left = left[0]
+    const int t0 = T(0), l0 = Lf(0);
+    tlF = __builtin_amdgcn_readfirstlane((2 * tl + l0 + t0 + 2) >> 2);
+    pTL = __builtin_amdgcn_readfirstlane(Lf(1) + 2 * l0 + 2 * tl + 2 * t0 + T(1));
+  }
+  if (is_dc) dc = (wave_sum(dcacc) + n) / (2 * n);
+  wave_lds_sync();
   switch (mode) {  // uniform
-    case 1: intra_pred_px<1, C>(L, p, par); break;
-    case 2: intra_pred_px<2, C>(L, p, par); break;
-    case 3: intra_pred_px<3, C>(L, p, par); break;
-    case 4: intra_pred_px<4, C>(L, p, par); break;
-    case 5: intra_pred_px<5, C>(L, p, par); break;
-    case 6: intra_pred_px<6, C>(L, p, par); break;
-    case 7: intra_pred_px<7, C>(L, p, par); break;
-    case 8: intra_pred_px<8, C>(L, p, par); break;
-    case 9: intra_pred_px<9, C>(L, p, par); break;
-    default: intra_pred_px<0, C>(L, p, par); break;
+    case 1: intra_pred<1, C>(L, p, tlF, pTL, dc); break;
+    case 2: intra_pred<2, C>(L, p, tlF, pTL, dc); break;
+    case 3: intra_pred<3, C>(L, p, tlF, pTL, dc); break;
+    case 4: intra_pred<4, C>(L, p, tlF, pTL, dc); break;
+    case 5: intra_pred<5, C>(L, p, tlF, pTL, dc); break;
+    case 6: intra_pred<6, C>(L, p, tlF, pTL, dc); break;
+    case 7: intra_pred<7, C>(L, p, tlF, pTL, dc); break;
+    case 8: intra_pred<8, C>(L, p, tlF, pTL, dc); break;
+    case 9: intra_pred<9, C>(L, p, tlF, pTL, dc); break;
+    default: intra_pred<0, C>(L, p, tlF, pTL, dc); break;
   }
-  __syncthreads();  // the next TU reads these pixels (and rewrites the edge arrays)
+  wave_lds_sync();  // the next TU reads these pixels (and rewrites the edge arrays)
 }
 
-// One chain: component C of SB row `row`.
+// One chain: component C of SB row `row`; its ncu intra CUs' words are staged
+// in g_cuw[0 .. ncu).
 template <int C>
-__device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, const thor_block_t *__restrict__ blk,
-                                          const uint32_t *__restrict__ list, int i0, int i1, unsigned *ctl,
-                                          unsigned *progress, int row, int full, const int16_t *__restrict__ resid,
-                                          int dbg_flags, bool timed, unsigned long long *tsb) {
+__device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, int ncu, unsigned *ctl, unsigned *progress,
+                                          int row, int full, const int16_t *__restrict__ resid, int dbg_flags) {
   unsigned long long tw = 0;  // ticks spent waiting on the row above (debug)
-  unsigned long long t_sb = 0, t_tu = 0, n_sb = 0, n_tu = 0;  // debug: SB transitions / TUs
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   uint8_t *const plane = C == 0 ? f.cy : (C == 1 ? f.cu : f.cv);
   const int stride = C ? f.sc : f.sy;
   const int pw = C ? f.W >> 1 : f.W, ph = C ? f.H >> 1 : f.H;
@@ -430,25 +427,17 @@ __device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, cons
   const int nsbw = (f.W + 63) >> 6;
   unsigned *my = progress + 3 * row + C;
   const unsigned *above = progress + 3 * (row - 1) + C;
-  int seen = row == 0 ? 0x7fffffff : 0, cur_sb = -2, ntu = 0;
-  int dbase = i0 - DESC_WIN;
-  for (int it = i0; it < i1; it++) {
-    if (it - dbase >= DESC_WIN) {  // stage the next window of CU descriptors
-      dbase = it;
-      __syncthreads();
-      for (int q = tid; q < DESC_WIN && it + q < i1; q += INTRA_THREADS) L.desc[q] = blk[list[it + q]];
-      __syncthreads();
-    }
-    // descriptor fields are uniform: scalar registers
-    const thor_block_t &D = L.desc[it - dbase];
-    const int y = __builtin_amdgcn_readfirstlane(D.ypos), x = __builtin_amdgcn_readfirstlane(D.xpos);
-    const int S = __builtin_amdgcn_readfirstlane(D.size), tb = __builtin_amdgcn_readfirstlane(D.tb_split) != 0;
-    const int mode = __builtin_amdgcn_readfirstlane(D.intra_mode), cmask = __builtin_amdgcn_readfirstlane(D.coeff_mask);
+  int seen = row == 0 ? 0x7fffffff : 0, cur_sb = -2;
+  uint2 wn = ncu > 0 ? g_cuw[0] : make_uint2(0, 0);
+  for (int it = 0; it < ncu; it++) {
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wn.x), w1 = __builtin_amdgcn_readfirstlane(wn.y);
+    if (it + 1 < ncu) wn = g_cuw[it + 1];  // next CU's words in flight during this one
+    const int y = w0 & 0xffff, x = w0 >> 16, S = w1 & 0xff, mode = (w1 >> 8) & 15, tb = (w1 >> 12) & 1;
+    const int cmask = (w1 >> 13) & 7, ur_cb = (w1 >> 16) & 1, dl_cb = (w1 >> 17) & 1;
     const int l = x >> 6;
     if (l != cur_sb) {
-      const unsigned long long ts0 = timed ? __builtin_amdgcn_s_memtime() : 0;
-      // SB transition: loads with no dependency first (residual, FULL interior),
-      // flush + publish the SB left behind, wait for the row above, edge row
+      // SB transition: flush + publish the SB left behind, loads with no
+      // dependency (residual, FULL interior), wait for the row above, edge row
       const bool from_prev = cur_sb == l - 1;
       if (cur_sb >= 0) publish_sb<C>(L, eb, ew, row, cur_sb, my, (unsigned)l);
       ResLoad<C> res;
@@ -456,25 +445,23 @@ __device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, cons
       ImgLoad<C, true> imf;
       ImgLoad<C, false> imn;
       if (full) imf.issue_interior(fr, pofs, stride, row, l, from_prev);
-      else imn.issue_interior(fr, pofs, stride, row, l, from_prev);
       if (cur_sb >= 0) store_sb<C>(L, fr, pofs, stride, row, cur_sb);
       int need = l + 2 < nsbw ? l + 2 : nsbw;
       if (dbg_flags & 1) need = 0;  // debug: ignore the wavefront dependency (wrong pixels)
       if (seen < need) {
-        if (tid == 0) {
-          const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0;
-          unsigned v = ld_progress(above);
-          unsigned spins = 0;
-          while ((int)v < need) {
-            __builtin_amdgcn_s_sleep(1);
-            v = ld_progress(above);
-            if (++spins > (1u << 27)) { atomicOr(&ctl[1], 1u); break; }
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        int v = (int)__builtin_amdgcn_readfirstlane(ld_progress(above));
+        unsigned spins = 0;
+        while (v < need) {
+          __builtin_amdgcn_s_sleep(1);
+          v = (int)__builtin_amdgcn_readfirstlane(ld_progress(above));
+          if (++spins > (1u << 27)) {
+            if (lane == 0) atomicOr(&ctl[1], 1u);
+            break;
           }
-          L.seen = (int)v;
-          if (timed) tw += __builtin_amdgcn_s_memtime() - t0;
         }
-        __syncthreads();
-        seen = L.seen;
+        seen = v;
+        tw += __builtin_amdgcn_s_memtime() - t0;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 edge loads below the poll
       if (full) {
@@ -485,74 +472,79 @@ __device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, cons
         imn.commit(L, from_prev);
       }
       res.commit(L);
-      __syncthreads();
+      wave_lds_sync();
       cur_sb = l;
-      if (timed) { t_sb += __builtin_amdgcn_s_memtime() - ts0; n_sb++; }
     }
-    const int ur_cb = upright_available(y, x, S, f.W), dl_cb = downleft_available(y, x, S, f.H);
-    const int nsteps = (C == 0 ? tb : (tb && S > 8)) ? 4 : 1;
-    const unsigned long long tt0 = timed ? __builtin_amdgcn_s_memtime() : 0;
-    for (int t = 0; t < nsteps; t++) {
-      const TuP p = make_tup<C>(S, tb, y, x, mode, cmask, t, ur_cb, dl_cb, stride);
-      if (dbg_flags & 4) {  // debug: barriers only (measures the TU loop overhead)
-        __syncthreads();
-        __syncthreads();
-      } else {
-        intra_tu<C>(L, p, ntu++ & 1);
-      }
-    }
-    if (timed) { t_tu += __builtin_amdgcn_s_memtime() - tt0; n_tu += nsteps; }
+    const int tbc = C == 0 ? tb : (tb && S > 8);
+    const int nsteps = tbc ? 4 : 1;
+    for (int t = 0; t < nsteps; t++) intra_tu<C>(L, make_tup<C>(S, tbc, y, x, mode, cmask, t, ur_cb, dl_cb));
   }
   if (cur_sb >= 0) {
     publish_sb<C>(L, eb, ew, row, cur_sb, my, 0x7fffffffu);
     store_sb<C>(L, fr, pofs, stride, row, cur_sb);
-  } else if (tid == 0) {
+  } else if (lane == 0) {
     __hip_atomic_store(my, 0x7fffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (timed && tid == 0) {
-    tsb[0] = t_sb; tsb[1] = t_tu; tsb[2] = n_sb; tsb[3] = n_tu;
   }
   return tw;
 }
 
-__global__ __launch_bounds__(INTRA_THREADS) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,
-                                                         const uint32_t *__restrict__ list, int n_intra, unsigned *ctl,
-                                                         unsigned *progress, int nrows, unsigned long long *dbg,
-                                                         int dbg_flags, int full_sb, const int16_t *__restrict__ resid) {
-  __shared__ IntraChain L;
-  const int tid = threadIdx.x;
-  for (;;) {
-    if (tid == 0) {
-      L.task = (int)atomicAdd(&ctl[0], 1u);
-      L.dcsum[0] = 0;
+// Per-frame setup before k_intra: each SB row's segment of the intra list
+// (decode order is raster SB order) into rowstart[0..nrows]; progress words
+// and the task head cleared.
+__global__ __launch_bounds__(64) void k_intra_setup(const thor_block_t *__restrict__ blk,
+                                                    const uint32_t *__restrict__ list, int n_intra, unsigned *ctl,
+                                                    unsigned *progress, int *rowstart, int nrows) {
+  for (int r = threadIdx.x; r <= nrows; r += 64) {
+    int lo = 0, hi = n_intra;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((blk[list[mid]].ypos >> 6) < r) lo = mid + 1;
+      else hi = mid;
     }
-    __syncthreads();
-    const int task = L.task;
-    __syncthreads();
+    rowstart[r] = lo;
+  }
+  for (int q = threadIdx.x; q < 3 * nrows; q += 64) progress[q] = 0;
+  if (threadIdx.x == 0) ctl[0] = 0;
+}
+
+__global__ __launch_bounds__(64) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,
+                                              const uint32_t *__restrict__ list, const int *__restrict__ rowstart,
+                                              unsigned *ctl, unsigned *progress, int nrows, unsigned long long *dbg,
+                                              int dbg_flags, int full_sb, const int16_t *__restrict__ resid) {
+  __shared__ IntraChain L;
+  const int lane = threadIdx.x;
+  for (;;) {
+    const int task = (int)__builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&ctl[0], 1u) : 0u);
     if (task >= 3 * nrows) return;
     const int row = task / 3, c = task - 3 * row;
-    // decode order is raster SB order: binary-search this row's segment
-    int lo = 0, hi = n_intra;
-    while (lo < hi) { int mid = (lo + hi) >> 1; if ((blk[list[mid]].ypos >> 6) < row) lo = mid + 1; else hi = mid; }
-    const int i0 = lo;
-    hi = n_intra;
-    while (lo < hi) { int mid = (lo + hi) >> 1; if ((blk[list[mid]].ypos >> 6) <= row) lo = mid + 1; else hi = mid; }
-    const int i1 = lo;
-    const unsigned long long t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    const int i0 = rowstart[row], ncu = rowstart[row + 1] - i0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    // stage the row's CU words (lane-parallel, four batches of loads in flight)
+    for (int b = 0; b < ncu; b += 256) {
+      uint32_t id[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int q = b + 64 * u + lane;
+        id[u] = q < ncu ? list[i0 + q] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int q = b + 64 * u + lane;
+        if (q < ncu) g_cuw[q] = cu_words(blk[id[u]], f.W, f.H);
+      }
+    }
+    wave_lds_sync();
     unsigned long long tw;
-    const bool timed = dbg != nullptr;
-    if (c == 0) tw = intra_chain<0>(L, f, blk, list, i0, i1, ctl, progress, row, full_sb, resid, dbg_flags, timed,
-                                      dbg ? dbg + 16 * task + 4 : nullptr);
-    else if (c == 1) tw = intra_chain<1>(L, f, blk, list, i0, i1, ctl, progress, row, full_sb, resid, dbg_flags, timed,
-                                      dbg ? dbg + 16 * task + 4 : nullptr);
-    else tw = intra_chain<2>(L, f, blk, list, i0, i1, ctl, progress, row, full_sb, resid, dbg_flags, timed,
-                                      dbg ? dbg + 16 * task + 4 : nullptr);
-    if (dbg && tid == 0) {
+    if (c == 0) tw = intra_chain<0>(L, f, ncu, ctl, progress, row, full_sb, resid, dbg_flags);
+    else if (c == 1) tw = intra_chain<1>(L, f, ncu, ctl, progress, row, full_sb, resid, dbg_flags);
+    else tw = intra_chain<2>(L, f, ncu, ctl, progress, row, full_sb, resid, dbg_flags);
+    if (dbg && lane == 0) {
       unsigned long long *o = dbg + 16 * task;
       o[0] = t0;
       o[1] = __builtin_amdgcn_s_memtime();
       o[2] = tw;
-      o[3] = (unsigned long long)(i1 - i0);
+      o[3] = (unsigned long long)ncu;
     }
+    wave_lds_sync();  // the next task restages g_cuw
   }
 }
