@@ -45,10 +45,9 @@ struct CompGeom {
 
 struct IntraChain {
   int16_t res[64 * 64];  // k_resid's residual over the SB (16-B aligned rows)
-  uint8_t img[65 * 72];  // SB image of this component
-  uint8_t raw[256];      // neighbours of the current TU: top at 0, left at 128 (make_top_and_left)
-  uint8_t flt[256];      // 1-2-1 filtered top / left, over n or 2n by mode
   int16_t p5[128];       // planar 5-tap filtered edges: top at 0, left at 64
+  uint8_t flt[256];      // directional edge array of the current TU (U_OFF layout below)
+  uint8_t img[65 * 72];  // SB image of this component
 };
 // Dynamic LDS: two words per intra CU of the chain's row (cu_words).
 extern __shared__ uint2 g_cuw[];
@@ -93,17 +92,18 @@ struct TuP {
 // Component C's transform block of TU step t (intra_prediction.c:57-143 +
 // dec/decode_block.c:48-88: tb_split gives 4 raster sub-TUs; chroma of an
 // 8x8 CU is not split).
-template <int C>
-__device__ __forceinline__ TuP make_tup(int S, int tbc, int y, int x, int mode, int cmask, int t, int ur_cb, int dl_cb) {
+__device__ __forceinline__ TuP make_tup(int comp, int S, int tbc, int y, int x, int mode, int cmask, int t, int ur_cb,
+                                        int dl_cb) {
   TuP p;
-  const int size = C ? S >> 1 : S;
+  const int ch = comp != 0;
+  const int size = S >> ch;
   const int n = tbc ? size >> 1 : size;
   const int i0_ = tbc ? (t >> 1) * n : 0, j0_ = tbc ? (t & 1) * n : 0;
-  const int yp = C ? y >> 1 : y, xp = C ? x >> 1 : x;
-  constexpr int sbm = CompGeom<C>::SZ - 1;
+  const int yp = y >> ch, xp = x >> ch;
+  const int sbm = (64 >> ch) - 1;
   p.n = n;
   p.lg = ilog2i(n);
-  p.has = (cmask >> C) & 1;
+  p.has = (cmask >> comp) & 1;
   p.mode = mode;
   p.iy = (yp & sbm) + i0_;
   p.ix = (xp & sbm) + j0_;
@@ -271,162 +271,298 @@ __device__ __forceinline__ int p5f(int k, int n, int v0, int v1, int v2, int v3,
   return v0 + 2 * v1 + 2 * v2 + 2 * v3 + v4;
 }
 
-// Pixel (i, j) of mode M from the edge arrays (get_intra_prediction,
-// intra_prediction.c:363-388; directional modes :216-361 with their 1-2-1
-// pre-filters over n for 4 / 7 / 8 and over 2n for 5 / 6 and 9).
-template <int M>
-__device__ __forceinline__ int intra_px(const IntraChain &L, int tlF, int pTL, int dc, int i, int j) {
-  const uint8_t *ft = L.flt, *fl = L.flt + 128;
-  if (M == 1) return clip255((L.p5[64 + i] + L.p5[j] - pTL + 4) / 8);  // planar, C division
-  if (M == 2) return L.raw[128 + i];
-  if (M == 3) return L.raw[j];
-  if (M == 4) {
-    const int d = i - j;
-    return d > 0 ? fl[d - 1] : (d == 0 ? tlF : ft[-d - 1]);
+// Probe-only phase timers (built with -DINTRA_PROBE_TIMERS by tools/intra_probe.py).
+struct ProbeAcc {
+  unsigned long long sb, a, c, ntu;
+};
+#ifdef INTRA_PROBE_TIMERS
+#define PROBE_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROBE_ADD(field, from) (pa.field += __builtin_amdgcn_s_memtime() - (from))
+#else
+#define PROBE_T(v)
+#define PROBE_ADD(field, from)
+#endif
+
+// The neighbour samples of one transform block, read from the SB image with
+// make_top_and_left's rules (intra_prediction.c:57-143): 128 outside the
+// frame, the last available sample repeated past the up-right / down-left
+// availability (toplen / leftlen), indices clamped to the 2n edge.
+struct Edges {
+  int iw;            // image row bytes of the component
+  int tbase, lbase;  // byte offsets in L.img of image row -1 at the TU's x / column -1 at its y
+  int cnt;           // 2n
+  const TuP *p;
+  __device__ __forceinline__ int top(const IntraChain &L, int m) const {
+    m = m < 0 ? 0 : (m > cnt - 1 ? cnt - 1 : m);
+    m = m < p->toplen ? m : p->toplen - 1;
+    const int x = L.img[tbase + m];
+    return p->top_none ? 128 : x;
   }
-  if (M == 5) return ft[i + j + 1];
-  if (M == 6) {
-    const int d = i + 2 * j;
-    return (d & 1) ? ft[(d + 1) >> 1] : (ft[d >> 1] + ft[(d >> 1) + 1]) >> 1;
+  __device__ __forceinline__ int left(const IntraChain &L, int m) const {
+    m = m < 0 ? 0 : (m > cnt - 1 ? cnt - 1 : m);
+    m = m < p->leftlen ? m : p->leftlen - 1;
+    const int x = L.img[lbase + m * iw];
+    return p->left_none ? 128 : x;
   }
-  if (M == 7) {
-    const int d = i - 2 * j;
-    if (d > 1) return fl[d - 2];
-    if (d == 1) return tlF;
-    if (d == 0) return (tlF + ft[0]) >> 1;
-    const int h = (-d) >> 1;
-    return (d & 1) ? ft[h] : (ft[h] + ft[h - 1]) >> 1;
+  __device__ __forceinline__ int side(const IntraChain &L, bool is_left, int m) const {
+    return is_left ? left(L, m) : top(L, m);
   }
-  if (M == 8) {
-    const int d = 2 * i - j;
-    if (d < -1) return ft[-d - 2];
-    if (d == -1) return tlF;
-    if (d == 0) return (tlF + fl[0]) >> 1;
-    const int h = d >> 1;
-    return (d & 1) ? fl[h] : (fl[h] + fl[h - 1]) >> 1;
+};
+
+// Edge arrays of the directional modes in L.flt (one byte per sample):
+//   4 / 7 / 8: U[U_OFF+1+k] = left filtered over n, U[U_OFF-1-k] = top
+//              filtered over n, U[U_OFF] = the filtered top-left corner;
+//   5 / 6:     U[k] = top filtered over 2n;   9: U[k] = left filtered over 2n.
+// Planar keeps its 5-tap sums in L.p5 (top at 0, left at 64); H, V and DC
+// read the image directly / reduce to one value.
+#define U_OFF 64
+
+// Phase A of mode M: the mode's edge array, R samples per lane (2n <= 64R);
+// the DC sum of get_dc_pred(xpos!=0 ? left:top, ypos!=0 ? top:left)
+// (:145-160, :366) by DPP.  Returns DC.
+template <int M, int R>
+__device__ __forceinline__ int tu_edges(IntraChain &L, const TuP &p, const Edges &E) {
+  const int n = p.n, cnt = 2 * n;
+  int dcacc = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int q = threadIdx.x + 64 * r;
+    if (M == 5 || M == 6 || M == 9) {  // one side over 2n (:216-361's pre-filter over 2n)
+      const bool lft = M == 9;
+      const int a = E.side(L, lft, q - 1), b = E.side(L, lft, q), c = E.side(L, lft, q + 1);
+      if (q < cnt) L.flt[q] = (uint8_t)f121(q, cnt, a, b, c);
+    } else {  // both sides over n: q < n the top edge, n <= q < 2n the left
+      const bool lft = q >= n;
+      const int k = lft ? q - n : q;
+      if (M == 0) {
+        const int xs = p.xnz & 1;
+        const int w = lft ? xs + (!p.ynz) : (!xs) + p.ynz;
+        const int v = E.side(L, lft, k);
+        dcacc += q < cnt ? v * w : 0;
+      } else if (M == 1) {
+        const int v0 = E.side(L, lft, k - 2), v1 = E.side(L, lft, k - 1), v2 = E.side(L, lft, k);
+        const int v3 = E.side(L, lft, k + 1), v4 = E.side(L, lft, k + 2);
+        if (q < cnt) L.p5[lft ? 64 + k : k] = (int16_t)p5f(k, n, v0, v1, v2, v3, v4);
+      } else {  // 4, 7, 8
+        const int a = E.side(L, lft, k - 1), b = E.side(L, lft, k), c = E.side(L, lft, k + 1);
+        if (q < cnt) L.flt[lft ? U_OFF + 1 + k : U_OFF - 1 - k] = (uint8_t)f121(k, n, a, b, c);
+      }
+    }
   }
-  if (M == 9) {
-    const int d = 2 * i + j;
-    return (d & 1) ? fl[(d + 1) >> 1] : (fl[d >> 1] + fl[(d >> 1) + 1]) >> 1;
-  }
-  return dc;
+  return M == 0 ? (wave_sum(dcacc) + n) / (2 * n) : 0;
 }
 
-// Phase C: four horizontally adjacent pixels per lane and step: prediction +
-// residual, one dword into the image.
-template <int M, int C>
-__device__ __forceinline__ void intra_pred(IntraChain &L, const TuP &p, int tlF, int pTL, int dc) {
-  using G = CompGeom<C>;
-  uint8_t *img = L.img + G::IW + IMG_X0;
+// Prediction of 4 horizontally adjacent pixels (i, j..j+3) of mode M
+// (get_intra_prediction, intra_prediction.c:363-388; directional modes
+// :216-361 as index pairs into the edge array: value (U[a] + U[b]) >> 1, a == b
+// where the mode takes one sample).
+template <int M>
+__device__ __forceinline__ void pred4(const IntraChain &L, const TuP &p, int iw, const uint8_t *trow,
+                                      const uint8_t *lcol, int pTL, int dc, int i, int j, int pv[4]) {
+  const uint8_t *U = L.flt;
+  if (M == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; e++) pv[e] = dc;
+  } else if (M == 1) {  // planar, C division (:186-214)
+    const uint2 t = *(const uint2 *)&L.p5[j];
+    const int li = L.p5[64 + i] - pTL + 4;
+    pv[0] = clip255((li + (int)(int16_t)(t.x & 0xffff)) / 8);
+    pv[1] = clip255((li + (int)(int16_t)(t.x >> 16)) / 8);
+    pv[2] = clip255((li + (int)(int16_t)(t.y & 0xffff)) / 8);
+    pv[3] = clip255((li + (int)(int16_t)(t.y >> 16)) / 8);
+  } else if (M == 2) {  // horizontal: left[i]
+    const int x = lcol[i * iw];
+    const int v = p.left_none ? 128 : x;
+#pragma unroll
+    for (int e = 0; e < 4; e++) pv[e] = v;
+  } else if (M == 3) {  // vertical: top[j]
+    const uint32_t x = *(const uint32_t *)(trow + j);
+    const uint32_t w = p.top_none ? 0x80808080u : x;
+#pragma unroll
+    for (int e = 0; e < 4; e++) pv[e] = (w >> (8 * e)) & 255;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      int a, b;
+      if (M == 4) {
+        a = b = U_OFF + i - j - e;
+      } else if (M == 5) {
+        a = b = i + j + e + 1;
+      } else if (M == 6 || M == 9) {
+        const int d = M == 6 ? i + 2 * (j + e) : 2 * i + j + e;
+        a = (d + 1) >> 1;
+        b = (d >> 1) + 1;
+      } else if (M == 7) {
+        const int d = i - 2 * (j + e);
+        const int t = -d;
+        a = d >= 1 ? U_OFF + d - 1 : U_OFF - ((t + 1) >> 1);
+        b = d >= 1 ? U_OFF + d - 1 : U_OFF - (t >> 1) - 1;
+      } else {  // 8
+        const int d = 2 * i - (j + e);
+        a = d <= -1 ? U_OFF + d + 1 : U_OFF + ((d + 1) >> 1);
+        b = d <= -1 ? U_OFF + d + 1 : U_OFF + (d >> 1) + 1;
+      }
+      pv[e] = (M == 4 || M == 5) ? (int)U[a] : ((int)U[a] + (int)U[b]) >> 1;
+    }
+  }
+}
+
+// Phase C: 4 horizontally adjacent pixels per lane and step (prediction +
+// residual, one dword into the image).
+template <int M>
+__device__ __forceinline__ void tu_pred(IntraChain &L, const TuP &p, int iw, int sz, const uint8_t *trow,
+                                        const uint8_t *lcol, int pTL, int dc) {
   const int n = p.n, lgq = p.lg - 2, ng = (n * n) >> 2;
+  uint8_t *img = L.img + iw + IMG_X0;
   for (int g = threadIdx.x; g < ng; g += 64) {
     const int i = g >> lgq, j = (g & ((n >> 2) - 1)) << 2;
     uint2 rw = make_uint2(0, 0);
-    if (p.has) rw = *(const uint2 *)&L.res[(p.iy + i) * G::SZ + p.ix + j];
-    const int r[4] = {(int)(int16_t)(rw.x & 0xffff), (int)(int16_t)(rw.x >> 16), (int)(int16_t)(rw.y & 0xffff),
-                      (int)(int16_t)(rw.y >> 16)};
-    uint32_t o = 0;
-#pragma unroll
-    for (int e = 0; e < 4; e++) o |= put_byte(clip255(intra_px<M>(L, tlF, pTL, dc, i, j + e) + r[e]), e);
-    *(uint32_t *)(img + (p.iy + i) * G::IW + p.ix + j) = o;
+    if (p.has) rw = *(const uint2 *)&L.res[(p.iy + i) * sz + p.ix + j];
+    int pv[4];
+    pred4<M>(L, p, iw, trow, lcol, pTL, dc, i, j, pv);
+    *(uint32_t *)(img + (p.iy + i) * iw + p.ix + j) = put_byte(clip255(pv[0] + (int)(int16_t)(rw.x & 0xffff)), 0) |
+                                                      put_byte(clip255(pv[1] + (int)(int16_t)(rw.x >> 16)), 1) |
+                                                      put_byte(clip255(pv[2] + (int)(int16_t)(rw.y & 0xffff)), 2) |
+                                                      put_byte(clip255(pv[3] + (int)(int16_t)(rw.y >> 16)), 3);
   }
 }
 
-// One transform block.  Phase A builds the neighbour arrays the mode needs,
-// one edge sample per lane and step (samples 0..2n-1 the top edge, 2n..4n-1
-// the left edge, make_top_and_left's rules: 128 outside the frame, the last
-// available sample repeated past the up-right / down-left availability,
-// indices clamped to the 2n edge), the corner terms uniformly and the DC sum
-// by DPP; phase C predicts every pixel.  The SB reaches the frame once, when
-// the chain leaves it.
-template <int C>
-__device__ __forceinline__ void intra_tu(IntraChain &L, const TuP &p) {
-  using G = CompGeom<C>;
-  const int lane = threadIdx.x;
-  const uint8_t *img = L.img + G::IW + IMG_X0;
-  const uint8_t *trow = img + (p.iy - 1) * G::IW + p.ix, *lcol = img + p.iy * G::IW + p.ix - 1;
-  const int n = p.n, cnt = 2 * n, mode = p.mode;
-  const bool is_dc = mode == 0;
-  const int flen = (mode == 5 || mode == 6 || mode == 9) ? cnt : n;
-  const int tbase = (int)(trow - L.img), lbase = (int)(lcol - L.img);
-  int dcacc = 0;
-  for (int q = lane; q < 2 * cnt; q += 64) {
-    const int side = q >= cnt;
-    const int k = q - side * cnt;
-    const int len = side ? p.leftlen : p.toplen, none = side ? p.left_none : p.top_none;
-    const int step = side ? G::IW : 1;
-    const int base = side ? lbase : tbase;
-    int v[5];
-#pragma unroll
-    for (int o = 0; o < 5; o++) {
-      int m = k - 2 + o;
-      m = m < 0 ? 0 : (m > cnt - 1 ? cnt - 1 : m);
-      m = m < len ? m : len - 1;
-      const int x = L.img[base + m * step];
-      v[o] = none ? 128 : x;
-    }
-    L.raw[128 * side + k] = (uint8_t)v[2];
-    // the one pre-filter this mode reads: 1-2-1 over n (4, 7, 8), over 2n of
-    // the top (5, 6) or of the left (9); planar 5-tap; DC sum
-    const bool want_f = (mode == 4 || mode == 7 || mode == 8) ? k < n
-                        : ((mode == 5 || mode == 6) ? !side : (mode == 9 ? (bool)side : false));
-    if (want_f) L.flt[128 * side + k] = (uint8_t)f121(k, flen, v[1], v[2], v[3]);
-    if (mode == 1 && k < n) L.p5[64 * side + k] = (int16_t)p5f(k, n, v[0], v[1], v[2], v[3], v[4]);
-    if (is_dc && k < n) {
-      // DC sum of get_dc_pred(xpos!=0 ? left:top, ypos!=0 ? top:left), :145-160, :366
-      const int xs = p.xnz & 1;
-      const int w = side ? xs + (!p.ynz) : (!xs) + p.ynz;
-      dcacc += v[2] * w;
-    }
-  }
-  int tlF = 0, pTL = 0, dc = 0;
-  if (mode == 1 || mode == 4 || mode == 7 || mode == 8) {  // corner terms (:77-99, :186-189), uniform
-    auto T = [&](int m) { return p.top_none ? 128 : (int)trow[m < p.toplen ? m : p.toplen - 1]; };
-    auto Lf = [&](int m) { return p.left_none ? 128 : (int)lcol[(m < p.leftlen ? m : p.leftlen - 1) * G::IW]; };
+// One transform block of mode M: phase A (the mode's edge array, corner
+// terms), phase C (every pixel).  LDS operations of the wave complete in
+// order, so the phases only need compiler ordering.
+template <int M>
+__device__ __forceinline__ void tu_mode(IntraChain &L, const TuP &p, int iw, int sz, ProbeAcc &pa) {
+  PROBE_T(ta0);
+  const uint8_t *img = L.img + iw + IMG_X0;
+  const uint8_t *trow = img + (p.iy - 1) * iw + p.ix, *lcol = img + p.iy * iw + p.ix - 1;
+  Edges E;
+  E.iw = iw;
+  E.tbase = (int)(trow - L.img);
+  E.lbase = (int)(lcol - L.img);
+  E.cnt = 2 * p.n;
+  E.p = &p;
+  int dc = 0, pTL = 0;
+  if (M != 2 && M != 3) dc = p.n == 64 ? tu_edges<M, 2>(L, p, E) : tu_edges<M, 1>(L, p, E);
+  if (M == 1 || M == 4 || M == 7 || M == 8) {  // corner terms (:77-99, :186-189), uniform
     int tl = p.top_none ? 128 : ((p.xnz & 2) ? trow[-1] : trow[0]);
     if (p.top_none) tl = p.left_none ? 128 : lcol[0];  // ypos+i==0: top_left = left[0]
-    const int t0 = T(0), l0 = Lf(0);
-    tlF = __builtin_amdgcn_readfirstlane((2 * tl + l0 + t0 + 2) >> 2);
-    pTL = __builtin_amdgcn_readfirstlane(Lf(1) + 2 * l0 + 2 * tl + 2 * t0 + T(1));
+    const int t0 = E.top(L, 0), l0 = E.left(L, 0);
+    if (M == 1) pTL = __builtin_amdgcn_readfirstlane(E.left(L, 1) + 2 * l0 + 2 * tl + 2 * t0 + E.top(L, 1));
+    else if (threadIdx.x == 0) L.flt[U_OFF] = (uint8_t)((2 * tl + l0 + t0 + 2) >> 2);
   }
-  if (is_dc) dc = (wave_sum(dcacc) + n) / (2 * n);
   wave_lds_sync();
-  switch (mode) {  // uniform
-    case 1: intra_pred<1, C>(L, p, tlF, pTL, dc); break;
-    case 2: intra_pred<2, C>(L, p, tlF, pTL, dc); break;
-    case 3: intra_pred<3, C>(L, p, tlF, pTL, dc); break;
-    case 4: intra_pred<4, C>(L, p, tlF, pTL, dc); break;
-    case 5: intra_pred<5, C>(L, p, tlF, pTL, dc); break;
-    case 6: intra_pred<6, C>(L, p, tlF, pTL, dc); break;
-    case 7: intra_pred<7, C>(L, p, tlF, pTL, dc); break;
-    case 8: intra_pred<8, C>(L, p, tlF, pTL, dc); break;
-    case 9: intra_pred<9, C>(L, p, tlF, pTL, dc); break;
-    default: intra_pred<0, C>(L, p, tlF, pTL, dc); break;
-  }
+  PROBE_ADD(a, ta0);
+  PROBE_T(tc0);
+  tu_pred<M>(L, p, iw, sz, trow, lcol, pTL, dc);
   wave_lds_sync();  // the next TU reads these pixels (and rewrites the edge arrays)
+  PROBE_ADD(c, tc0);
+  (void)pa;
 }
 
-// One chain: component C of SB row `row`; its ncu intra CUs' words are staged
-// in g_cuw[0 .. ncu).
-template <int C>
-__device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, int ncu, unsigned *ctl, unsigned *progress,
-                                          int row, int full, const int16_t *__restrict__ resid, int dbg_flags) {
+__device__ __forceinline__ void intra_tu(IntraChain &L, const TuP &p, int iw, int sz, ProbeAcc &pa) {
+  switch (p.mode) {  // uniform
+    case 1: tu_mode<1>(L, p, iw, sz, pa); break;
+    case 2: tu_mode<2>(L, p, iw, sz, pa); break;
+    case 3: tu_mode<3>(L, p, iw, sz, pa); break;
+    case 4: tu_mode<4>(L, p, iw, sz, pa); break;
+    case 5: tu_mode<5>(L, p, iw, sz, pa); break;
+    case 6: tu_mode<6>(L, p, iw, sz, pa); break;
+    case 7: tu_mode<7>(L, p, iw, sz, pa); break;
+    case 8: tu_mode<8>(L, p, iw, sz, pa); break;
+    case 9: tu_mode<9>(L, p, iw, sz, pa); break;
+    default: tu_mode<0>(L, p, iw, sz, pa); break;
+  }
+}
+
+// What a chain needs to move between SBs (uniform).
+struct ChainCtx {
+  __amdgpu_buffer_rsrc_t fr, rr, eb;  // current frame slot, residual plane, edge rows
+  int pofs, stride, pw, ew, row, nsbw, full, dbg_flags;
+  unsigned *my, *ctl;
+  const unsigned *above;
+};
+
+// The chain enters SB l (component class CH: 0 luma, 1 chroma): flush +
+// publish the SB left behind, issue the loads with no dependency (residual,
+// FULL interior), store the old image, wait for the row above, then the
+// edge row.
+template <int CH>
+__device__ __forceinline__ void sb_enter(IntraChain &L, const ChainCtx &k, int l, int &cur_sb, int &seen,
+                                         unsigned long long &tw) {
+  const bool from_prev = cur_sb == l - 1;
+  if (cur_sb >= 0) publish_sb<CH>(L, k.eb, k.ew, k.row, cur_sb, k.my, (unsigned)l);
+  ResLoad<CH> res;
+  res.issue(k.rr, k.pw, k.row, l);
+  ImgLoad<CH, true> imf;
+  ImgLoad<CH, false> imn;
+  if (k.full) imf.issue_interior(k.fr, k.pofs, k.stride, k.row, l, from_prev);
+  if (cur_sb >= 0) store_sb<CH>(L, k.fr, k.pofs, k.stride, k.row, cur_sb);
+  int need = l + 2 < k.nsbw ? l + 2 : k.nsbw;
+  if (k.dbg_flags & 1) need = 0;  // debug: ignore the wavefront dependency (wrong pixels)
+  if (seen < need) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    int v = (int)__builtin_amdgcn_readfirstlane(ld_progress(k.above));
+    unsigned spins = 0;
+    while (v < need) {
+      __builtin_amdgcn_s_sleep(1);
+      v = (int)__builtin_amdgcn_readfirstlane(ld_progress(k.above));
+      if (++spins > (1u << 27)) {
+        if (threadIdx.x == 0) atomicOr(&k.ctl[1], 1u);
+        break;
+      }
+    }
+    seen = v;
+    tw += __builtin_amdgcn_s_memtime() - t0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 edge loads below the poll
+  if (k.full) {
+    imf.issue_edge(k.eb, k.ew, k.row, l);
+    imf.commit(L, from_prev);
+  } else {
+    imn.issue_edge(k.eb, k.ew, k.row, l);
+    imn.commit(L, from_prev);
+  }
+  res.commit(L);
+  wave_lds_sync();
+  cur_sb = l;
+}
+template <int CH>
+__device__ __forceinline__ void sb_leave(IntraChain &L, const ChainCtx &k, int cur_sb) {
+  publish_sb<CH>(L, k.eb, k.ew, k.row, cur_sb, k.my, 0x7fffffffu);
+  store_sb<CH>(L, k.fr, k.pofs, k.stride, k.row, cur_sb);
+}
+
+// One chain: component comp of SB row `row`; its ncu intra CUs' words are
+// staged in g_cuw[0 .. ncu).  The transform-block code is shared by the
+// three components (one copy in the instruction cache).
+__device__ __forceinline__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, int comp, int ncu,
+                                                          unsigned *ctl, unsigned *progress, int row, int full,
+                                                          const int16_t *__restrict__ resid, int dbg_flags,
+                                                          ProbeAcc &pa) {
   unsigned long long tw = 0;  // ticks spent waiting on the row above (debug)
-  const int lane = threadIdx.x;
-  uint8_t *const plane = C == 0 ? f.cy : (C == 1 ? f.cu : f.cv);
-  const int stride = C ? f.sc : f.sy;
-  const int pw = C ? f.W >> 1 : f.W, ph = C ? f.H >> 1 : f.H;
-  const int16_t *rplane = resid + (C == 0 ? 0 : (long long)f.W * f.H + (C == 2 ? (long long)pw * ph : 0));
+  const int ch = comp != 0;
+  uint8_t *const plane = comp == 0 ? f.cy : (comp == 1 ? f.cu : f.cv);
+  const int pw = f.W >> ch, ph = f.H >> ch;
+  const int16_t *rplane = resid + (comp == 0 ? 0 : (long long)f.W * f.H + (comp == 2 ? (long long)pw * ph : 0));
   const uint8_t *slot = f.cy - f.offy;  // the current frame's ring slot
-  const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc((void *)slot, 0, (int)f.slot_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)rplane, 0, 2 * pw * ph, 0x00020000);
-  const int pofs = (int)(plane - slot);
-  const int ew = C ? f.ewc : f.ewy;
-  const uint8_t *ebase = f.edge + (C == 0 ? 0 : (long long)f.nsbrows * f.ewy + (C == 2 ? (long long)f.nsbrows * f.ewc : 0));
-  const __amdgpu_buffer_rsrc_t eb = __builtin_amdgcn_make_buffer_rsrc((void *)ebase, 0, f.nsbrows * ew, 0x00020000);
-  const int nsbw = (f.W + 63) >> 6;
-  unsigned *my = progress + 3 * row + C;
-  const unsigned *above = progress + 3 * (row - 1) + C;
+  ChainCtx k;
+  k.fr = __builtin_amdgcn_make_buffer_rsrc((void *)slot, 0, (int)f.slot_bytes, 0x00020000);
+  k.rr = __builtin_amdgcn_make_buffer_rsrc((void *)rplane, 0, 2 * pw * ph, 0x00020000);
+  k.pofs = (int)(plane - slot);
+  k.stride = ch ? f.sc : f.sy;
+  k.pw = pw;
+  k.ew = ch ? f.ewc : f.ewy;
+  const uint8_t *ebase =
+      f.edge + (comp == 0 ? 0 : (long long)f.nsbrows * f.ewy + (comp == 2 ? (long long)f.nsbrows * f.ewc : 0));
+  k.eb = __builtin_amdgcn_make_buffer_rsrc((void *)ebase, 0, f.nsbrows * k.ew, 0x00020000);
+  k.row = row;
+  k.nsbw = (f.W + 63) >> 6;
+  k.full = full;
+  k.dbg_flags = dbg_flags;
+  k.my = progress + 3 * row + comp;
+  k.ctl = ctl;
+  k.above = progress + 3 * (row - 1) + comp;
+  const int iw = ch ? CompGeom<1>::IW : CompGeom<0>::IW, sz = 64 >> ch;
   int seen = row == 0 ? 0x7fffffff : 0, cur_sb = -2;
   uint2 wn = ncu > 0 ? g_cuw[0] : make_uint2(0, 0);
   for (int it = 0; it < ncu; it++) {
@@ -436,54 +572,24 @@ __device__ unsigned long long intra_chain(IntraChain &L, const FrameCtx &f, int 
     const int cmask = (w1 >> 13) & 7, ur_cb = (w1 >> 16) & 1, dl_cb = (w1 >> 17) & 1;
     const int l = x >> 6;
     if (l != cur_sb) {
-      // SB transition: flush + publish the SB left behind, loads with no
-      // dependency (residual, FULL interior), wait for the row above, edge row
-      const bool from_prev = cur_sb == l - 1;
-      if (cur_sb >= 0) publish_sb<C>(L, eb, ew, row, cur_sb, my, (unsigned)l);
-      ResLoad<C> res;
-      res.issue(rr, pw, row, l);
-      ImgLoad<C, true> imf;
-      ImgLoad<C, false> imn;
-      if (full) imf.issue_interior(fr, pofs, stride, row, l, from_prev);
-      if (cur_sb >= 0) store_sb<C>(L, fr, pofs, stride, row, cur_sb);
-      int need = l + 2 < nsbw ? l + 2 : nsbw;
-      if (dbg_flags & 1) need = 0;  // debug: ignore the wavefront dependency (wrong pixels)
-      if (seen < need) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        int v = (int)__builtin_amdgcn_readfirstlane(ld_progress(above));
-        unsigned spins = 0;
-        while (v < need) {
-          __builtin_amdgcn_s_sleep(1);
-          v = (int)__builtin_amdgcn_readfirstlane(ld_progress(above));
-          if (++spins > (1u << 27)) {
-            if (lane == 0) atomicOr(&ctl[1], 1u);
-            break;
-          }
-        }
-        seen = v;
-        tw += __builtin_amdgcn_s_memtime() - t0;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 edge loads below the poll
-      if (full) {
-        imf.issue_edge(eb, ew, row, l);
-        imf.commit(L, from_prev);
-      } else {
-        imn.issue_edge(eb, ew, row, l);
-        imn.commit(L, from_prev);
-      }
-      res.commit(L);
-      wave_lds_sync();
-      cur_sb = l;
+      PROBE_T(ts0);
+      if (ch) sb_enter<1>(L, k, l, cur_sb, seen, tw);
+      else sb_enter<0>(L, k, l, cur_sb, seen, tw);
+      PROBE_ADD(sb, ts0);
     }
-    const int tbc = C == 0 ? tb : (tb && S > 8);
+    const int tbc = ch ? (tb && S > 8) : tb;
     const int nsteps = tbc ? 4 : 1;
-    for (int t = 0; t < nsteps; t++) intra_tu<C>(L, make_tup<C>(S, tbc, y, x, mode, cmask, t, ur_cb, dl_cb));
+    for (int t = 0; t < nsteps; t++)
+      intra_tu(L, make_tup(comp, S, tbc, y, x, mode, cmask, t, ur_cb, dl_cb), iw, sz, pa);
+#ifdef INTRA_PROBE_TIMERS
+    pa.ntu += nsteps;
+#endif
   }
   if (cur_sb >= 0) {
-    publish_sb<C>(L, eb, ew, row, cur_sb, my, 0x7fffffffu);
-    store_sb<C>(L, fr, pofs, stride, row, cur_sb);
-  } else if (lane == 0) {
-    __hip_atomic_store(my, 0x7fffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ch) sb_leave<1>(L, k, cur_sb);
+    else sb_leave<0>(L, k, cur_sb);
+  } else if (threadIdx.x == 0) {
+    __hip_atomic_store(k.my, 0x7fffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return tw;
 }
@@ -535,15 +641,18 @@ __global__ __launch_bounds__(64) void k_intra(FrameCtx f, const thor_block_t *__
     }
     wave_lds_sync();
     unsigned long long tw;
-    if (c == 0) tw = intra_chain<0>(L, f, ncu, ctl, progress, row, full_sb, resid, dbg_flags);
-    else if (c == 1) tw = intra_chain<1>(L, f, ncu, ctl, progress, row, full_sb, resid, dbg_flags);
-    else tw = intra_chain<2>(L, f, ncu, ctl, progress, row, full_sb, resid, dbg_flags);
+    ProbeAcc pa = {0, 0, 0, 0};
+    tw = intra_chain(L, f, c, ncu, ctl, progress, row, full_sb, resid, dbg_flags, pa);
     if (dbg && lane == 0) {
       unsigned long long *o = dbg + 16 * task;
       o[0] = t0;
       o[1] = __builtin_amdgcn_s_memtime();
       o[2] = tw;
       o[3] = (unsigned long long)ncu;
+      o[4] = pa.sb;
+      o[5] = pa.a;
+      o[6] = pa.c;
+      o[7] = pa.ntu;
     }
     wave_lds_sync();  // the next task restages g_cuw
   }

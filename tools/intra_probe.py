@@ -33,8 +33,9 @@ for flags in [int(v) for v in os.environ.get("PROBE_FLAGS", "0,1,5").split(",")]
         r, c = divmod(task, 3)
         if r % 6 and r != nrows - 1:
             continue
-        print("  row %2d comp %d busy %9.0f wait %9.0f cus %d ticks/cu %.0f | sb: %d x %.0f (incl wait)  tu: %d x %.0f" % (
-            r, c, h[task, 1] - h[task, 0], h[task, 2], h[task, 3],
-            (h[task, 1] - h[task, 0] - h[task, 2]) / max(1, h[task, 3]),
-            h[task, 6], h[task, 4] / max(1, h[task, 6]), h[task, 7], h[task, 5] / max(1, h[task, 7])))
+        busy = h[task, 1] - h[task, 0]
+        print("  row %2d comp %d busy %9.0f wait %9.0f cus %d tus %d | per TU: sb %.0f A %.0f C %.0f other %.0f" % (
+            r, c, busy, h[task, 2], h[task, 3], h[task, 7], h[task, 4] / max(1, h[task, 7]),
+            h[task, 5] / max(1, h[task, 7]), h[task, 6] / max(1, h[task, 7]),
+            (busy - h[task, 4] - h[task, 5] - h[task, 6]) / max(1, h[task, 7])))
 lib.thor_dec_debug_intra(dec.h, None, 0)
