@@ -125,6 +125,40 @@ void *thor_dec_stream(thor_dec_t *d);
 /* Set the stream (e.g. torch's current stream); NULL = the context's own. */
 int thor_dec_set_stream(thor_dec_t *d, void *stream);
 
+/* ---- batched encoder transform-block chain ----------------------------- *
+ * One descriptor per transform block (TU) of an RD candidate.  The chain is
+ * encode_and_reconstruct_block_inter / _intra's per-TU body
+ * (enc/encode_block.c:1434-1518): get_residual (:484-493) -> transform
+ * (common/transform.c:249-330) -> quantize (enc/encode_block.c:75-172,
+ * rdoq 0) -> [cbp] dequantize + inverse_transform (common/common_block.c:
+ * 132-146, common/transform.c:432-518) -> reconstruct_block
+ * (common/common_block.c:148-156) or rec = pred -> SSD(orig, rec).
+ * 32 bytes, naturally aligned. */
+typedef struct thor_enc_tu {
+  int32_t orig_off;    /* byte offset of the TU's (0,0) in `orig`             */
+  int32_t pred_off;    /* byte offset of the TU's (0,0) in `pred`             */
+  int32_t rec_off;     /* byte offset of the TU's (0,0) in `rec`              */
+  int32_t coeff_off;   /* int16 offset of the TU's q x q level tile in `coeffq`
+                          (q = min(size,16), the compact pool layout above)   */
+  int32_t orig_stride, pred_stride, rec_stride;
+  uint8_t size;        /* 4, 8, 16, 32 or 64                                   */
+  uint8_t qp;          /* component qp (chroma: chroma_qp[qp], common/common_block.c:78-83) */
+  uint8_t type;        /* coeff_block_type: bit1 intra, bit0 chroma (enc/encode_block.c:77-78) */
+  uint8_t fast;        /* transform `fast` flag       */
+} thor_enc_tu_t;
+
+/* Run the chain for `n` TUs (all pointers DEVICE pointers).  Per TU: the q x q
+ * quantised levels into coeffq, cbp (0/1; 255 = invalid descriptor) and the
+ * TU's SSD(orig, rec).  Enqueued on `stream` (hipStream_t, NULL = default). */
+int thor_enc_tu_batch(const thor_enc_tu_t *tus, int n, const uint8_t *orig, const uint8_t *pred, uint8_t *rec,
+                      int16_t *coeffq, uint8_t *cbp, uint32_t *ssd, void *stream);
+
+/* cost_calc (enc/encode_block.c:1218-1228) for `ncu` candidates: the SSDs of
+ * TUs tu_first[c] .. tu_first[c]+tu_count[c]-1 (Y, U and V TUs of the CU)
+ * plus (int32)(lambda * nbits[c] + 0.5), clamped to 2^30.  DEVICE pointers. */
+int thor_enc_cost_batch(const uint32_t *ssd, const int32_t *tu_first, const int32_t *tu_count, const int32_t *nbits,
+                        double lambda, uint32_t *cost, int ncu, void *stream);
+
 /* ---- device memory helpers (so the C-ABI is usable without torch) ------ */
 void *thor_dev_alloc(size_t bytes);
 int thor_dev_free(void *p);

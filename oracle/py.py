@@ -53,6 +53,8 @@ def load(build: bool = True):
     _lib.or_dequantize.argtypes = [P, P, i, i]
     _lib.or_inverse_transform.argtypes = [P, P, i]
     _lib.or_transform.argtypes = [P, P, i, i]
+    _lib.or_encode_tu.argtypes = [P, i, P, i, P, i, i, i, i, i, P, P]
+    _lib.or_encode_tu.restype = i
     _lib.or_quantize.argtypes = [P, P, i, i, i]
     _lib.or_quantize.restype = i
     _lib.or_reconstruct_block.argtypes = [P, P, P, i, i]

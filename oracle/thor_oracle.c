@@ -861,3 +861,39 @@ int or_decode_frame(const thor_seq_t *seq, const thor_frame_hdr_t *hdr, or_frame
   free(pb);
   return err;
 }
+
+/* One transform block of an RD candidate, as encode_and_reconstruct_block_inter
+ * / _intra run it per TU (enc/encode_block.c:1434-1518): get_residual
+ * (:484-493), transform, quantize (rdoq 0), then dequantize + inverse_transform
+ * + reconstruct_block if cbp, else rec = pred (:1512-1517).  Writes the q x q
+ * levels compact (q = min(size,16)) and returns cbp; *ssd = SSD(orig, rec)
+ * (ssd_calc, :783-797). */
+int or_encode_tu(const uint8_t *orig, int os, const uint8_t *pred, int ps, uint8_t *rec, int rs, int size, int qp,
+                 int type, int fast, int16_t *levels, uint32_t *ssd) {
+  int16_t res[64 * 64], coeff[64 * 64], coeffq[64 * 64], rco[64 * 64], rblk[64 * 64];
+  uint8_t pb[64 * 64];
+  int q = MIN(size, 16);
+  for (int i = 0; i < size; i++)
+    for (int j = 0; j < size; j++) {
+      res[i * size + j] = (int16_t)(orig[i * os + j] - pred[i * ps + j]);
+      pb[i * size + j] = pred[i * ps + j];
+    }
+  memset(coeff, 0, sizeof(coeff));
+  memset(coeffq, 0, sizeof(coeffq));
+  or_transform(res, coeff, size, fast);
+  int cbp = or_quantize(coeff, coeffq, qp, size, type);
+  for (int i = 0; i < q; i++)
+    for (int j = 0; j < q; j++) levels[i * q + j] = coeffq[i * size + j];
+  uint8_t out[64 * 64];
+  if (cbp) {
+    or_dequantize(coeffq, rco, qp, size);
+    or_inverse_transform(rco, rblk, size);
+    or_reconstruct_block(rblk, pb, out, size, size);
+  } else {
+    memcpy(out, pb, (size_t)size * size);
+  }
+  for (int i = 0; i < size; i++)
+    for (int j = 0; j < size; j++) rec[i * rs + j] = out[i * size + j];
+  *ssd = or_ssd(orig, out, os, size, size, size);
+  return cbp;
+}

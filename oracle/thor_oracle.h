@@ -38,6 +38,9 @@ void or_clpf_block(const uint8_t *src, uint8_t *dst, int sstride, int dstride, i
 uint32_t or_sad(const uint8_t *a, const uint8_t *b, int astride, int bstride, int width, int height);
 uint32_t or_ssd(const uint8_t *a, const uint8_t *b, int astride, int bstride, int width, int height);
 
+int or_encode_tu(const uint8_t *orig, int os, const uint8_t *pred, int ps, uint8_t *rec, int rs, int size, int qp,
+                 int type, int fast, int16_t *levels, uint32_t *ssd);
+
 /* ---- frames ------------------------------------------------------------- */
 typedef struct or_frame {
   uint8_t *y, *u, *v; /* interior (0,0) pointers of padded planes */

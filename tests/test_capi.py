@@ -23,6 +23,11 @@ def test_library_loads_and_exports_batched_api():
         assert hasattr(lib, name), name
     for name in L.BATCHED_SYMBOLS:
         assert hasattr(lib, name), name
+    # the reference's SIMD kernel surface (common/common_kernels.h:31-41, enc/enc_kernels.h:32-37)
+    declared = _declared("thor_kernels.h")
+    assert set(declared) == set(L.SIMD_SURFACE_SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), name
     assert b"gfx950" in lib.thor_version()
 
 

@@ -126,3 +126,23 @@ def test_clpf_block(lib):
         lib.or_clpf_block(ptr(src), ptr(dst), 128, sb, x0, y0, size, 128, 128)
         l, t = x0 & ~(sb - 1), y0 & ~(sb - 1)
         assert np.array_equal(dst[y0 - t:y0 - t + size, x0 - l:x0 - l + size], want)
+
+
+def test_encoder_tu_chain(lib):
+    """or_encode_tu against the reference's own functions composed as
+    encode_and_reconstruct_block_inter (tests/golden/enc_tu.npz)."""
+    E = np.load(os.path.join(GOLD, "enc_tu.npz"))
+    for k, (size, qp, typ, fast, cbp) in enumerate(E["enc_meta"]):
+        size = int(size)
+        q = min(size, 16)
+        org = np.ascontiguousarray(E["enc_orig"][k])
+        pb = np.ascontiguousarray(E["enc_pred"][k])
+        rec = np.zeros((64, 64), np.uint8)
+        lv = np.zeros(q * q, np.int16)
+        ssd = C.c_uint32()
+        c = lib.or_encode_tu(ptr(org), 64, ptr(pb), 64, ptr(rec), 64, size, int(qp), int(typ), int(fast), ptr(lv),
+                             C.byref(ssd))
+        assert c == cbp, k
+        assert np.array_equal(lv.reshape(q, q), E["enc_levels"][k][:q, :q]), k
+        assert np.array_equal(rec[:size, :size], E["enc_rec"][k][:size, :size]), k
+        assert ssd.value == E["enc_ssd"][k], k

@@ -25,6 +25,7 @@ class ThorFrameHdr(C.Structure):
 BATCHED_SYMBOLS = [
     "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_build_intra_list", "thor_dec_set_stop_stage",
     "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
+    "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
 SIMD_SURFACE_SYMBOLS = [
@@ -71,6 +72,31 @@ def load(path: str = LIB_PATH):
     L.thor_dec_set_timing.argtypes = [P, i]
     L.thor_dec_stage_ms.argtypes = [P, C.POINTER(C.c_double), i]
     L.thor_dec_stage_ms.restype = i
+    L.thor_enc_tu_batch.argtypes = [P, i, P, P, P, P, P, P, P]
+    L.thor_enc_tu_batch.restype = i
+    L.thor_enc_cost_batch.argtypes = [P, P, P, P, C.c_double, P, i, P]
+    L.thor_enc_cost_batch.restype = i
+    # the reference's SIMD kernel surface (include/thor_kernels.h)
+    u8p = P
+    L.transform_simd.argtypes = [P, P, i, i]
+    L.inverse_transform_simd.argtypes = [P, P, i]
+    L.block_avg_simd.argtypes = [P, P, P, i, i, i, i, i]
+    L.sad_calc_simd_unaligned.argtypes = [P, P, i, i, i, i]
+    L.sad_calc_simd_unaligned.restype = i
+    L.sad_calc_simd.argtypes = [P, P, i, i, i, i]
+    L.sad_calc_simd.restype = i
+    L.ssd_calc_simd.argtypes = [P, P, i, i, i]
+    L.ssd_calc_simd.restype = i
+    L.widesad_calc_simd.argtypes = [P, P, i, i, i, i, C.POINTER(C.c_int)]
+    L.widesad_calc_simd.restype = C.c_uint
+    for n in ("sad_calc_fasthalf_simd", "sad_calc_fastquarter_simd"):
+        getattr(L, n).argtypes = [P, P, i, i, i, i, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        getattr(L, n).restype = C.c_uint
+    L.detect_clpf_simd.argtypes = [P, P, i, i, i, i, i, i, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.clpf_block4.argtypes = [u8p, u8p, i, i, i, i, i, i]
+    L.clpf_block8.argtypes = [u8p, u8p, i, i, i, i, i, i]
+    L.get_inter_prediction_luma_simd.argtypes = [i, i, i, i, P, i, P, i, i]
+    L.get_inter_prediction_chroma_simd.argtypes = [i, i, i, i, P, i, P, i]
     L.thor_dev_alloc.argtypes = [C.c_size_t]
     L.thor_dev_alloc.restype = P
     L.thor_dev_free.argtypes = [P]
