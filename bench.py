@@ -38,31 +38,27 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 STAGES = ["prep", "inter", "intra", "deblock", "clpf", "pad"]
 
 
-def inter_alg_bytes(frames) -> float:
-    """Algorithmic HBM bytes of the inter-reconstruction kernel over a pass of
-    the stream (BASELINE.md 'Algorithmic bytes'):
-    per inter-reconstructed pixel 1.5 B reference read (x2 bi-pred) + 1.5 B
-    reconstruction write (4:2:0, luma px counted, chroma folded into the 1.5),
-    + 2 B per coded coefficient slot read, + 72 B per descriptor read."""
-    total = 0.0
-    for fr in frames:
-        b = fr.blocks
-        inter = b["mode"] != 1
-        px = b["bwidth"].astype(np.float64) * b["bheight"].astype(np.float64)
-        bi = (b["mode"] == 3) | (((b["mode"] == 0) | (b["mode"] == 4)) & (b["dir"] == 2))
-        ref = 1.5 * px * np.where(bi, 2.0, 1.0)
-        total += float(np.sum((ref + 1.5 * px)[inter]))
-        total += 72.0 * float(np.count_nonzero(inter))
-        # coefficient slots of inter CUs
-        for c in range(3):
-            has = inter & ((b["coeff_mask"] >> c) & 1).astype(bool)
-            S = b["size"].astype(np.int64)
-            n = S if c == 0 else S // 2
-            tbs = b["tb_split"].astype(bool) if c == 0 else (b["tb_split"].astype(bool) & (S > 8))
-            nt = np.where(tbs, n // 2, n)
-            q = np.minimum(nt, 16)
-            slots = np.where(tbs, 4 * q * q, q * q)
-            total += 2.0 * float(np.sum(slots[has]))
+def recon_alg_bytes(fr, width: int, height: int) -> float:
+    """Algorithmic HBM bytes of one k_recon launch (the inter-reconstruction
+    kernel) on frame `fr`: per inter-predicted luma px
+    1.5 B reference read (4:2:0, chroma folded in; x2 bi-pred) + 1.5 B
+    reconstruction write; + the int16 residual read where the CU component is
+    coded (2 B per luma px for Y, 2 B per chroma px for U and V); + 72 B per
+    inter CU descriptor; + one 4 B cell-map word per 8x8 luma unit of the
+    frame.  Halo re-reads and LDS staging are not counted."""
+    b = fr.blocks
+    inter = b["mode"] != 1
+    w = b["bwidth"].astype(np.float64)
+    h = b["bheight"].astype(np.float64)
+    px = np.where(b["mode"] == 0, w * h, b["size"].astype(np.float64) ** 2)
+    bi = (b["mode"] == 3) | (((b["mode"] == 0) | (b["mode"] == 4)) & (b["dir"] == 2))
+    total = float(np.sum((1.5 * px * np.where(bi, 2.0, 1.0) + 1.5 * px)[inter]))
+    total += 72.0 * float(np.count_nonzero(inter))
+    coded = inter & (b["mode"] != 0)
+    for c in range(3):
+        has = coded & ((b["coeff_mask"] >> c) & 1).astype(bool)
+        total += 2.0 * float(np.sum((px if c == 0 else px / 4.0)[has]))
+    total += 4.0 * (width * height / 64.0)
     return total
 
 
@@ -104,7 +100,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per inter launch (profiles/)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per k_recon launch (default profiles/traffic_latest.json)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -150,8 +147,9 @@ def main():
 
     lib = L.load()
     lib.thor_dec_set_timing(dec.h, 1)
-    ms = (C.c_double * 6)()
-    lib.thor_dec_stage_ms(dec.h, ms, 6)  # reset accumulators
+    cap = 8 * len(frames) * (a.steps + 1)
+    mk_stage, mk_ms = (C.c_int * cap)(), (C.c_double * cap)()
+    lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)  # drop the warmup marks
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(local)
@@ -160,8 +158,20 @@ def main():
         step()
     torch.cuda.synchronize(local)
     elapsed = time.perf_counter() - t0
-    lib.thor_dec_stage_ms(dec.h, ms, 6)
-    stage_ms = [ms[i] / a.steps for i in range(6)]  # per step (whole stream)
+    nm = lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)
+    # attribute the marks to frames: every frame opens with its side-info stage (0)
+    per_frame, cur = [], None
+    for k in range(nm):
+        if mk_stage[k] == 0:
+            cur = [0.0] * 6
+            per_frame.append(cur)
+        cur[mk_stage[k]] += mk_ms[k]
+    assert len(per_frame) == a.steps * len(frames), (len(per_frame), a.steps, len(frames))
+    stage_ms = [sum(f[i] for f in per_frame) / a.steps for i in range(6)]  # per step (whole stream)
+    # k_recon roofline over the P frames (the I frame has no inter pixels)
+    pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]
+    recon_ms = sum(per_frame[s * len(frames) + i][1] for s in range(a.steps) for i in pidx) / (a.steps * len(pidx))
+    alg = sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -174,12 +184,11 @@ def main():
     value = world * px_step * a.steps / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
 
-    alg = inter_alg_bytes(frames)  # per step (all frames)
-    inter_ms = stage_ms[1]
-    achieved = alg / (inter_ms / 1e3) / 1e9 if inter_ms > 0 else 0.0
+    achieved = alg / (recon_ms / 1e3) / 1e9 if recon_ms > 0 else 0.0
     traffic = None
-    if a.traffic_json and os.path.exists(a.traffic_json):
-        traffic = json.load(open(a.traffic_json)).get("inter_hbm_bytes_per_launch")
+    tj = a.traffic_json or os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tj):
+        traffic = json.load(open(tj)).get("recon_hbm_bytes_per_p_launch")
 
     if rank == 0:
         out = {
@@ -209,14 +218,15 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_inter",
+                "kernel": "k_recon",
                 "achieved": round(achieved, 1),
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic,
-                "alg_bytes_per_launch": round(alg / len(frames)),
-                "avg_launch_us": round(inter_ms / len(frames) * 1e3, 2),
+                "alg_bytes_per_launch": round(alg),
+                "avg_launch_us": round(recon_ms * 1e3, 2),
+                "launches": "P frames (inter reconstruction); hipEvents on the decode stream",
             },
         }
         if not a.no_cpu_baseline and world == 1:

@@ -91,17 +91,24 @@ void thor_dec_destroy(thor_dec_t *d);
 /* Decode (reconstruct) one frame.  `blocks`, `coeffs`, `clpf_flags` and
  * `intra_list` are DEVICE pointers (inputs resident in HBM); `nblocks`
  * descriptors in decode order.  `intra_list` holds the indices of the intra
- * CUs in decode order (thor_build_intra_list), the only planning data the
- * parser hands over besides the descriptors.  Enqueues every stage on the
+ * CUs in decode order (thor_build_intra_list) and `tu_list` the coded
+ * transform blocks (thor_build_tu_list): the only planning data the parser
+ * hands over besides the descriptors.  Enqueues every stage on the
  * context's stream and returns without waiting: per-4x4 side info, inter MC +
  * dequant + inverse transform + reconstruction, intra, deblock Y/UV, CLPF,
  * padding.  The reconstructed frame becomes reference `frame_num`. */
 int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
-                   const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra);
+                   const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
+                   const uint32_t *tu_list, int n_tu);
 
 /* Host helper: write the decode-order indices of the intra CUs of a frame
  * (host descriptors) to `out` (may be NULL to count); returns the count. */
 int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);
+/* Host helper: the frame's coded transform blocks (the residual work list the
+ * parser knows from the cbp flags, dec/decode_block.c:90-120): one entry
+ * block << 4 | component << 2 | tb-split quarter per coded TU, in any order.
+ * `out` may be NULL to count; returns the count. */
+int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);
 
 /* Stage control for parity debugging: 0 recon only, 1 +deblock, 2 +CLPF (default 2). */
 int thor_dec_set_stop_stage(thor_dec_t *d, int stage);
@@ -115,9 +122,14 @@ int thor_dec_sync(thor_dec_t *d);
 /* Per-stage GPU timing with hipEvents on the context's stream.  When on,
  * thor_dec_frame brackets each stage; thor_dec_stage_ms waits for the stream
  * and returns the milliseconds accumulated per stage since the last call:
- * [0] side info, [1] inter recon, [2] intra, [3] deblock, [4] CLPF, [5] pad. */
+ * [0] side info + residuals (k_prep, k_resid), [1] inter recon (k_recon), [2] intra,
+ * [3] deblock, [4] CLPF, [5] pad. */
 int thor_dec_set_timing(thor_dec_t *d, int on);
 int thor_dec_stage_ms(thor_dec_t *d, double *ms, int nstages);
+/* The same marks one by one in enqueue order (stage index, milliseconds), so
+ * a caller can attribute them to frames; returns the count (<= cap) and
+ * clears the marks. */
+int thor_dec_stage_marks(thor_dec_t *d, int *stage, double *ms, int cap);
 
 /* The HIP stream the context enqueues on (hipStream_t as void*), so callers
  * can record events / capture graphs around thor_dec_frame. */

@@ -14,17 +14,14 @@
 #include "common.h"
 
 // kernels (recon.hip, intra.hip, loopfilter.hip)
-__global__ void k_prep(const thor_block_t *, int, uint16_t *, int32_t *, int);
-__global__ void k_resid(const thor_block_t *, const int16_t *, int16_t *, int, int);
+__global__ void k_frame_prep(const thor_block_t *, int, uint16_t *, int32_t *, const uint32_t *, int, const int16_t *,
+                             int16_t *, const uint32_t *, int, unsigned *, unsigned *, int *, int, int, int, int, int);
 __global__ void k_recon(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int16_t *,
                         unsigned long long *);
-__global__ void k_intra_setup(const thor_block_t *, const uint32_t *, int, unsigned *, unsigned *, int *, int);
 __global__ void k_intra(FrameCtx, const thor_block_t *, const uint32_t *, const int *, unsigned *, unsigned *, int,
                         unsigned long long *, int, int, const int16_t *);
-__global__ void k_deblock_luma_v(uint8_t *, int, int, int, const uint16_t *, int);
-__global__ void k_deblock_luma_h(uint8_t *, int, int, int, const uint16_t *, int);
-__global__ void k_deblock_chroma_v(uint8_t *, uint8_t *, int, int, int, const uint16_t *, int);
-__global__ void k_deblock_chroma_h(uint8_t *, uint8_t *, int, int, int, const uint16_t *, int);
+__global__ void k_deblock_v(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, int, int, int, int);
+__global__ void k_deblock_h(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, int, int, int, int);
 __global__ void k_clpf(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, const uint8_t *);
 __global__ void k_pad(uint8_t *, uint8_t *, uint8_t *, int, int, int, int);
 
@@ -60,7 +57,7 @@ struct thor_dec {
   int32_t *cellmap;
   unsigned *ctl;       // [0] intra row head, [1] timeout flag
   unsigned *progress;  // intra wavefront progress per (SB row, component)
-  int16_t *resid;      // residual planes (Y, U, V; int16), written by k_resid, read by k_recon / k_intra
+  int16_t *resid;      // residual planes (Y, U, V; int16), written by k_prep_resid, read by k_recon / k_intra
   uint8_t *edge;       // SB-row edge rows (FrameCtx::edge)
   int ewy, ewc;
   unsigned long long *dbg;  // optional per-row intra timing (debug)
@@ -290,9 +287,11 @@ static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
 }
 
 int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
-                   const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra) {
+                   const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
+                   const uint32_t *tu_list, int n_tu) {
   if (!d || !hdr || nblocks < 0 || (nblocks > 0 && !blocks)) return THOR_ERR_ARG;
   if (n_intra > 0 && !intra_list) return THOR_ERR_ARG;
+  if (n_tu < 0 || (n_tu > 0 && (!tu_list || !coeffs))) return THOR_ERR_ARG;
   HIPCHK(hipSetDevice(d->device));
   int W = d->seq.width, H = d->seq.height;
   int cur = pick_slot(d, hdr->frame_num);
@@ -302,27 +301,28 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
   for (int a = 0; a < f.nref; a++)
     for (int b = a + 1; b < f.nref; b++)
       if (((f.ref_fnum[a] ^ f.ref_fnum[b]) & 127) == 0) return THOR_ERR_REF;
-  int cs = W / 4;
   hipStream_t st = d->stream;
   if (nblocks > 0) {
     {
-    StageMark m(d, ST_PREP);
-    k_prep<<<(nblocks + 3) / 4, 256, 0, st>>>(blocks, nblocks, d->cellinfo, d->cellmap, cs);
-    HIPCHK(hipGetLastError());
+      // side info + residuals of every coded transform block + intra chain setup
+      StageMark m(d, ST_PREP);
+      const int nrows = (H + 63) / 64;
+      int *rowstart = (int *)(d->progress + 3 * (nrows + 1));
+      const int nprep = (nblocks + 3) / 4, nres = (n_tu + 3) / 4;
+      k_frame_prep<<<nprep + nres + 1, 256, 0, st>>>(blocks, nblocks, d->cellinfo, d->cellmap, tu_list, n_tu, coeffs,
+                                                     d->resid, intra_list, n_intra, d->ctl, d->progress, rowstart,
+                                                     nrows, W, H, nprep, nres);
+      HIPCHK(hipGetLastError());
     }
     int nsb = ((W + 63) / 64) * ((H + 63) / 64);
-    StageMark m(d, ST_INTER);
-    k_resid<<<dim3(nblocks, 3), 64, 0, st>>>(blocks, coeffs, d->resid, W, H);
-    HIPCHK(hipGetLastError());
+    StageMark m(d, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
     k_recon<<<8 * ((2 * nsb + 7) / 8), 64, 0, st>>>(f, blocks, coeffs, d->cellmap, d->resid, d->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   if (n_intra > 0) {
     int nrows = (H + 63) / 64;
     StageMark m(d, ST_INTRA);
-    int *rowstart = (int *)(d->progress + 3 * (nrows + 1));
-    k_intra_setup<<<1, 64, 0, st>>>(blocks, intra_list, n_intra, d->ctl, d->progress, rowstart, nrows);
-    HIPCHK(hipGetLastError());
+    int *rowstart = (int *)(d->progress + 3 * (nrows + 1));  // set up by k_frame_prep
     // full SB images only when inter CUs were reconstructed (their pixels are intra neighbours)
     int full_sb = n_intra < nblocks;
     // one single-wave chain per (SB row, component); LDS holds the row's CU words
@@ -335,11 +335,11 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
     StageMark m(d, ST_DEBLOCK);
     int nv = ((W >> 3) - 1) * (H >> 3);
     int nh = (W >> 3) * ((H >> 3) - 1);
-    k_deblock_luma_v<<<(nv + 255) / 256, 256, 0, st>>>(f.cy, d->sy, W, H, d->cellinfo, hdr->qp);
-    k_deblock_luma_h<<<(nh + 255) / 256, 256, 0, st>>>(f.cy, d->sy, W, H, d->cellinfo, hdr->qp);
     int qpc = chroma_qp_host(hdr->qp);
-    k_deblock_chroma_v<<<dim3((nv + 255) / 256, 2), 256, 0, st>>>(f.cu, f.cv, d->sc, W, H, d->cellinfo, qpc);
-    k_deblock_chroma_h<<<dim3((nh + 255) / 256, 2), 256, 0, st>>>(f.cu, f.cv, d->sc, W, H, d->cellinfo, qpc);
+    // luma and both chroma planes of one edge direction per launch
+    const int bv = (nv + 255) / 256, bh = (nh + 255) / 256;
+    k_deblock_v<<<3 * bv, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, hdr->qp, qpc, bv, bv);
+    k_deblock_h<<<3 * bh, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, hdr->qp, qpc, bh, bh);
     HIPCHK(hipGetLastError());
   }
   if (d->stop_stage >= 2 && d->seq.clpf && hdr->clpf_on && clpf_flags) {
@@ -394,6 +394,43 @@ int thor_dec_stage_ms(thor_dec_t *d, double *ms, int nstages) {
   d->ev_marks.clear();
   d->ev_used = 0;
   return THOR_OK;
+}
+
+int thor_dec_stage_marks(thor_dec_t *d, int *stage, double *ms, int cap) {
+  if (!d || cap < 0 || (cap > 0 && (!stage || !ms))) return THOR_ERR_ARG;
+  HIPCHK(hipStreamSynchronize(d->stream));
+  int n = 0;
+  for (auto &m : d->ev_marks) {
+    if (n >= cap) break;
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, m.second.first, m.second.second));
+    stage[n] = m.first;
+    ms[n] = t;
+    n++;
+  }
+  d->ev_marks.clear();
+  d->ev_used = 0;
+  return n;
+}
+
+int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out) {
+  if (nblocks < 0 || (nblocks > 0 && !host_blocks)) return THOR_ERR_ARG;
+  if (nblocks >= (1 << 27)) return THOR_ERR_ARG;
+  int n = 0;
+  for (int b = 0; b < nblocks; b++) {
+    const thor_block_t &B = host_blocks[b];
+    if (B.mode == M_SKIP) continue;  // SKIP carries no residual (dec/decode_block.c:213-242)
+    for (int c = 0; c < 3; c++) {
+      if (!((B.coeff_mask >> c) & 1)) continue;
+      // tb-split gives 4 quarters; chroma of an 8x8 CU is not split (dec/decode_block.c:449-450)
+      const int split = B.tb_split && (c == 0 || B.size > 8);
+      for (int t = 0; t < (split ? 4 : 1); t++) {
+        if (out) out[n] = ((uint32_t)b << 4) | ((uint32_t)c << 2) | (uint32_t)t;
+        n++;
+      }
+    }
+  }
+  return n;
 }
 
 int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out) {

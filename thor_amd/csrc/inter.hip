@@ -5,7 +5,7 @@
 // predict four size/2 quarters with mv_arr[i], :381-392; truncating bi-pred
 // average, :272-283) through get_inter_prediction_luma/chroma
 // (common/inter_prediction.c:72-180), then reconstruct_block
-// (common/common_block.c:148-156) with the residual k_resid (resid.hip) left in
+// (common/common_block.c:148-156) with the residual k_prep_resid (resid.hip) left in
 // the int16 residual planes (dequantize + inverse_transform, :90-120).
 //
 // One wave per half SB (rows 0-31 or 32-63), mapped XCD-major (a band of

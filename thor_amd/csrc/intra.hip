@@ -44,7 +44,7 @@ struct CompGeom {
 };
 
 struct IntraChain {
-  int16_t res[64 * 64];  // k_resid's residual over the SB (16-B aligned rows)
+  int16_t res[64 * 64];  // k_prep_resid's residual over the SB (16-B aligned rows)
   int16_t p5[128];       // planar 5-tap filtered edges: top at 0, left at 64
   uint8_t flt[256];      // directional edge array of the current TU (U_OFF layout below)
   uint8_t img[65 * 72];  // SB image of this component
@@ -137,7 +137,7 @@ __device__ __forceinline__ int wave_sum(int v) {
          __builtin_amdgcn_readlane(v, 48);
 }
 
-// Residual of SB (k, l), 8 int16 per item, plain loads (written by k_resid in
+// Residual of SB (k, l), 8 int16 per item, plain loads (written by k_prep_resid in
 // an earlier launch; rows past the plane read as 0).
 template <int C>
 struct ResLoad {
@@ -597,9 +597,10 @@ __device__ __forceinline__ unsigned long long intra_chain(IntraChain &L, const F
 // Per-frame setup before k_intra: each SB row's segment of the intra list
 // (decode order is raster SB order) into rowstart[0..nrows]; progress words
 // and the task head cleared.
-__global__ __launch_bounds__(64) void k_intra_setup(const thor_block_t *__restrict__ blk,
-                                                    const uint32_t *__restrict__ list, int n_intra, unsigned *ctl,
-                                                    unsigned *progress, int *rowstart, int nrows) {
+__device__ __forceinline__ void intra_setup_body(const thor_block_t *__restrict__ blk,
+                                                 const uint32_t *__restrict__ list, int n_intra, unsigned *ctl,
+                                                 unsigned *progress, int *rowstart, int nrows) {
+  if (threadIdx.x >= 64) return;
   for (int r = threadIdx.x; r <= nrows; r += 64) {
     int lo = 0, hi = n_intra;
     while (lo < hi) {
@@ -611,6 +612,30 @@ __global__ __launch_bounds__(64) void k_intra_setup(const thor_block_t *__restri
   }
   for (int q = threadIdx.x; q < 3 * nrows; q += 64) progress[q] = 0;
   if (threadIdx.x == 0) ctl[0] = 0;
+}
+
+// k_frame_prep: everything a frame needs before reconstruction, in one launch
+// of 256-lane workgroups: [0, nprep) the per-4x4 side info (prep_body, four
+// CUs per workgroup), [nprep, nprep + nres) the residuals of the coded
+// transform blocks (resid_tu, four per workgroup), and one last workgroup that
+// sets up the intra chains (row segments of the intra list, progress words).
+// All three only read the frame's parse output.
+__global__ __launch_bounds__(256) void k_frame_prep(const thor_block_t *__restrict__ blk, int nblocks,
+                                                    uint16_t *__restrict__ cellinfo, int32_t *__restrict__ cellmap,
+                                                    const uint32_t *__restrict__ tus, int ntus,
+                                                    const int16_t *__restrict__ coeffs, int16_t *__restrict__ resid,
+                                                    const uint32_t *__restrict__ ilist, int n_intra, unsigned *ctl,
+                                                    unsigned *progress, int *rowstart, int nrows, int W, int H,
+                                                    int nprep, int nres) {
+  __shared__ ResidLds RL[4];
+  const int b = blockIdx.x;
+  if (b < nprep) prep_body(b, blk, nblocks, cellinfo, cellmap, W >> 2);
+  else if (b < nprep + nres) {
+    const int w = threadIdx.x >> 6;
+    resid_tu(RL[w], (b - nprep) * 4 + w, blk, tus, ntus, coeffs, resid, W, H);
+  } else if (n_intra > 0) {
+    intra_setup_body(blk, ilist, n_intra, ctl, progress, rowstart, nrows);
+  }
 }
 
 __global__ __launch_bounds__(64) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,

@@ -37,10 +37,10 @@ __device__ __forceinline__ void filt4(int &p1, int &p0, int &q0, int &q1, int tc
 }
 
 // Vertical luma edges: one thread per (edge column j = 8e, 8-row group).
-__global__ __launch_bounds__(256) void k_deblock_luma_v(uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
+__device__ __forceinline__ void k_deblock_luma_v_body(int bx, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
                                                         int qp) {
   int ne = (W >> 3) - 1;
-  int t = blockIdx.x * 256 + threadIdx.x;
+  int t = bx * 256 + threadIdx.x;
   int g = t / ne, e = t - g * ne + 1;
   if (g >= (H >> 3)) return;
   int i = g * 8, j = e * 8;
@@ -83,10 +83,10 @@ __global__ __launch_bounds__(256) void k_deblock_luma_v(uint8_t *Y, int sy, int 
 }
 
 // Horizontal luma edges: one thread per (edge row i = 8k >= 8, 8-column group).
-__global__ __launch_bounds__(256) void k_deblock_luma_h(uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
+__device__ __forceinline__ void k_deblock_luma_h_body(int bx, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
                                                         int qp) {
   int ng = W >> 3;
-  int t = blockIdx.x * 256 + threadIdx.x;
+  int t = bx * 256 + threadIdx.x;
   int k = t / ng, gcol = t - k * ng;
   int i = (k + 1) * 8, j = gcol * 8;
   if (i >= H) return;
@@ -122,11 +122,11 @@ __global__ __launch_bounds__(256) void k_deblock_luma_h(uint8_t *Y, int sy, int 
 
 // Chroma (deblock_frame_uv): intra-only edges, p0/q0 modified.  One thread
 // per (edge, 8-luma-row/column group) per plane (blockIdx.y = plane).
-__global__ __launch_bounds__(256) void k_deblock_chroma_v(uint8_t *U, uint8_t *V, int sc, int W, int H,
+__device__ __forceinline__ void k_deblock_chroma_v_body(int bx, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
                                                           const uint16_t *cell, int qpc) {
-  uint8_t *C = blockIdx.y ? V : U;
+  uint8_t *C = by ? V : U;
   int ne = (W >> 3) - 1;
-  int t = blockIdx.x * 256 + threadIdx.x;
+  int t = bx * 256 + threadIdx.x;
   int g = t / ne, e = t - g * ne + 1;
   if (g >= (H >> 3)) return;
   int i = g * 8, j = e * 8;
@@ -148,11 +148,11 @@ __global__ __launch_bounds__(256) void k_deblock_chroma_v(uint8_t *U, uint8_t *V
   }
 }
 
-__global__ __launch_bounds__(256) void k_deblock_chroma_h(uint8_t *U, uint8_t *V, int sc, int W, int H,
+__device__ __forceinline__ void k_deblock_chroma_h_body(int bx, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
                                                           const uint16_t *cell, int qpc) {
-  uint8_t *C = blockIdx.y ? V : U;
+  uint8_t *C = by ? V : U;
   int ng = W >> 3;
-  int t = blockIdx.x * 256 + threadIdx.x;
+  int t = bx * 256 + threadIdx.x;
   int k = t / ng, gcol = t - k * ng;
   int i = (k + 1) * 8, j = gcol * 8;
   if (i >= H) return;
@@ -180,6 +180,29 @@ __global__ __launch_bounds__(256) void k_deblock_chroma_h(uint8_t *U, uint8_t *V
 // Every 8x8 block that is not BIPRED is filtered per plane with coded
 // residual (clpf_block, common/common_block.c:180-197), reading the
 // unfiltered SB (LDS copy) with clamping at the SB border.
+// One launch per edge direction: luma blocks first, then U, then V (the
+// chroma filters read only the cell side info, never luma pixels, so the
+// planes are independent within a pass; vertical edges of all planes before
+// horizontal ones, deblock_frame_y / deblock_frame_uv, common/common_frame.c:46-321).
+__global__ __launch_bounds__(256) void k_deblock_v(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
+                                                   const uint16_t *cell, int qp, int qpc, int nbl, int nbc) {
+  const int b = blockIdx.x;
+  if (b < nbl) k_deblock_luma_v_body(b, Y, sy, W, H, cell, qp);
+  else {
+    const int c = (b - nbl) >= nbc;
+    k_deblock_chroma_v_body(b - nbl - c * nbc, c, U, V, sc, W, H, cell, qpc);
+  }
+}
+__global__ __launch_bounds__(256) void k_deblock_h(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
+                                                   const uint16_t *cell, int qp, int qpc, int nbl, int nbc) {
+  const int b = blockIdx.x;
+  if (b < nbl) k_deblock_luma_h_body(b, Y, sy, W, H, cell, qp);
+  else {
+    const int c = (b - nbl) >= nbc;
+    k_deblock_chroma_h_body(b - nbl - c * nbc, c, U, V, sc, W, H, cell, qpc);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_clpf(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
                                               const uint16_t *cell, const uint8_t *flags) {
   __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];

@@ -8,14 +8,13 @@
 #include "common.h"
 
 // ---------------------------------------------------------------------------
-// k_prep: one wavefront per CU.  Writes the per-4x4 cell map (CU index) and
+// prep_body (k_frame_prep, intra.hip): one wavefront per CU.  Writes the per-4x4 cell map (CU index) and
 // the packed side-info that copy_deblock_data (dec/decode_block.c:122-156)
 // stores for deblocking/CLPF.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_prep(const thor_block_t *__restrict__ blk, int nblocks,
-                                              uint16_t *__restrict__ cellinfo, int32_t *__restrict__ cellmap,
-                                              int cstride) {
-  int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void prep_body(int bx, const thor_block_t *__restrict__ blk, int nblocks,
+                                          uint16_t *__restrict__ cellinfo, int32_t *__restrict__ cellmap, int cstride) {
+  int b = bx * 4 + (threadIdx.x >> 6);
   int lane = threadIdx.x & 63;
   if (b >= nblocks) return;
   const thor_block_t &B = blk[b];

@@ -1,4 +1,4 @@
-// k_resid: residual of every coded transform block of a frame (gfx950).
+// Residuals of every coded transform block of a frame (gfx950), computed in k_prep_resid.
 //
 // Restates the residual half of decode_and_reconstruct_block_inter / _intra
 // (dec/decode_block.c:48-120): dequantize (common/common_block.c:132-146),
@@ -48,7 +48,7 @@ __device__ __forceinline__ int sx8(int w, int i) { return __builtin_amdgcn_sbfe(
 // at `out` (row stride `ostride` int16).
 __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int ntu, int qp, int16_t *__restrict__ out,
                            int ostride) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int rep = ntu == 64, n = rep ? 32 : ntu, q = n < 16 ? n : 16;
   const int step = 32 / n;
   const int lshift = qp / 6, scale = dequant_scale(qp % 6);
@@ -92,14 +92,18 @@ __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int nt
   wave_lds_sync();  // the next TU rewrites D and T
 }
 
-__global__ __launch_bounds__(64) void k_resid(const thor_block_t *__restrict__ blk, const int16_t *__restrict__ coeffs,
-                                              int16_t *__restrict__ resid, int W, int H) {
-  __shared__ ResidLds L;
-  const int lane = threadIdx.x;
-  const thor_block_t &B = blk[blockIdx.x];
-  const int c = blockIdx.y;
-  const int mode = B.mode, cmask = B.coeff_mask;
-  if (mode == M_SKIP || !((cmask >> c) & 1)) return;
+// resid_tu: one wavefront per coded transform block, from the frame's TU list
+// (thor_build_tu_list: entry = block << 4 | component << 2 | tb-split quarter).
+// Every TU is independent, so the launch is as wide as the frame's coded
+// residual and a skip-dominated P frame launches only a handful of waves.
+__device__ __forceinline__ void resid_tu(ResidLds &L, int idx, const thor_block_t *__restrict__ blk,
+                                         const uint32_t *__restrict__ tus, int ntus, const int16_t *__restrict__ coeffs,
+                                         int16_t *__restrict__ resid, int W, int H) {
+  const int lane = threadIdx.x & 63;
+  if (idx >= ntus) return;
+  const uint32_t e = tus[idx];
+  const thor_block_t &B = blk[e >> 4];
+  const int c = (e >> 2) & 3, t = e & 3;
   *(uint4 *)&L.M[16 * lane] = *(const uint4 *)&g_dct32.v[16 * lane];
   const int S = B.size, tb = B.tb_split != 0;
   const int size = c ? S >> 1 : S;
@@ -110,9 +114,7 @@ __global__ __launch_bounds__(64) void k_resid(const thor_block_t *__restrict__ b
   const int pw = c ? W >> 1 : W;
   const int py = c ? B.ypos >> 1 : B.ypos, px = c ? B.xpos >> 1 : B.xpos;
   int16_t *plane = resid + (c == 0 ? 0 : (long long)W * H + (c == 2 ? (long long)(W >> 1) * (H >> 1) : 0));
+  const int oy = (t >> 1) * ntu, ox = (t & 1) * ntu;  // tb-split quarters in raster order, :101-102
   wave_lds_sync();
-  for (int t = 0; t < (tbc ? 4 : 1); t++) {  // tb-split quarters in raster order, :101-102
-    const int oy = (t >> 1) * ntu, ox = (t & 1) * ntu;
-    tu_inverse(L, coeffs + B.coeff_off[c] + t * q * q, ntu, qp, plane + (long long)(py + oy) * pw + px + ox, pw);
-  }
+  tu_inverse(L, coeffs + B.coeff_off[c] + t * q * q, ntu, qp, plane + (long long)(py + oy) * pw + px + ox, pw);
 }

@@ -30,6 +30,8 @@ class DeviceFrame:
     clpf: int
     intra: int
     n_intra: int
+    tus: int
+    n_tu: int
     nbytes: int  # bytes uploaded (descriptors + coefficients + flags + list)
 
 
@@ -91,14 +93,19 @@ class GpuDecoder:
         n_intra = self.lib.thor_build_intra_list(blocks.ctypes.data, len(blocks), None)
         ilist = np.zeros(max(n_intra, 1), np.uint32)
         self.lib.thor_build_intra_list(blocks.ctypes.data, len(blocks), ilist.ctypes.data)
+        n_tu = self.lib.thor_build_tu_list(blocks.ctypes.data, len(blocks), None)
+        tlist = np.zeros(max(n_tu, 1), np.uint32)
+        self.lib.thor_build_tu_list(blocks.ctypes.data, len(blocks), tlist.ctypes.data)
         bb, cb, fb, ib = self._buf(blocks), self._buf(coeffs), self._buf(flags), self._buf(ilist)
+        tb = self._buf(tlist)
         hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
-        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra
-        return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, nbytes)
+        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + 4 * n_tu
+        return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, tb.ptr,
+                           n_tu, nbytes)
 
     def decode(self, d: DeviceFrame):
         rc = self.lib.thor_dec_frame(self.h, C.byref(d.hdr), d.blocks, d.nblocks, d.coeffs, d.clpf or None,
-                                     d.intra, d.n_intra)
+                                     d.intra, d.n_intra, d.tus, d.n_tu)
         L.check(rc, "thor_dec_frame")
 
     def set_stop_stage(self, stage: int):

@@ -23,8 +23,8 @@ class ThorFrameHdr(C.Structure):
 
 # Every symbol the public headers declare (checked by tests/test_capi.py).
 BATCHED_SYMBOLS = [
-    "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_build_intra_list", "thor_dec_set_stop_stage",
-    "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
+    "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_build_intra_list", "thor_build_tu_list", "thor_dec_set_stop_stage",
+    "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_stage_marks", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
@@ -55,10 +55,12 @@ def load(path: str = LIB_PATH):
     L.thor_dec_create.argtypes = [C.POINTER(ThorSeq), i, i]
     L.thor_dec_create.restype = P
     L.thor_dec_destroy.argtypes = [P]
-    L.thor_dec_frame.argtypes = [P, C.POINTER(ThorFrameHdr), P, i, P, P, P, i]
+    L.thor_dec_frame.argtypes = [P, C.POINTER(ThorFrameHdr), P, i, P, P, P, i, P, i]
     L.thor_dec_frame.restype = i
     L.thor_build_intra_list.argtypes = [P, i, P]
     L.thor_build_intra_list.restype = i
+    L.thor_build_tu_list.argtypes = [P, i, P]
+    L.thor_build_tu_list.restype = i
     L.thor_dec_set_stop_stage.argtypes = [P, i]
     L.thor_dec_read_frame.argtypes = [P, i, P, P, P]
     L.thor_dec_read_frame.restype = i
@@ -72,6 +74,8 @@ def load(path: str = LIB_PATH):
     L.thor_dec_set_timing.argtypes = [P, i]
     L.thor_dec_stage_ms.argtypes = [P, C.POINTER(C.c_double), i]
     L.thor_dec_stage_ms.restype = i
+    L.thor_dec_stage_marks.argtypes = [P, P, P, i]
+    L.thor_dec_stage_marks.restype = i
     L.thor_enc_tu_batch.argtypes = [P, i, P, P, P, P, P, P, P]
     L.thor_enc_tu_batch.restype = i
     L.thor_enc_cost_batch.argtypes = [P, P, P, P, C.c_double, P, i, P]

@@ -38,6 +38,13 @@ def pmc(db, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
 
+def per_dispatch(db, counter, kernel):
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, value from counters_collection where counter_name=? order by dispatch_id",
+                     (counter,))
+    return [float(v) for n, v in rows if short(n) == kernel]
+
+
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -67,9 +74,17 @@ def main():
         wb = w.get(k, 0.0) * 1024
         traffic["kernels"][k] = {"fetch_kib_raw": round(f.get(k, 0.0), 1), "write_kib_raw": round(w.get(k, 0.0), 1),
                                  "hbm_bytes_per_launch": round(fb + wb), "launches": nf.get(k, 0)}
-    if "k_inter" in traffic["kernels"]:
-        traffic["inter_hbm_bytes_per_launch"] = traffic["kernels"]["k_inter"]["hbm_bytes_per_launch"]
+    # k_recon on P frames only: one launch per frame, the stream's frame 0 is the
+    # I frame (no inter pixels), so drop every 8th dispatch in dispatch order
+    fr = per_dispatch(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE", "k_recon")
+    wr = per_dispatch(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE", "k_recon")
+    if fr and wr and len(fr) == len(wr):
+        pf = [v for i, v in enumerate(fr) if i % 8 != 0]
+        pw = [v for i, v in enumerate(wr) if i % 8 != 0]
+        traffic["recon_hbm_bytes_per_p_launch"] = round((sum(pf) * 2 + sum(pw)) * 1024 / len(pf))
+        traffic["recon_p_launches"] = len(pf)
     json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
+    json.dump(traffic, open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
 
