@@ -10,10 +10,16 @@ reconstruction, intra, deblock Y/UV, CLPF and reference padding, all through
 libthor_amd.so's C-ABI.  The parse output (block descriptors, coefficients,
 intra list, CLPF flags) is resident in HBM before timing starts; bit parsing
 is CPU work outside the hot path.  The decoded frames are checked bit-exact
-against the reference decoder's md5s after the timed region.
+against the reference decoder's md5s (every context) after warmup.
 
-N > 1: one process per GPU, each reconstructing its own copy of the stream
-(independent streams, no data-path collective): scaling "weak".
+Per GPU, --streams K (default 7) independent decoder contexts each decode
+their own copy of the stream on their own HIP stream, interleaved frame by
+frame (a server decoding K streams): value = K x stream pixels / time.  The
+single-stream latency of one pass is reported next to it
+(config.single_stream_ms_per_pass).
+
+N > 1: one process per GPU, each with its own K streams (independent
+streams, no data-path collective): scaling "weak".
 
 Prints one JSON line (rank 0).
 """
@@ -30,6 +36,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# one hardware queue per decoder context (HIP's default is 4 per process);
+# must be set before the HIP runtime initialises
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np  # noqa: E402
 
@@ -100,8 +110,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=7, help="independent decoder contexts per GPU")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC-derived HBM bytes per k_recon launch (default profiles/traffic_latest.json)")
+                    help="PMC-derived HBM bytes per k_recon launch (default tools/traffic_latest.json, "
+                         "copied from profiles/<tag>_traffic.json by tools/prof_summary.py)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -126,39 +138,80 @@ def main():
     gold = os.path.join(ROOT, "tests", "golden")
     meta = json.load(open(os.path.join(gold, "streams.json")))["k4_low"]
     seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
-    dec = GpuDecoder(seq, device=local)
-    stream = torch.cuda.current_stream(local)
-    dec.set_stream(C.c_void_p(stream.cuda_stream))
-    devs = [dec.upload(fr) for fr in frames]
+    # K decoder contexts per GPU, each decoding its own copy of the stream on its
+    # own HIP stream (independent streams, as a server decodes many): the I
+    # frame's intra chain occupies ~100 waves, so other streams' frames fill the
+    # GPU meanwhile.  Context 0 alone gives the single-stream latency.
+    K = max(1, a.streams)
+    # each context enqueues on its own non-blocking HIP stream (created by
+    # thor_dec_create, consecutively, so they spread over the hardware queues)
+    decs, devs = [], []
+    for k in range(K):
+        dk = GpuDecoder(seq, device=local)
+        decs.append(dk)
+        devs.append([dk.upload(fr) for fr in frames])
+    dec = decs[0]
     torch.cuda.synchronize(local)
 
-    def step():
-        for d in devs:
-            dec.decode(d)
+    # Each context decodes the stream cyclically (frames 0..7, 0..7, ...); context
+    # k runs (8k/K) frames out of phase with context 0, so the contexts' I frames
+    # (the latency-bound intra chain) do not all fall into the same slot.
+    nf = len(frames)
+    phase = [(k * nf) // K for k in range(K)]
 
+    def step(ks=range(K)):
+        for i in range(nf):  # interleave the contexts frame by frame
+            for k in ks:
+                decs[k].decode(devs[k][(phase[k] + i) % nf])
+
+    def sync_all():
+        for dk in decs:
+            dk.sync()
+        torch.cuda.synchronize(local)
+
+    for k in range(K):  # one plain pass (every reference resident), then shift to the context's phase
+        for i in range(nf + phase[k]):
+            decs[k].decode(devs[k][i % nf])
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize(local)
+    sync_all()
 
-    # check bit-exactness of what the steps produce
-    got = {fr.frame_num: dec.read_i420(fr.frame_num) for fr in frames}
-    yuv = b"".join(got[k] for k in sorted(got))
-    bit_exact = hashlib.md5(yuv).hexdigest() == meta["dec_md5"]
+    # check bit-exactness of what every context produced
+    bit_exact = True
+    for dk in decs:
+        got = {fr.frame_num: dk.read_i420(fr.frame_num) for fr in frames}
+        yuv = b"".join(got[k] for k in sorted(got))
+        bit_exact &= hashlib.md5(yuv).hexdigest() == meta["dec_md5"]
 
     lib = L.load()
-    lib.thor_dec_set_timing(dec.h, 1)
-    cap = 8 * len(frames) * (a.steps + 1)
-    mk_stage, mk_ms = (C.c_int * cap)(), (C.c_double * cap)()
-    lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)  # drop the warmup marks
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize(local)
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    torch.cuda.synchronize(local)
+    sync_all()
     elapsed = time.perf_counter() - t0
+
+    # single-stream latency of one pass over the stream (context 0 alone)
+    lsteps = max(1, min(a.steps, 10))
+    t1 = time.perf_counter()
+    for _ in range(lsteps):
+        step(ks=[0])
+    sync_all()
+    latency_ms = (time.perf_counter() - t1) / lsteps * 1e3
+
+    # instrumented pass (not part of `value`): hipEvents around every stage of
+    # every frame on the decode stream, for the stage breakdown and the roofline
+    isteps = max(1, min(a.steps, 5))
+    lib.thor_dec_set_timing(dec.h, 1)
+    cap = 8 * len(frames) * (isteps + 1)
+    mk_stage, mk_ms = (C.c_int * cap)(), (C.c_double * cap)()
+    lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)
+    for _ in range(isteps):
+        step(ks=[0])
     nm = lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)
+    lib.thor_dec_set_timing(dec.h, 0)
     # attribute the marks to frames: every frame opens with its side-info stage (0)
     per_frame, cur = [], None
     for k in range(nm):
@@ -166,11 +219,11 @@ def main():
             cur = [0.0] * 6
             per_frame.append(cur)
         cur[mk_stage[k]] += mk_ms[k]
-    assert len(per_frame) == a.steps * len(frames), (len(per_frame), a.steps, len(frames))
-    stage_ms = [sum(f[i] for f in per_frame) / a.steps for i in range(6)]  # per step (whole stream)
+    assert len(per_frame) == isteps * len(frames), (len(per_frame), isteps, len(frames))
+    stage_ms = [sum(f[i] for f in per_frame) / isteps for i in range(6)]  # per step (whole stream)
     # k_recon roofline over the P frames (the I frame has no inter pixels)
     pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]
-    recon_ms = sum(per_frame[s * len(frames) + i][1] for s in range(a.steps) for i in pidx) / (a.steps * len(pidx))
+    recon_ms = sum(per_frame[s * len(frames) + i][1] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
     alg = sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda")
@@ -181,12 +234,12 @@ def main():
         bit_exact = bool(ok.item())
 
     px_step = seq.width * seq.height * len(frames)
-    value = world * px_step * a.steps / elapsed / 1e6
+    value = world * K * px_step * a.steps / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
 
     achieved = alg / (recon_ms / 1e3) / 1e9 if recon_ms > 0 else 0.0
     traffic = None
-    tj = a.traffic_json or os.path.join(ROOT, "profiles", "traffic_latest.json")
+    tj = a.traffic_json or os.path.join(ROOT, "tools", "traffic_latest.json")
     if os.path.exists(tj):
         traffic = json.load(open(tj)).get("recon_hbm_bytes_per_p_launch")
 
@@ -213,8 +266,13 @@ def main():
                 "frames": len(frames),
                 "width": seq.width,
                 "height": seq.height,
-                "parallelism": "replicas%d" % world,
+                "parallelism": "streams: %d GPU(s) x %d independent decoder contexts" % (world, K),
+                "streams_per_gpu": K,
+                "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                "single_stream_ms_per_pass": round(latency_ms, 4),
+                "single_stream_mpx_s": round(px_step / latency_ms / 1e3, 1),
                 "stage_ms_per_step": {k: round(v, 4) for k, v in zip(STAGES, stage_ms)},
+                "stage_note": "hipEvent-bracketed stages from a separate instrumented pass",
             },
             "roofline": {
                 "bound": "hbm",
@@ -232,7 +290,8 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(meta, gold)
         print(json.dumps(out), flush=True)
-    dec.close()
+    for dk in decs:
+        dk.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -53,12 +53,21 @@ def main():
     rows = kernel_stats(os.path.join(d, "trace", "run_results.db"))
     lines = ["# rocprofv3 --kernel-trace --stats  (%s)" % tag,
              "# command: rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline",
+             "# (averages below mix the concurrent multi-stream timed region and the single-stream passes)",
              "%-24s %8s %14s %12s %8s" % ("kernel", "calls", "total_us", "avg_us", "pct")]
     for name, calls, tot, avg, pct in rows:
         lines.append("%-24s %8d %14.1f %12.3f %8.2f" % (short(name), calls, tot, avg, pct))
     # per-dispatch durations of the last step (one launch per frame, 8 frames)
     c = sqlite3.connect(os.path.join(d, "trace", "run_results.db"))
     seq = [(short(n), dur / 1e3) for n, dur in c.execute("select name, duration from kernels order by start")]
+    # the bench's last phase is the single-context instrumented pass (5 steps x 8
+    # frames, frame order 0..7): its k_recon P-frame dispatches are the ones the
+    # bench's hipEvent roofline times
+    rec = [v for n, v in seq if n == "k_recon"][-40:]
+    prec = [v for i, v in enumerate(rec) if i % 8 != 0]
+    if prec:
+        lines.append("# k_recon, instrumented single-stream pass, P frames: %d dispatches, avg %.2f us"
+                     % (len(prec), sum(prec) / len(prec)))
     lines.append("# last step, per frame (us): I P P P P P P P")
     for k in sorted({n for n, _ in seq if n.startswith("k_")}):
         ds = [v for n, v in seq if n == k][-8:]
@@ -84,7 +93,8 @@ def main():
         traffic["recon_hbm_bytes_per_p_launch"] = round((sum(pf) * 2 + sum(pw)) * 1024 / len(pf))
         traffic["recon_p_launches"] = len(pf)
     json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
-    json.dump(traffic, open(os.path.join(out, "traffic_latest.json"), "w"), indent=1)
+    # the GPU box does not receive profiles/ (.gpurunignore): bench.py reads this copy
+    json.dump(traffic, open(os.path.join(root, "tools", "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
 
