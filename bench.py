@@ -110,7 +110,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=7, help="independent decoder contexts per GPU")
+    ap.add_argument("--streams", type=int, default=12, help="independent decoder contexts per GPU")
+    ap.add_argument("--groups", type=int, default=3,
+                    help="batches per frame slot (contexts of a group share one launch per stage)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per k_recon launch (default tools/traffic_latest.json, "
                          "copied from profiles/<tag>_traffic.json by tools/prof_summary.py)")
@@ -132,7 +134,7 @@ def main():
         torch.cuda.set_device(local)
 
     from thor_amd import lib as L
-    from thor_amd.decoder import GpuDecoder
+    from thor_amd.decoder import GpuDecoder, decode_batch
     from thor_amd.trace import load_trace
 
     gold = os.path.join(ROOT, "tests", "golden")
@@ -153,16 +155,33 @@ def main():
     dec = decs[0]
     torch.cuda.synchronize(local)
 
-    # Each context decodes the stream cyclically (frames 0..7, 0..7, ...); context
-    # k runs (8k/K) frames out of phase with context 0, so the contexts' I frames
-    # (the latency-bound intra chain) do not all fall into the same slot.
+    # Contexts are split into G groups; a group decodes its contexts' next frames
+    # with one launch per stage (thor_dec_frames) on its leader's HIP stream.
+    # Every context decodes the stream cyclically (frames 0..7, 0..7, ...) and
+    # group g runs (8g/G) frames out of phase with group 0, so the groups' I
+    # frames (the latency-bound intra chains) overlap other groups' P frames.
     nf = len(frames)
-    phase = [(k * nf) // K for k in range(K)]
+    G = max(1, min(a.groups, K))
+    groups = [list(range(g, K, G)) for g in range(G)]
+    gphase = [(g * nf) // G for g in range(G)]
+    phase = [0] * K
+    for g, ks in enumerate(groups):
+        for k in ks:
+            phase[k] = gphase[g]
 
-    def step(ks=range(K)):
-        for i in range(nf):  # interleave the contexts frame by frame
-            for k in ks:
-                decs[k].decode(devs[k][(phase[k] + i) % nf])
+    for gk in groups:  # a group's members enqueue on their leader's stream
+        for k in gk[1:]:
+            decs[k].set_stream(C.c_void_p(decs[gk[0]].stream()))
+
+    def step(ks=None, gs=None):
+        for i in range(nf):  # interleave the groups frame by frame
+            if ks is not None:
+                for k in ks:
+                    decs[k].decode(devs[k][(phase[k] + i) % nf])
+                continue
+            for g in (range(G) if gs is None else gs):
+                gk = groups[g]
+                decode_batch([decs[k] for k in gk], [devs[k][(gphase[g] + i) % nf] for k in gk])
 
     def sync_all():
         for dk in decs:
@@ -201,17 +220,20 @@ def main():
     sync_all()
     latency_ms = (time.perf_counter() - t1) / lsteps * 1e3
 
-    # instrumented pass (not part of `value`): hipEvents around every stage of
-    # every frame on the decode stream, for the stage breakdown and the roofline
+    # instrumented pass (not part of `value`): group 0 alone, hipEvents around
+    # every stage of every batched launch on its stream, for the stage breakdown
+    # and the roofline (one launch = the group's B frames)
     isteps = max(1, min(a.steps, 5))
-    lib.thor_dec_set_timing(dec.h, 1)
+    lead = decs[groups[0][0]]
+    B = len(groups[0])
+    lib.thor_dec_set_timing(lead.h, 1)
     cap = 8 * len(frames) * (isteps + 1)
     mk_stage, mk_ms = (C.c_int * cap)(), (C.c_double * cap)()
-    lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)
+    lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
     for _ in range(isteps):
-        step(ks=[0])
-    nm = lib.thor_dec_stage_marks(dec.h, mk_stage, mk_ms, cap)
-    lib.thor_dec_set_timing(dec.h, 0)
+        step(gs=[0])
+    nm = lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
+    lib.thor_dec_set_timing(lead.h, 0)
     # attribute the marks to frames: every frame opens with its side-info stage (0)
     per_frame, cur = [], None
     for k in range(nm):
@@ -220,11 +242,11 @@ def main():
             per_frame.append(cur)
         cur[mk_stage[k]] += mk_ms[k]
     assert len(per_frame) == isteps * len(frames), (len(per_frame), isteps, len(frames))
-    stage_ms = [sum(f[i] for f in per_frame) / isteps for i in range(6)]  # per step (whole stream)
+    stage_ms = [sum(f[i] for f in per_frame) / isteps / B for i in range(6)]  # per stream pass
     # k_recon roofline over the P frames (the I frame has no inter pixels)
     pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]
     recon_ms = sum(per_frame[s * len(frames) + i][1] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
-    alg = sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
+    alg = B * sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -268,11 +290,12 @@ def main():
                 "height": seq.height,
                 "parallelism": "streams: %d GPU(s) x %d independent decoder contexts" % (world, K),
                 "streams_per_gpu": K,
+                "batch_groups": G,
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "single_stream_ms_per_pass": round(latency_ms, 4),
                 "single_stream_mpx_s": round(px_step / latency_ms / 1e3, 1),
                 "stage_ms_per_step": {k: round(v, 4) for k, v in zip(STAGES, stage_ms)},
-                "stage_note": "hipEvent-bracketed stages from a separate instrumented pass",
+                "stage_note": "per stream pass: hipEvent-bracketed batched stages of group 0 alone / frames per launch",
             },
             "roofline": {
                 "bound": "hbm",
@@ -284,7 +307,8 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": round(alg),
                 "avg_launch_us": round(recon_ms * 1e3, 2),
-                "launches": "P frames (inter reconstruction); hipEvents on the decode stream",
+                "frames_per_launch": B,
+                "launches": "batched P-frame launches of group 0 alone; hipEvents on its stream",
             },
         }
         if not a.no_cpu_baseline and world == 1:

@@ -101,6 +101,26 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
                    const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
                    const uint32_t *tu_list, int n_tu);
 
+/* One frame's parse output (DEVICE pointers), as thor_dec_frame takes it. */
+typedef struct thor_frame_in {
+  const thor_block_t *blocks;
+  int32_t nblocks;
+  const int16_t *coeffs;
+  const uint8_t *clpf_flags;
+  const uint32_t *intra_list;
+  int32_t n_intra;
+  const uint32_t *tu_list;
+  int32_t n_tu;
+} thor_frame_in_t;
+
+/* Decode one frame in each of `n` DIFFERENT contexts with one launch per stage
+ * (grid dimension = frame, up to 8 frames per launch): a server decoding many
+ * streams batches their next frames.  All contexts must share the device and frame size.
+ * Work is enqueued on ds[0]'s stream, ordered after each member context's
+ * earlier work on its own stream and before its later work.  n = 1 is
+ * thor_dec_frame. */
+int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins);
+
 /* Host helper: write the decode-order indices of the intra CUs of a frame
  * (host descriptors) to `out` (may be NULL to count); returns the count. */
 int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);

@@ -79,3 +79,35 @@ def test_gpu_matches_oracle_pixelwise():
                 assert bad.size == 0, (fr.decode_order, nm, bad[:5].tolist(), int(len(bad)))
     finally:
         gdec.close()
+
+
+def test_batched_contexts_match_reference(streams):
+    """thor_dec_frames: one launch per stage decodes the next frame of several
+    streams (distinct contexts, same frame size) at once; every stream must
+    still match the reference decoder per frame and stage."""
+    import hashlib
+
+    from thor_amd.decoder import GpuDecoder, decode_batch
+    from thor_amd.trace import load_trace
+
+    names = ["cif_low", "cif_med", "cif_high", "cif_hdb"]
+    decs, devs, frs = [], [], []
+    try:
+        for nm in names:
+            seq, frames = load_trace(trace_path(nm))
+            d = GpuDecoder(seq)
+            decs.append(d)
+            frs.append(frames)
+            devs.append([d.upload(fr) for fr in frames])
+        nmax = max(len(f) for f in frs)
+        for i in range(nmax):
+            live = [k for k in range(len(names)) if i < len(frs[k])]
+            decode_batch([decs[k] for k in live], [devs[k][i] for k in live])
+            for k in live:
+                fr = frs[k][i]
+                got = decs[k].read_i420(fr.frame_num)
+                want = streams[names[k]]["stage_md5"][fr.decode_order]["final"]
+                assert hashlib.md5(got).hexdigest() == want, (names[k], i)
+    finally:
+        for d in decs:
+            d.close()

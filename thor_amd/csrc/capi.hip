@@ -13,17 +13,14 @@
 
 #include "common.h"
 
-// kernels (recon.hip, intra.hip, loopfilter.hip)
-__global__ void k_frame_prep(const thor_block_t *, int, uint16_t *, int32_t *, const uint32_t *, int, const int16_t *,
-                             int16_t *, const uint32_t *, int, unsigned *, unsigned *, int *, int, int, int, int, int);
-__global__ void k_recon(FrameCtx, const thor_block_t *, const int16_t *, const int32_t *, int16_t *,
-                        unsigned long long *);
-__global__ void k_intra(FrameCtx, const thor_block_t *, const uint32_t *, const int *, unsigned *, unsigned *, int,
-                        unsigned long long *, int, int, const int16_t *);
-__global__ void k_deblock_v(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, int, int, int, int);
-__global__ void k_deblock_h(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, int, int, int, int);
-__global__ void k_clpf(uint8_t *, uint8_t *, uint8_t *, int, int, int, int, const uint16_t *, const uint8_t *);
-__global__ void k_pad(uint8_t *, uint8_t *, uint8_t *, int, int, int, int);
+// kernels (intra.hip, inter.hip, loopfilter.hip): the frame batch by value, first argument
+__global__ void k_frame_prep(const FrameBatch);
+__global__ void k_recon(const FrameBatch, unsigned long long *);
+__global__ void k_intra(const FrameBatch, unsigned long long *, int);
+__global__ void k_deblock_v(const FrameBatch, int);
+__global__ void k_deblock_h(const FrameBatch, int);
+__global__ void k_clpf(const FrameBatch);
+__global__ void k_pad(const FrameBatch);
 
 #define HIPCHK(x)                                                                               \
   do {                                                                                          \
@@ -64,6 +61,7 @@ struct thor_dec {
   unsigned long long *dbg_recon;  // optional k_recon phase stamps (debug)
   int dbg_flags;
   int stop_stage;
+  hipEvent_t xev[2];  // cross-stream ordering when a batch mixes contexts on different streams
   // optional per-stage timing (hipEvents on the decode stream)
   int timing;
   std::vector<hipEvent_t> ev_pool;
@@ -160,6 +158,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->dbg_recon = nullptr;
   d->dbg_flags = 0;
   d->timing = 0;
+  d->xev[0] = d->xev[1] = nullptr;
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
   d->stream = d->own_stream;
@@ -178,6 +177,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->ewc = (W / 2 + 2 * EDGE_MARGIN + 15) & ~15;
   ok = ok && hipMalloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc)) == hipSuccess;
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
+  for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&d->xev[i], hipEventDisableTiming) == hipSuccess;
   {  // k_intra stages a row's CU words in LDS (up to (W/8) x 8 CUs)
     size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
     if (lds > 48 * 1024)
@@ -202,6 +202,8 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->progress) (void)hipFree(d->progress);
   if (d->resid) (void)hipFree(d->resid);
   if (d->edge) (void)hipFree(d->edge);
+  for (int i = 0; i < 2; i++)
+    if (d->xev[i]) (void)hipEventDestroy(d->xev[i]);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
   if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
   delete d;
@@ -249,8 +251,10 @@ static int pick_slot(const thor_dec *d, int frame_num) {
   return best;
 }
 
-static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
-  FrameCtx f;
+// FrameCtx of the frame about to be decoded into slot `cur_slot`; the resident
+// references are every other occupied slot.  Returns false if two resident
+// frame numbers collide modulo 128 (k_recon's lookup table key).
+static bool make_ctx(const thor_dec *d, int cur_slot, int frame_num, FrameCtx &f) {
   memset(&f, 0, sizeof(f));
   uint8_t *cur = d->slots + (long long)cur_slot * d->slot_bytes;
   f.cy = cur + d->offy;
@@ -268,96 +272,158 @@ static FrameCtx make_ctx(const thor_dec *d, int cur_slot, int frame_num) {
   f.H = d->seq.height;
   f.frame_num = frame_num;
   f.bipred = d->seq.bipred;
-  f.nref = 0;
-  for (int s = 0; s < d->nslots; s++) {
-    if (s == cur_slot || d->slot_fnum[s] < 0) continue;
-    f.ref_fnum[f.nref] = d->slot_fnum[s];
-    f.ref_slot[f.nref] = s;
-    f.nref++;
-  }
   f.edge = d->edge;
   f.ewy = d->ewy;
   f.ewc = d->ewc;
   f.nsbrows = (d->seq.height + 63) / 64;
+  f.cellinfo = d->cellinfo;
+  f.cellmap = d->cellmap;
+  f.resid = d->resid;
+  f.ctl = d->ctl;
+  f.progress = d->progress;
+  f.rowstart = (int *)(d->progress + 3 * (f.nsbrows + 1));
   int8_t lut[128];
   memset(lut, -1, sizeof(lut));
-  for (int r = 0; r < f.nref; r++) lut[f.ref_fnum[r] & 127] = (int8_t)f.ref_slot[r];
+  f.nref = 0;
+  for (int s = 0; s < d->nslots; s++) {
+    if (s == cur_slot || d->slot_fnum[s] < 0) continue;
+    const int k = d->slot_fnum[s] & 127;
+    if (lut[k] >= 0) return false;
+    lut[k] = (int8_t)s;
+    f.nref++;
+  }
   memcpy(f.slot_lut, lut, sizeof(lut));
-  return f;
+  return true;
+}
+
+static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins);
+
+int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins) {
+  if (!ds || !hdrs || !ins || n <= 0) return THOR_ERR_ARG;
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < i; j++)
+      if (ds[i] == ds[j]) return THOR_ERR_ARG;  // one frame per context per call (a stream's frames are serial)
+  for (int o = 0; o < n; o += THOR_MAX_BATCH) {  // THOR_MAX_BATCH frames per launch
+    const int rc = dec_frames_chunk(ds + o, n - o < THOR_MAX_BATCH ? n - o : THOR_MAX_BATCH, hdrs + o, ins + o);
+    if (rc != THOR_OK) return rc;
+  }
+  return THOR_OK;
+}
+
+static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins) {
+  thor_dec *lead = ds[0];
+  if (!lead) return THOR_ERR_ARG;
+  const int W = lead->seq.width, H = lead->seq.height;
+  for (int i = 0; i < n; i++) {
+    const thor_dec *d = ds[i];
+    const thor_frame_in_t &in = ins[i];
+    if (!d || d->device != lead->device || d->seq.width != W || d->seq.height != H) return THOR_ERR_ARG;
+    if (in.nblocks < 0 || (in.nblocks > 0 && !in.blocks)) return THOR_ERR_ARG;
+    if (in.n_intra < 0 || (in.n_intra > 0 && !in.intra_list)) return THOR_ERR_ARG;
+    if (in.n_tu < 0 || (in.n_tu > 0 && (!in.tu_list || !in.coeffs))) return THOR_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(lead->device));
+  hipStream_t st = lead->stream;
+  // FrameCtx of every frame, passed by value (kernel argument segment)
+  FrameBatch fb;
+  memset(&fb, 0, sizeof(fb));
+  FrameCtx *hp = fb.f;
+  int cur[THOR_MAX_BATCH];
+  int max_prep = 1, any_intra = 0, any_clpf = 0, any_deblock = 0;
+  for (int i = 0; i < n; i++) {
+    thor_dec *d = ds[i];
+    const thor_frame_in_t &in = ins[i];
+    cur[i] = pick_slot(d, hdrs[i].frame_num);
+    FrameCtx &f = hp[i];
+    if (!make_ctx(d, cur[i], hdrs[i].frame_num, f)) return THOR_ERR_REF;
+    f.blk = in.blocks;
+    f.coeffs = in.coeffs;
+    f.tus = in.tu_list;
+    f.ilist = in.intra_list;
+    f.clpf_flags = in.clpf_flags;
+    f.nblocks = in.nblocks;
+    f.ntus = in.n_tu;
+    f.nintra = in.n_intra;
+    f.nprep = (in.nblocks + 3) / 4;
+    f.nres = (in.n_tu + 3) / 4;
+    f.full_sb = in.n_intra < in.nblocks;  // full SB images only when inter CUs were reconstructed
+    f.qp = hdrs[i].qp;
+    f.qpc = chroma_qp_host(hdrs[i].qp);
+    f.deblock = d->stop_stage >= 1 && d->seq.deblocking;
+    f.clpf_on = d->stop_stage >= 2 && d->seq.clpf && hdrs[i].clpf_on && in.clpf_flags;
+    max_prep = max_prep > f.nprep + f.nres + 1 ? max_prep : f.nprep + f.nres + 1;
+    any_intra |= in.n_intra > 0;
+    any_clpf |= f.clpf_on;
+    any_deblock |= f.deblock;
+  }
+  // order the batch after each member context's earlier work on other streams
+  for (int i = 1; i < n; i++)
+    if (ds[i]->stream != st) {
+      HIPCHK(hipEventRecord(lead->xev[0], ds[i]->stream));
+      HIPCHK(hipStreamWaitEvent(st, lead->xev[0], 0));
+    }
+  const int nsb = ((W + 63) / 64) * ((H + 63) / 64);
+  const int nrows = (H + 63) / 64;
+  {
+    // side info + residuals of every coded transform block + intra chain setup
+    StageMark m(lead, ST_PREP);
+    k_frame_prep<<<dim3(max_prep, n), 256, 0, st>>>(fb);
+    HIPCHK(hipGetLastError());
+  }
+  {
+    StageMark m(lead, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
+    k_recon<<<dim3(8 * ((2 * nsb + 7) / 8), n), 64, 0, st>>>(fb, lead->dbg_recon);
+    HIPCHK(hipGetLastError());
+  }
+  if (any_intra) {
+    StageMark m(lead, ST_INTRA);
+    // one single-wave chain per (SB row, component); LDS holds the row's CU words
+    size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
+    k_intra<<<dim3(3 * nrows, n), 64, lds, st>>>(fb, lead->dbg, lead->dbg_flags);
+    HIPCHK(hipGetLastError());
+  }
+  if (any_deblock) {
+    StageMark m(lead, ST_DEBLOCK);
+    int nv = ((W >> 3) - 1) * (H >> 3);
+    int nh = (W >> 3) * ((H >> 3) - 1);
+    // luma and both chroma planes of one edge direction per launch
+    const int bv = (nv + 255) / 256, bh = (nh + 255) / 256;
+    k_deblock_v<<<dim3(3 * bv, n), 256, 0, st>>>(fb, bv);
+    k_deblock_h<<<dim3(3 * bh, n), 256, 0, st>>>(fb, bh);
+    HIPCHK(hipGetLastError());
+  }
+  if (any_clpf && (W / 64) * (H / 64) > 0) {
+    StageMark m(lead, ST_CLPF);
+    k_clpf<<<dim3((W / 64) * (H / 64), n), 256, 0, st>>>(fb);
+    HIPCHK(hipGetLastError());
+  }
+  {
+    StageMark m(lead, ST_PAD);
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(fb);
+    HIPCHK(hipGetLastError());
+  }
+  // later work a member context enqueues on its own stream follows this batch
+  bool rec = false;
+  for (int i = 1; i < n; i++)
+    if (ds[i]->stream != st) {
+      if (!rec) HIPCHK(hipEventRecord(lead->xev[1], st));
+      rec = true;
+      HIPCHK(hipStreamWaitEvent(ds[i]->stream, lead->xev[1], 0));
+    }
+  for (int i = 0; i < n; i++) {
+    ds[i]->slot_fnum[cur[i]] = hdrs[i].frame_num;
+    ds[i]->slot_age[cur[i]] = ds[i]->decode_count++;
+  }
+  (void)nsb;
+  return THOR_OK;
 }
 
 int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
                    const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
                    const uint32_t *tu_list, int n_tu) {
-  if (!d || !hdr || nblocks < 0 || (nblocks > 0 && !blocks)) return THOR_ERR_ARG;
-  if (n_intra > 0 && !intra_list) return THOR_ERR_ARG;
-  if (n_tu < 0 || (n_tu > 0 && (!tu_list || !coeffs))) return THOR_ERR_ARG;
-  HIPCHK(hipSetDevice(d->device));
-  int W = d->seq.width, H = d->seq.height;
-  int cur = pick_slot(d, hdr->frame_num);
-  FrameCtx f = make_ctx(d, cur, hdr->frame_num);
-  // k_recon resolves references through a 128-entry table keyed by
-  // frame_num & 127: resident frame numbers must be distinct modulo 128
-  for (int a = 0; a < f.nref; a++)
-    for (int b = a + 1; b < f.nref; b++)
-      if (((f.ref_fnum[a] ^ f.ref_fnum[b]) & 127) == 0) return THOR_ERR_REF;
-  hipStream_t st = d->stream;
-  if (nblocks > 0) {
-    {
-      // side info + residuals of every coded transform block + intra chain setup
-      StageMark m(d, ST_PREP);
-      const int nrows = (H + 63) / 64;
-      int *rowstart = (int *)(d->progress + 3 * (nrows + 1));
-      const int nprep = (nblocks + 3) / 4, nres = (n_tu + 3) / 4;
-      k_frame_prep<<<nprep + nres + 1, 256, 0, st>>>(blocks, nblocks, d->cellinfo, d->cellmap, tu_list, n_tu, coeffs,
-                                                     d->resid, intra_list, n_intra, d->ctl, d->progress, rowstart,
-                                                     nrows, W, H, nprep, nres);
-      HIPCHK(hipGetLastError());
-    }
-    int nsb = ((W + 63) / 64) * ((H + 63) / 64);
-    StageMark m(d, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
-    k_recon<<<8 * ((2 * nsb + 7) / 8), 64, 0, st>>>(f, blocks, coeffs, d->cellmap, d->resid, d->dbg_recon);
-    HIPCHK(hipGetLastError());
-  }
-  if (n_intra > 0) {
-    int nrows = (H + 63) / 64;
-    StageMark m(d, ST_INTRA);
-    int *rowstart = (int *)(d->progress + 3 * (nrows + 1));  // set up by k_frame_prep
-    // full SB images only when inter CUs were reconstructed (their pixels are intra neighbours)
-    int full_sb = n_intra < nblocks;
-    // one single-wave chain per (SB row, component); LDS holds the row's CU words
-    size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
-    k_intra<<<3 * nrows, 64, lds, st>>>(f, blocks, intra_list, rowstart, d->ctl, d->progress, nrows, d->dbg,
-                                        d->dbg_flags, full_sb, d->resid);
-    HIPCHK(hipGetLastError());
-  }
-  if (d->stop_stage >= 1 && d->seq.deblocking) {
-    StageMark m(d, ST_DEBLOCK);
-    int nv = ((W >> 3) - 1) * (H >> 3);
-    int nh = (W >> 3) * ((H >> 3) - 1);
-    int qpc = chroma_qp_host(hdr->qp);
-    // luma and both chroma planes of one edge direction per launch
-    const int bv = (nv + 255) / 256, bh = (nh + 255) / 256;
-    k_deblock_v<<<3 * bv, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, hdr->qp, qpc, bv, bv);
-    k_deblock_h<<<3 * bh, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, hdr->qp, qpc, bh, bh);
-    HIPCHK(hipGetLastError());
-  }
-  if (d->stop_stage >= 2 && d->seq.clpf && hdr->clpf_on && clpf_flags) {
-    int nsb = (W / 64) * (H / 64);
-    if (nsb > 0) {
-      StageMark m(d, ST_CLPF);
-      k_clpf<<<nsb, 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H, d->cellinfo, clpf_flags);
-      HIPCHK(hipGetLastError());
-    }
-  }
-  {
-    StageMark m(d, ST_PAD);
-    k_pad<<<dim3(H + 2 * THOR_PAD_Y, 3), 256, 0, st>>>(f.cy, f.cu, f.cv, d->sy, d->sc, W, H);
-    HIPCHK(hipGetLastError());
-  }
-  d->slot_fnum[cur] = hdr->frame_num;
-  d->slot_age[cur] = d->decode_count++;
-  return THOR_OK;
+  if (!d || !hdr) return THOR_ERR_ARG;
+  thor_frame_in_t in = {blocks, nblocks, coeffs, clpf_flags, intra_list, n_intra, tu_list, n_tu};
+  return thor_dec_frames(&d, 1, hdr, &in);
 }
 
 // Debug hook (not in the public header): per-row intra timing into a device
@@ -468,9 +534,20 @@ int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const u
   HIPCHK(hipMemcpy2D(base + d->offy, d->sy, y, W, W, H, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy2D(base + d->offu, d->sc, u, W / 2, W / 2, H / 2, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy2D(base + d->offv, d->sc, v, W / 2, W / 2, H / 2, hipMemcpyHostToDevice));
-  k_pad<<<dim3(H + 2 * THOR_PAD_Y, 3), 256, 0, d->stream>>>(base + d->offy, base + d->offu, base + d->offv, d->sy,
-                                                            d->sc, W, H);
-  HIPCHK(hipGetLastError());
+  {
+    FrameBatch fb;
+    memset(&fb, 0, sizeof(fb));
+    FrameCtx *hp = fb.f;
+    hp->cy = base + d->offy;
+    hp->cu = base + d->offu;
+    hp->cv = base + d->offv;
+    hp->sy = d->sy;
+    hp->sc = d->sc;
+    hp->W = W;
+    hp->H = H;
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(fb);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipStreamSynchronize(d->stream));
   d->slot_fnum[s] = frame_num;
   d->slot_age[s] = d->decode_count++;

@@ -12,8 +12,9 @@
 // block_mode_t, common/types.h:83-90
 enum { M_SKIP = 0, M_INTRA = 1, M_INTER = 2, M_BIPRED = 3, M_MERGE = 4 };
 
-// Everything a per-frame kernel needs to address the current frame and the
-// resident references.  Passed by value (kernel argument segment).
+// Everything a per-frame kernel needs to address the current frame, the
+// resident references and the frame's parse output.  One per frame of a
+// batch (FrameBatch below).
 struct FrameCtx {
   uint8_t *cy, *cu, *cv;  // current frame, interior (0,0)
   const uint8_t *slots;   // base of the reference ring
@@ -25,15 +26,36 @@ struct FrameCtx {
   int frame_num;
   int bipred;             // sequence-level luma filter table select (dec/maindec.c:147)
   int nref;
-  int ref_fnum[THOR_MAX_SLOTS];
-  int ref_slot[THOR_MAX_SLOTS];
   int slot_lut[32];       // frame_num & 127 -> slot (int8, -1 none), 4 per word
   // Edge rows: the bottom pixel row of every SB row, per component (the only
   // pixels one intra chain hands to the next).  Y rows of ewy bytes, then U
   // and V rows of ewc bytes; column x at byte EDGE_MARGIN + x.
   uint8_t *edge;
   int ewy, ewc, nsbrows;
+  // The frame's job (parse output, DEVICE pointers) and its context's work
+  // buffers.  Batched launches read one FrameCtx per frame from device memory
+  // (grid y / z = frame of the batch).
+  const thor_block_t *blk;
+  const int16_t *coeffs;
+  const uint32_t *tus, *ilist;
+  const uint8_t *clpf_flags;
+  uint16_t *cellinfo;
+  int32_t *cellmap;
+  int16_t *resid;
+  unsigned *ctl, *progress;
+  int *rowstart;
+  int nblocks, ntus, nintra, nprep, nres, full_sb;
+  int qp, qpc, deblock, clpf_on;
 };
+// A batch of frames travels in the kernel argument segment (8 x 384 B, under
+// the 4 KB kernarg limit): the host fills it per call, no upload copy.  Every
+// batched kernel takes it as its FIRST argument and reads the per-frame
+// contexts straight from the kernarg segment (scalar loads, dynamic index).
+#define THOR_MAX_BATCH 8
+struct FrameBatch {
+  FrameCtx f[THOR_MAX_BATCH];
+};
+#define FRAME_BATCH_CTX() ((const FrameCtx *)__builtin_amdgcn_kernarg_segment_ptr())
 #define EDGE_MARGIN 32
 
 // Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits
@@ -79,13 +101,6 @@ __device__ __forceinline__ int dct32_entry(int k, int n) {
 __device__ __forceinline__ const uint8_t *slot_plane(const FrameCtx &f, int slot, int comp) {
   const uint8_t *s = f.slots + (long long)slot * f.slot_bytes;
   return s + (comp == 0 ? f.offy : (comp == 1 ? f.offu : f.offv));
-}
-
-// Reference lookup by display frame number; -1 if not resident.
-__device__ __forceinline__ int find_slot(const FrameCtx &f, int fnum) {
-  for (int r = 0; r < f.nref; r++)
-    if (f.ref_fnum[r] == fnum) return f.ref_slot[r];
-  return -1;
 }
 
 // gdequant_table, common/common_block.c:98

@@ -157,7 +157,7 @@ struct LdsLuma {
   }
 };
 struct GlobLuma {
-  static constexpr bool PF = true;
+  static constexpr bool PF = false;
   __amdgpu_buffer_rsrc_t ring;
   int o, stride;  // ring offset of strip row 0, column -2 (dword aligned)
   __device__ __forceinline__ void get(int r, uint32_t d[3]) const {
@@ -174,7 +174,7 @@ struct LdsChroma {
   }
 };
 struct GlobChroma {
-  static constexpr bool PF = true;
+  static constexpr bool PF = false;
   __amdgpu_buffer_rsrc_t ring;
   int o, uvd, stride;  // ring offset (U) of strip row 0, column -1 (dword aligned)
   __device__ __forceinline__ void get(int r, uint32_t du[2], uint32_t dv[2]) const {
@@ -500,11 +500,15 @@ __device__ __forceinline__ uint32_t add_res2(uint32_t p, const int16_t *__restri
          put_byte(clip255((int)((p >> 8) & 255) + (int)(int16_t)(a >> 16)), 1);
 }
 
-__global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__restrict__ blk,
-                                              const int16_t *__restrict__ coeffs,
-                                              const int32_t *__restrict__ cellmap, int16_t *__restrict__ resid,
-                                              unsigned long long *__restrict__ dbg) {
+__global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned long long *__restrict__ dbg) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ ReconLds L;
+  const FrameCtx &f = F[blockIdx.y];
+  if (f.nblocks <= 0) return;
+  if (blockIdx.y) dbg = nullptr;
+  const thor_block_t *__restrict__ blk = f.blk;
+  const int32_t *__restrict__ cellmap = f.cellmap;
+  int16_t *__restrict__ resid = f.resid;
   const int lane = threadIdx.x;
   // debug only (null in the product path): s_memrealtime stamps, 8 u64 per wave
   unsigned long long *stamp = dbg ? dbg + blockIdx.x * 8 : nullptr;
@@ -526,10 +530,8 @@ __global__ __launch_bounds__(64) void k_recon(FrameCtx f, const thor_block_t *__
   const int sby = sb / sbw, sbx = sb - sby * sbw;
   const int cs = f.W >> 2;
 
-  // reference lookup table, straight from the kernel argument (packed by the host)
-  if (lane < 32)
-    *(int *)&L.lut[4 * lane] =
-        ((const int *)((const char *)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(FrameCtx, slot_lut)))[lane];
+  // reference lookup table (packed by the host)
+  if (lane < 32) *(int *)&L.lut[4 * lane] = f.slot_lut[lane];
 
   // ---- P0: lane = cell row cr of 8x8 unit uu of the half ----
   const int uu = lane >> 1, cr = lane & 1;

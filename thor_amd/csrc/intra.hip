@@ -620,29 +620,33 @@ __device__ __forceinline__ void intra_setup_body(const thor_block_t *__restrict_
 // transform blocks (resid_tu, four per workgroup), and one last workgroup that
 // sets up the intra chains (row segments of the intra list, progress words).
 // All three only read the frame's parse output.
-__global__ __launch_bounds__(256) void k_frame_prep(const thor_block_t *__restrict__ blk, int nblocks,
-                                                    uint16_t *__restrict__ cellinfo, int32_t *__restrict__ cellmap,
-                                                    const uint32_t *__restrict__ tus, int ntus,
-                                                    const int16_t *__restrict__ coeffs, int16_t *__restrict__ resid,
-                                                    const uint32_t *__restrict__ ilist, int n_intra, unsigned *ctl,
-                                                    unsigned *progress, int *rowstart, int nrows, int W, int H,
-                                                    int nprep, int nres) {
+__global__ __launch_bounds__(256) void k_frame_prep(const FrameBatch fb_) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ ResidLds RL[4];
+  const FrameCtx &f = F[blockIdx.y];
   const int b = blockIdx.x;
-  if (b < nprep) prep_body(b, blk, nblocks, cellinfo, cellmap, W >> 2);
-  else if (b < nprep + nres) {
+  if (f.nblocks <= 0) return;
+  if (b < f.nprep) prep_body(b, f.blk, f.nblocks, f.cellinfo, f.cellmap, f.W >> 2);
+  else if (b < f.nprep + f.nres) {
     const int w = threadIdx.x >> 6;
-    resid_tu(RL[w], (b - nprep) * 4 + w, blk, tus, ntus, coeffs, resid, W, H);
-  } else if (n_intra > 0) {
-    intra_setup_body(blk, ilist, n_intra, ctl, progress, rowstart, nrows);
+    resid_tu(RL[w], (b - f.nprep) * 4 + w, f.blk, f.tus, f.ntus, f.coeffs, f.resid, f.W, f.H);
+  } else if (b == f.nprep + f.nres && f.nintra > 0) {
+    intra_setup_body(f.blk, f.ilist, f.nintra, f.ctl, f.progress, f.rowstart, f.nsbrows);
   }
 }
 
-__global__ __launch_bounds__(64) void k_intra(FrameCtx f, const thor_block_t *__restrict__ blk,
-                                              const uint32_t *__restrict__ list, const int *__restrict__ rowstart,
-                                              unsigned *ctl, unsigned *progress, int nrows, unsigned long long *dbg,
-                                              int dbg_flags, int full_sb, const int16_t *__restrict__ resid) {
+__global__ __launch_bounds__(64) void k_intra(const FrameBatch fb_, unsigned long long *dbg, int dbg_flags) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ IntraChain L;
+  const FrameCtx &f = F[blockIdx.y];
+  if (f.nintra <= 0) return;
+  if (blockIdx.y) dbg = nullptr;
+  const thor_block_t *__restrict__ blk = f.blk;
+  const uint32_t *__restrict__ list = f.ilist;
+  const int *__restrict__ rowstart = f.rowstart;
+  unsigned *ctl = f.ctl, *progress = f.progress;
+  const int nrows = f.nsbrows, full_sb = f.full_sb;
+  const int16_t *__restrict__ resid = f.resid;
   const int lane = threadIdx.x;
   for (;;) {
     const int task = (int)__builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&ctl[0], 1u) : 0u);

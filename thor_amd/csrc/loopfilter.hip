@@ -180,36 +180,40 @@ __device__ __forceinline__ void k_deblock_chroma_h_body(int bx, int by, uint8_t 
 // Every 8x8 block that is not BIPRED is filtered per plane with coded
 // residual (clpf_block, common/common_block.c:180-197), reading the
 // unfiltered SB (LDS copy) with clamping at the SB border.
-// One launch per edge direction: luma blocks first, then U, then V (the
-// chroma filters read only the cell side info, never luma pixels, so the
-// planes are independent within a pass; vertical edges of all planes before
-// horizontal ones, deblock_frame_y / deblock_frame_uv, common/common_frame.c:46-321).
-__global__ __launch_bounds__(256) void k_deblock_v(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
-                                                   const uint16_t *cell, int qp, int qpc, int nbl, int nbc) {
+// One launch per edge direction for every frame of a batch (grid y = frame):
+// luma blocks first, then U, then V (the chroma filters read only the cell
+// side info, never luma pixels, so the planes are independent within a pass;
+// vertical edges of all planes before horizontal ones, deblock_frame_y /
+// deblock_frame_uv, common/common_frame.c:46-321).
+__global__ __launch_bounds__(256) void k_deblock_v(const FrameBatch fb_, int nbl) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
+  const FrameCtx &f = F[blockIdx.y];
+  if (!f.deblock) return;
   const int b = blockIdx.x;
-  if (b < nbl) k_deblock_luma_v_body(b, Y, sy, W, H, cell, qp);
+  if (b < nbl) k_deblock_luma_v_body(b, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
   else {
-    const int c = (b - nbl) >= nbc;
-    k_deblock_chroma_v_body(b - nbl - c * nbc, c, U, V, sc, W, H, cell, qpc);
+    const int c = (b - nbl) >= nbl;
+    k_deblock_chroma_v_body(b - nbl - c * nbl, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
   }
 }
-__global__ __launch_bounds__(256) void k_deblock_h(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
-                                                   const uint16_t *cell, int qp, int qpc, int nbl, int nbc) {
+__global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
+  const FrameCtx &f = F[blockIdx.y];
+  if (!f.deblock) return;
   const int b = blockIdx.x;
-  if (b < nbl) k_deblock_luma_h_body(b, Y, sy, W, H, cell, qp);
+  if (b < nbl) k_deblock_luma_h_body(b, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
   else {
-    const int c = (b - nbl) >= nbc;
-    k_deblock_chroma_h_body(b - nbl - c * nbc, c, U, V, sc, W, H, cell, qpc);
+    const int c = (b - nbl) >= nbl;
+    k_deblock_chroma_h_body(b - nbl - c * nbl, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
   }
 }
 
-__global__ __launch_bounds__(256) void k_clpf(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
-                                              const uint16_t *cell, const uint8_t *flags) {
-  __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];
-  __shared__ int cand;
+__device__ __forceinline__ void k_clpf_body(int bx, uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
+                                            const uint16_t *cell, const uint8_t *flags, uint8_t *sY, uint8_t *sU,
+                                            uint8_t *sV, int &cand) {
   int nh = W >> 6;
-  int k = blockIdx.x / nh, l = blockIdx.x - (blockIdx.x / nh) * nh;
-  if (!flags[blockIdx.x]) return;
+  int k = bx / nh, l = bx - (bx / nh) * nh;
+  if (!flags[bx]) return;
   int tid = threadIdx.x;
   int cs = W >> 2;
   if (tid == 0) cand = 0;
@@ -262,32 +266,99 @@ __global__ __launch_bounds__(256) void k_clpf(uint8_t *Y, uint8_t *U, uint8_t *V
     (pl ? v0 : u0)[(long long)r * sc + c] = (uint8_t)(X + delta);
   }
 }
+__global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
+  __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];
+  __shared__ int cand;
+  const FrameCtx &f = F[blockIdx.y];
+  if (!f.clpf_on || (int)blockIdx.x >= (f.W >> 6) * (f.H >> 6)) return;
+  k_clpf_body(blockIdx.x, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, cand);
+}
+
 
 // pad_yuv_frame (common/common_frame.c:405-462): every padding byte equals
-// the nearest interior pixel (rows clamp, then columns clamp).  One workgroup
-// per padded row of one plane; blockIdx.y = plane.
-__global__ __launch_bounds__(256) void k_pad(uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H) {
-  int plane = blockIdx.y;
-  uint8_t *P = plane == 0 ? Y : (plane == 1 ? U : V);
-  int s = plane ? sc : sy;
-  int w = plane ? W >> 1 : W, h = plane ? H >> 1 : H;
-  int pad = plane ? THOR_PAD_C : THOR_PAD_Y;
-  int row = (int)blockIdx.x - pad;
-  if (row >= h + pad) return;
-  int src_row = row < 0 ? 0 : (row >= h ? h - 1 : row);
-  const uint8_t *src = P + (long long)src_row * s;
-  uint8_t *dst = P + (long long)row * s;
-  if (row >= 0 && row < h) {
-    int t = threadIdx.x;
-    if (t < pad) dst[-pad + t] = src[0];
-    else if (t < 2 * pad) dst[w + t - pad] = src[w - 1];
-  } else {
-    // full padded row: w + 2*pad bytes (multiple of 16 for our strides)
-    int total = w + 2 * pad;
-    for (int c = threadIdx.x; c < total; c += 256) {
-      int sc_ = c - pad;
-      sc_ = sc_ < 0 ? 0 : (sc_ >= w ? w - 1 : sc_);
-      dst[c - pad] = src[sc_];
-    }
+// the nearest interior pixel (rows clamp, then columns clamp).  Work unit = one
+// 16-byte chunk of padding: per plane, the side margins of every interior row
+// (left [-pad, 0), right [w & ~15, w + pad) -- a chunk straddling the right
+// edge keeps its interior bytes), then the top / bottom pad rows over
+// [-pad, w + pad) rounded up to 16 (still inside the stride).  Rows start
+// 16-byte aligned at x = -pad (create_yuv_frame's strides and pads).
+struct PadPlane {
+  uint8_t *P;
+  int s, w, h, pad, nl, nr, rc, sides, total;
+  __device__ __forceinline__ PadPlane(uint8_t *P_, int s_, int w_, int h_, int pad_) : P(P_), s(s_), w(w_), h(h_), pad(pad_) {
+    nl = pad >> 4;
+    nr = (w + pad - (w & ~15) + 15) >> 4;
+    rc = (w + 2 * pad + 15) >> 4;
+    sides = h * (nl + nr);
+    total = sides + 2 * pad * rc;
   }
+  __device__ __forceinline__ void chunk(int e) const {
+    int row, x0;
+    const uint8_t *src;
+    if (e < sides) {
+      row = e / (nl + nr);
+      const int k = e - row * (nl + nr);
+      src = P + (long long)row * s;
+      x0 = k < nl ? -pad + 16 * k : (w & ~15) + 16 * (k - nl);
+    } else {
+      const int e2 = e - sides, r = e2 / rc;
+      x0 = -pad + 16 * (e2 - r * rc);
+      row = r < pad ? r - pad : h + (r - pad);
+      src = P + (long long)(r < pad ? 0 : h - 1) * s;
+    }
+    uint8_t *dst = P + (long long)row * s + x0;
+    uint4 v;
+    if (x0 >= 0 && x0 + 16 <= w) {
+      v = *(const uint4 *)(src + x0);
+    } else if (x0 + 16 <= 0 || x0 >= w) {
+      const uint32_t b = (uint32_t)src[x0 < 0 ? 0 : w - 1] * 0x01010101u;
+      v = make_uint4(b, b, b, b);
+    } else {
+      uint32_t wd[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          int x = x0 + 4 * q + j;
+          x = x < 0 ? 0 : (x > w - 1 ? w - 1 : x);
+          acc |= (uint32_t)src[x] << (8 * j);
+        }
+        wd[q] = acc;
+      }
+      v = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
+    *(uint4 *)dst = v;
+  }
+};
+__device__ __forceinline__ void k_pad_body(int e, uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H) {
+  const PadPlane py(Y, sy, W, H, THOR_PAD_Y);
+  if (e < py.total) {
+    py.chunk(e);
+    return;
+  }
+  e -= py.total;
+  const PadPlane pu(U, sc, W >> 1, H >> 1, THOR_PAD_C);
+  if (e < pu.total) {
+    pu.chunk(e);
+    return;
+  }
+  e -= pu.total;
+  const PadPlane pv(V, sc, W >> 1, H >> 1, THOR_PAD_C);
+  if (e < pv.total) pv.chunk(e);
+}
+// every frame of a batch (grid z); also used on one frame by thor_dec_write_frame
+__global__ __launch_bounds__(256) void k_pad(const FrameBatch fb_) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
+  const FrameCtx &f = F[blockIdx.y];
+  k_pad_body(blockIdx.x * 256 + threadIdx.x, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H);
+}
+// 16-byte chunks of padding of one frame (host-side copy of PadPlane's count)
+static inline int pad_chunks(int W, int H) {
+  auto plane = [](int w, int h, int pad) {
+    const int nl = pad >> 4, nr = (w + pad - (w & ~15) + 15) >> 4, rc = (w + 2 * pad + 15) >> 4;
+    return h * (nl + nr) + 2 * pad * rc;
+  };
+  return plane(W, H, THOR_PAD_Y) + 2 * plane(W >> 1, H >> 1, THOR_PAD_C);
 }

@@ -108,6 +108,9 @@ class GpuDecoder:
                                      d.intra, d.n_intra, d.tus, d.n_tu)
         L.check(rc, "thor_dec_frame")
 
+    def frame_in(self, d: DeviceFrame) -> L.ThorFrameIn:
+        return L.ThorFrameIn(d.blocks, d.nblocks, d.coeffs, d.clpf or None, d.intra, d.n_intra, d.tus, d.n_tu)
+
     def set_stop_stage(self, stage: int):
         L.check(self.lib.thor_dec_set_stop_stage(self.h, stage), "thor_dec_set_stop_stage")
 
@@ -136,3 +139,14 @@ class GpuDecoder:
         y, u, v = (np.ascontiguousarray(p, dtype=np.uint8) for p in (y, u, v))
         L.check(self.lib.thor_dec_write_frame(self.h, frame_num, y.ctypes.data, u.ctypes.data, v.ctypes.data),
                 "thor_dec_write_frame")
+
+
+def decode_batch(decs, frames):
+    """Decode frames[i] (a DeviceFrame of decs[i]) for every i with one launch
+    per stage (thor_dec_frames); the contexts must be distinct."""
+    n = len(decs)
+    lib = decs[0].lib
+    hs = (C.c_void_p * n)(*[d.h for d in decs])
+    hdrs = (L.ThorFrameHdr * n)(*[f.hdr for f in frames])
+    ins = (L.ThorFrameIn * n)(*[d.frame_in(f) for d, f in zip(decs, frames)])
+    L.check(lib.thor_dec_frames(hs, n, hdrs, ins), "thor_dec_frames")

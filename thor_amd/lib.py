@@ -21,9 +21,14 @@ class ThorFrameHdr(C.Structure):
     _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32)]
 
 
+class ThorFrameIn(C.Structure):
+    _fields_ = [("blocks", C.c_void_p), ("nblocks", C.c_int32), ("coeffs", C.c_void_p), ("clpf_flags", C.c_void_p),
+                ("intra_list", C.c_void_p), ("n_intra", C.c_int32), ("tu_list", C.c_void_p), ("n_tu", C.c_int32)]
+
+
 # Every symbol the public headers declare (checked by tests/test_capi.py).
 BATCHED_SYMBOLS = [
-    "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_build_intra_list", "thor_build_tu_list", "thor_dec_set_stop_stage",
+    "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_dec_frames", "thor_build_intra_list", "thor_build_tu_list", "thor_dec_set_stop_stage",
     "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_stage_marks", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
@@ -57,6 +62,8 @@ def load(path: str = LIB_PATH):
     L.thor_dec_destroy.argtypes = [P]
     L.thor_dec_frame.argtypes = [P, C.POINTER(ThorFrameHdr), P, i, P, P, P, i, P, i]
     L.thor_dec_frame.restype = i
+    L.thor_dec_frames.argtypes = [P, i, P, P]
+    L.thor_dec_frames.restype = i
     L.thor_build_intra_list.argtypes = [P, i, P]
     L.thor_build_intra_list.restype = i
     L.thor_build_tu_list.argtypes = [P, i, P]

@@ -39,10 +39,16 @@ def pmc(db, counter):
 
 
 def per_dispatch(db, counter, kernel):
+    """Values of `counter` for the widest-grid dispatches of `kernel` (the
+    batched launches), in dispatch order."""
     c = sqlite3.connect(db)
-    rows = c.execute("select kernel_name, value from counters_collection where counter_name=? order by dispatch_id",
-                     (counter,))
-    return [float(v) for n, v in rows if short(n) == kernel]
+    rows = [(float(v), int(g)) for n, v, g in c.execute(
+        "select kernel_name, value, grid_size from counters_collection where counter_name=? order by dispatch_id",
+        (counter,)) if short(n) == kernel]
+    if not rows:
+        return []
+    gmax = max(g for _, g in rows)
+    return [v for v, g in rows if g == gmax]
 
 
 def main():
@@ -83,8 +89,8 @@ def main():
         wb = w.get(k, 0.0) * 1024
         traffic["kernels"][k] = {"fetch_kib_raw": round(f.get(k, 0.0), 1), "write_kib_raw": round(w.get(k, 0.0), 1),
                                  "hbm_bytes_per_launch": round(fb + wb), "launches": nf.get(k, 0)}
-    # k_recon on P frames only: one launch per frame, the stream's frame 0 is the
-    # I frame (no inter pixels), so drop every 8th dispatch in dispatch order
+    # k_recon on P frames only: the batched launches (one group, frame order
+    # 0..7: frame 0 is the I frame, no inter pixels), so drop every 8th
     fr = per_dispatch(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE", "k_recon")
     wr = per_dispatch(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE", "k_recon")
     if fr and wr and len(fr) == len(wr):
@@ -92,6 +98,7 @@ def main():
         pw = [v for i, v in enumerate(wr) if i % 8 != 0]
         traffic["recon_hbm_bytes_per_p_launch"] = round((sum(pf) * 2 + sum(pw)) * 1024 / len(pf))
         traffic["recon_p_launches"] = len(pf)
+        traffic["recon_note"] = "bench.py --streams 4 --groups 1: one k_recon launch = 4 frames"
     json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
     # the GPU box does not receive profiles/ (.gpurunignore): bench.py reads this copy
     json.dump(traffic, open(os.path.join(root, "tools", "traffic_latest.json"), "w"), indent=1)
