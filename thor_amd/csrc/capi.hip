@@ -387,14 +387,14 @@ static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t
     int nv = ((W >> 3) - 1) * (H >> 3);
     int nh = (W >> 3) * ((H >> 3) - 1);
     // luma and both chroma planes of one edge direction per launch
-    const int bv = (nv + 255) / 256, bh = (nh + 255) / 256;
+    const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
     k_deblock_v<<<dim3(3 * bv, n), 256, 0, st>>>(fb, bv);
     k_deblock_h<<<dim3(3 * bh, n), 256, 0, st>>>(fb, bh);
     HIPCHK(hipGetLastError());
   }
   if (any_clpf && (W / 64) * (H / 64) > 0) {
     StageMark m(lead, ST_CLPF);
-    k_clpf<<<dim3((W / 64) * (H / 64), n), 256, 0, st>>>(fb);
+    k_clpf<<<dim3(((W / 64) * (H / 64) + CLPF_SBS - 1) / CLPF_SBS, n), 256, 0, st>>>(fb);
     HIPCHK(hipGetLastError());
   }
   {

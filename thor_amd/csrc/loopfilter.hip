@@ -37,14 +37,20 @@ __device__ __forceinline__ void filt4(int &p1, int &p0, int &q0, int &q1, int tc
 }
 
 // Vertical luma edges: one thread per (edge column j = 8e, 8-row group).
-__device__ __forceinline__ void k_deblock_luma_v_body(int bx, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
+__device__ __forceinline__ void k_deblock_luma_v_body(int t, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
                                                         int qp) {
   int ne = (W >> 3) - 1;
-  int t = bx * 256 + threadIdx.x;
   int g = t / ne, e = t - g * ne + 1;
   if (g >= (H >> 3)) return;
   int i = g * 8, j = e * 8;
   int beta = beta_of(qp), tc = tc_of(qp);
+  // the two 4-row segments' edge decisions first (side info only): most edges of
+  // a skip-dominated frame are off and need no pixel reads at all
+  const int cs = W >> 2;
+  const int qa = (i >> 2) * cs + (j >> 2), qb = qa + cs;
+  const bool on0 = luma_edge_on(cell[qa - 1], cell[qa], j, true);
+  const bool on1 = luma_edge_on(cell[qb - 1], cell[qb], j, true);
+  if (!on0 && !on1) return;
   uint8_t *base = Y + (long long)i * sy + j - 4;
   uint32_t A[8], Bv[8];
   for (int r = 0; r < 8; r++) {
@@ -58,12 +64,8 @@ __device__ __forceinline__ void k_deblock_luma_v_body(int bx, uint8_t *Y, int sy
 #define Q1(r) ((int)((Bv[r] >> 8) & 255))
   int d = abs(P1(2) - P0(2)) + abs(Q1(2) - Q0(2)) + abs(P1(5) - P0(5)) + abs(Q1(5) - Q0(5));
   if (d >= beta) return;
-  int cs = W >> 2;
-  bool any = false;
   for (int m = 0; m < 8; m += 4) {
-    int qi = ((i + m) >> 2) * cs + (j >> 2);
-    if (!luma_edge_on(cell[qi - 1], cell[qi], j, true)) continue;
-    any = true;
+    if (!(m ? on1 : on0)) continue;
     for (int r = m; r < m + 4; r++) {
       int p1 = P1(r), p0 = P0(r), q0 = Q0(r), q1 = Q1(r);
       filt4(p1, p0, q0, q1, tc);
@@ -75,7 +77,6 @@ __device__ __forceinline__ void k_deblock_luma_v_body(int bx, uint8_t *Y, int sy
 #undef P0
 #undef Q0
 #undef Q1
-  if (!any) return;
   for (int r = 0; r < 8; r++) {
     *(uint32_t *)(base + (long long)r * sy) = A[r];
     *(uint32_t *)(base + (long long)r * sy + 4) = Bv[r];
@@ -83,27 +84,27 @@ __device__ __forceinline__ void k_deblock_luma_v_body(int bx, uint8_t *Y, int sy
 }
 
 // Horizontal luma edges: one thread per (edge row i = 8k >= 8, 8-column group).
-__device__ __forceinline__ void k_deblock_luma_h_body(int bx, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
+__device__ __forceinline__ void k_deblock_luma_h_body(int t, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
                                                         int qp) {
   int ng = W >> 3;
-  int t = bx * 256 + threadIdx.x;
   int k = t / ng, gcol = t - k * ng;
   int i = (k + 1) * 8, j = gcol * 8;
   if (i >= H) return;
   int beta = beta_of(qp), tc = tc_of(qp);
+  const int cs = W >> 2;
+  const int qa = (i >> 2) * cs + (j >> 2);
+  const bool on0 = luma_edge_on(cell[qa - cs], cell[qa], i, false);
+  const bool on1 = luma_edge_on(cell[qa + 1 - cs], cell[qa + 1], i, false);
+  if (!on0 && !on1) return;
   uint8_t *base = Y + (long long)(i - 2) * sy + j;
   uint2 rows[4];  // rows i-2 .. i+1 (p1, p0, q0, q1)
   for (int r = 0; r < 4; r++) rows[r] = *(uint2 *)(base + (long long)r * sy);
   auto px = [&](int r, int c) -> int { return (int)(((c < 4 ? rows[r].x : rows[r].y) >> (8 * (c & 3))) & 255); };
   int d = abs(px(0, 2) - px(1, 2)) + abs(px(3, 2) - px(2, 2)) + abs(px(0, 5) - px(1, 5)) + abs(px(3, 5) - px(2, 5));
   if (d >= beta) return;
-  int cs = W >> 2;
-  bool any = false;
   uint32_t out[4][2] = {{rows[0].x, rows[0].y}, {rows[1].x, rows[1].y}, {rows[2].x, rows[2].y}, {rows[3].x, rows[3].y}};
   for (int n = 0; n < 8; n += 4) {
-    int qi = (i >> 2) * cs + ((j + n) >> 2);
-    if (!luma_edge_on(cell[qi - cs], cell[qi], i, false)) continue;
-    any = true;
+    if (!(n ? on1 : on0)) continue;
     int w = n >> 2;
     uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
     for (int c = 0; c < 4; c++) {
@@ -116,17 +117,15 @@ __device__ __forceinline__ void k_deblock_luma_h_body(int bx, uint8_t *Y, int sy
     }
     out[0][w] = o0; out[1][w] = o1; out[2][w] = o2; out[3][w] = o3;
   }
-  if (!any) return;
   for (int r = 0; r < 4; r++) *(uint2 *)(base + (long long)r * sy) = make_uint2(out[r][0], out[r][1]);
 }
 
 // Chroma (deblock_frame_uv): intra-only edges, p0/q0 modified.  One thread
 // per (edge, 8-luma-row/column group) per plane (blockIdx.y = plane).
-__device__ __forceinline__ void k_deblock_chroma_v_body(int bx, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
+__device__ __forceinline__ void k_deblock_chroma_v_body(int t, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
                                                           const uint16_t *cell, int qpc) {
   uint8_t *C = by ? V : U;
   int ne = (W >> 3) - 1;
-  int t = bx * 256 + threadIdx.x;
   int g = t / ne, e = t - g * ne + 1;
   if (g >= (H >> 3)) return;
   int i = g * 8, j = e * 8;
@@ -148,11 +147,10 @@ __device__ __forceinline__ void k_deblock_chroma_v_body(int bx, int by, uint8_t 
   }
 }
 
-__device__ __forceinline__ void k_deblock_chroma_h_body(int bx, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
+__device__ __forceinline__ void k_deblock_chroma_h_body(int t, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
                                                           const uint16_t *cell, int qpc) {
   uint8_t *C = by ? V : U;
   int ng = W >> 3;
-  int t = bx * 256 + threadIdx.x;
   int k = t / ng, gcol = t - k * ng;
   int i = (k + 1) * 8, j = gcol * 8;
   if (i >= H) return;
@@ -185,15 +183,21 @@ __device__ __forceinline__ void k_deblock_chroma_h_body(int bx, int by, uint8_t 
 // side info, never luma pixels, so the planes are independent within a pass;
 // vertical edges of all planes before horizontal ones, deblock_frame_y /
 // deblock_frame_uv, common/common_frame.c:46-321).
+// DB_ITEMS edge segments per lane (grid-stride): the launch is a quarter as
+// many waves, and most segments of a skip-dominated frame end after two
+// side-info reads.
+#define DB_ITEMS 4
 __global__ __launch_bounds__(256) void k_deblock_v(const FrameBatch fb_, int nbl) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   const FrameCtx &f = F[blockIdx.y];
   if (!f.deblock) return;
   const int b = blockIdx.x;
-  if (b < nbl) k_deblock_luma_v_body(b, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
-  else {
-    const int c = (b - nbl) >= nbl;
-    k_deblock_chroma_v_body(b - nbl - c * nbl, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+  const int c = b < nbl ? -1 : ((b - nbl) >= nbl);
+  const int bb = c < 0 ? b : b - nbl - c * nbl;
+  for (int r = 0; r < DB_ITEMS; r++) {
+    const int t = bb * 256 + (int)threadIdx.x + r * nbl * 256;
+    if (c < 0) k_deblock_luma_v_body(t, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+    else k_deblock_chroma_v_body(t, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
   }
 }
 __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl) {
@@ -201,10 +205,12 @@ __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl
   const FrameCtx &f = F[blockIdx.y];
   if (!f.deblock) return;
   const int b = blockIdx.x;
-  if (b < nbl) k_deblock_luma_h_body(b, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
-  else {
-    const int c = (b - nbl) >= nbl;
-    k_deblock_chroma_h_body(b - nbl - c * nbl, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+  const int c = b < nbl ? -1 : ((b - nbl) >= nbl);
+  const int bb = c < 0 ? b : b - nbl - c * nbl;
+  for (int r = 0; r < DB_ITEMS; r++) {
+    const int t = bb * 256 + (int)threadIdx.x + r * nbl * 256;
+    if (c < 0) k_deblock_luma_h_body(t, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+    else k_deblock_chroma_h_body(t, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
   }
 }
 
@@ -266,13 +272,20 @@ __device__ __forceinline__ void k_clpf_body(int bx, uint8_t *Y, uint8_t *U, uint
     (pl ? v0 : u0)[(long long)r * sc + c] = (uint8_t)(X + delta);
   }
 }
+#define CLPF_SBS 1
 __global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];
   __shared__ int cand;
   const FrameCtx &f = F[blockIdx.y];
-  if (!f.clpf_on || (int)blockIdx.x >= (f.W >> 6) * (f.H >> 6)) return;
-  k_clpf_body(blockIdx.x, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, cand);
+  if (!f.clpf_on) return;
+  const int nsb = (f.W >> 6) * (f.H >> 6);
+  for (int r = 0; r < CLPF_SBS; r++) {  // CLPF_SBS SBs per workgroup (most are not flagged)
+    const int sb = blockIdx.x * CLPF_SBS + r;
+    if (sb >= nsb) break;
+    k_clpf_body(sb, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, cand);
+    __syncthreads();  // the next SB reuses the LDS copies
+  }
 }
 
 

@@ -38,14 +38,22 @@ __constant__ Dct32Table g_dct32 = Dct32Table();
 
 struct ResidLds {
   int8_t M[1024];
-  int16_t D[256];      // dequantised q x q tile
-  int16_t T[16 * 32];  // pass-1 output [k][y']
+  int16_t D[256];      // dequantised q x q tile, transposed: D[k][m]
+  int16_t T[16 * 32];  // pass-1 output, transposed: T[y][k]
 };
 
 __device__ __forceinline__ int sx8(int w, int i) { return __builtin_amdgcn_sbfe(w, 8 * i, 8); }
 
+typedef short s16x2_r __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int rdot2(uint32_t a, uint32_t b, int c) {  // a.lo*b.lo + a.hi*b.hi + c (int16 pairs)
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2_r, a), __builtin_bit_cast(s16x2_r, b), c, false);
+}
+
 // One TU across the wave; writes the n x n (x2 replicated for 64) residual
-// at `out` (row stride `ostride` int16).
+// at `out` (row stride `ostride` int16).  Lane p = lane % n owns basis column
+// p (q basis rows as int16 pairs in registers); the dequantised coefficients
+// (transposed) and the pass-1 output (transposed) are read as int16 pairs
+// broadcast to every lane of a group, so each pass is q/2 v_dot2 per output.
 __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int ntu, int qp, int16_t *__restrict__ out,
                            int ostride) {
   const int lane = threadIdx.x & 63;
@@ -53,40 +61,40 @@ __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int nt
   const int step = 32 / n;
   const int lshift = qp / 6, scale = dequant_scale(qp % 6);
   const int rshift = ilog2i(ntu) - 1, add = 1 << (rshift - 1);
-  for (int e = lane; e < q * q; e += 64)
-    L.D[e] = (int16_t)wrap16(((coef[e] * scale) * (1 << lshift) + add) >> rshift);  // int16 store, :143
+  for (int e = lane; e < q * q; e += 64) {  // dequantize (int16 store, common_block.c:143), transposed
+    const int m = e / q, k = e - m * q;
+    L.D[k * q + m] = (int16_t)wrap16(((coef[e] * scale) * (1 << lshift) + add) >> rshift);
+  }
+  const int p = lane & (n - 1), grp = lane / n, ngrp = 64 / n;
+  uint32_t mc[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    mc[j] = 2 * j < q ? ((uint32_t)(int)L.M[(2 * j * step) * 32 + p] & 0xffffu) |
+                            ((uint32_t)(int)L.M[((2 * j + 1) * step) * 32 + p] << 16)
+                      : 0u;
   wave_lds_sync();
-  for (int e = lane; e < q * n; e += 64) {  // pass 1, transform.c:455-463
-    const int k = e / n, yp = e - k * n;
-    int s = 0;
-    for (int m = 0; m < q; m++) s += (int)L.M[(m * step) * 32 + yp] * (int)L.D[m * q + k];
-    L.T[k * n + yp] = (int16_t)clip16((s + 64) >> 7);
+  for (int k = grp; k < q; k += ngrp) {  // pass 1, transform.c:455-463: T[k][p]
+    const uint32_t *dk = (const uint32_t *)&L.D[k * q];
+    int s = 64;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (2 * j < q) s = rdot2(mc[j], dk[j], s);
+    L.T[p * q + k] = (int16_t)clip16(s >> 7);
   }
   wave_lds_sync();
-  for (int e = lane; e < (n * n) >> 2; e += 64) {  // pass 2, four columns per lane, :466-484
-    const int yp = (e << 2) / n, xp = (e << 2) - yp * n;
-    int r[4] = {0, 0, 0, 0};
-    for (int k = 0; k < q; k++) {
-      const int t = L.T[k * n + yp];
-      const int mw = *(const int *)&L.M[(k * step) * 32 + xp];
+  for (int y = grp; y < n; y += ngrp) {  // pass 2, :466-484: out[y][p]
+    const uint32_t *ty = (const uint32_t *)&L.T[y * q];
+    int s = 2048;
 #pragma unroll
-      for (int j = 0; j < 4; j++) r[j] += sx8(mw, j) * t;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) r[j] = clip16((r[j] + 2048) >> 12);
+    for (int j = 0; j < 8; j++)
+      if (2 * j < q) s = rdot2(mc[j], ty[j], s);
+    const int r = clip16(s >> 12);
     if (rep) {  // 2x2 replication
-      uint4 w;
-      w.x = (uint32_t)(r[0] & 0xffff) * 0x10001u;
-      w.y = (uint32_t)(r[1] & 0xffff) * 0x10001u;
-      w.z = (uint32_t)(r[2] & 0xffff) * 0x10001u;
-      w.w = (uint32_t)(r[3] & 0xffff) * 0x10001u;
-      *(uint4 *)(out + (long long)(2 * yp) * ostride + 2 * xp) = w;
-      *(uint4 *)(out + (long long)(2 * yp + 1) * ostride + 2 * xp) = w;
+      const uint32_t w = (uint32_t)(r & 0xffff) * 0x10001u;
+      *(uint32_t *)(out + (long long)(2 * y) * ostride + 2 * p) = w;
+      *(uint32_t *)(out + (long long)(2 * y + 1) * ostride + 2 * p) = w;
     } else {
-      uint2 w;
-      w.x = (uint32_t)(r[0] & 0xffff) | ((uint32_t)r[1] << 16);
-      w.y = (uint32_t)(r[2] & 0xffff) | ((uint32_t)r[3] << 16);
-      *(uint2 *)(out + (long long)yp * ostride + xp) = w;
+      out[(long long)y * ostride + p] = (int16_t)r;
     }
   }
   wave_lds_sync();  // the next TU rewrites D and T
