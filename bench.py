@@ -113,6 +113,9 @@ def main():
     ap.add_argument("--streams", type=int, default=12, help="independent decoder contexts per GPU")
     ap.add_argument("--groups", type=int, default=3,
                     help="batches per frame slot (contexts of a group share one launch per stage)")
+    ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
+                    help="streams: independent streams per GPU (default); rows: ONE stream's SB rows split "
+                         "across the ranks with an RCCL all-gather of the bands before intra/deblock")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per k_recon launch (default tools/traffic_latest.json, "
                          "copied from profiles/<tag>_traffic.json by tools/prof_summary.py)")
@@ -132,6 +135,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
+
+    if a.shard == "rows":
+        return rows_mode(a, torch, dist, rank, world, local)
 
     from thor_amd import lib as L
     from thor_amd.decoder import GpuDecoder, decode_batch
@@ -318,6 +324,66 @@ def main():
         dk.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def rows_mode(a, torch, dist, rank, world, local):
+    """--shard rows: one 4K stream, its SB rows split across the ranks
+    (thor_amd/shard.py); strong scaling.  Each frame: band reconstruction,
+    RCCL all-gather of the bands (device buffers, torch's stream), then the
+    whole-frame intra / deblock / CLPF / pad on every rank."""
+    from thor_amd.decoder import GpuDecoder
+    from thor_amd.shard import RowShard
+    from thor_amd.trace import load_trace
+
+    if dist is None:  # a one-rank group keeps the same code path
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+    gold = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold, "streams.json")))["k4_low"]
+    seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
+    dec = GpuDecoder(seq, device=local)
+    dec.set_stream(C.c_void_p(torch.cuda.current_stream(local).cuda_stream))
+    devs = [dec.upload(fr) for fr in frames]
+    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True)
+
+    def step():
+        for d, fr in zip(devs, frames):
+            sh.decode(d, fr.frame_num)
+
+    for _ in range(max(1, a.warmup)):
+        step()
+    torch.cuda.synchronize(local)
+    got = {fr.frame_num: dec.read_i420(fr.frame_num) for fr in frames}
+    ok = hashlib.md5(b"".join(got[k] for k in sorted(got))).hexdigest() == meta["dec_md5"]
+    dist.barrier()
+    torch.cuda.synchronize(local)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(local)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    okt = torch.tensor([1 if ok else 0], device="cuda")
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    elapsed, ok = float(t.item()), bool(okt.item())
+    px_step = seq.width * seq.height * len(frames)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(px_step * a.steps / elapsed / 1e6, 2), "unit": "Mpixels/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u8/i16", "data": "synthetic (seeded clip) encoded by the reference Thorenc",
+            "bit_exact": ok,
+            "config": {"workload": "ONE 4K 8-frame LDB-low stream, SB rows sharded across %d GPU(s): band k_recon, "
+                                   "RCCL all-gather of pre-deblock bands, whole-frame intra/deblock/CLPF/pad" % world,
+                       "parallelism": "rows%d" % world, "frames": len(frames)},
+        }), flush=True)
+    dec.close()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -121,6 +121,22 @@ typedef struct thor_frame_in {
  * thor_dec_frame. */
 int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins);
 
+/* ---- row-band sharding of one stream across GPUs ---
+ * thor_dec_set_band: k_recon reconstructs only SB rows [sb_row0, sb_row1) of
+ * this context's frames (0, 0 = all).  thor_dec_frame_begin enqueues side info,
+ * residuals and the band's inter reconstruction; the caller then exchanges
+ * bands (thor_dec_get_rows / thor_dec_put_rows on DEVICE buffers, e.g. an RCCL
+ * all-gather on the same stream); thor_dec_frame_end enqueues intra, deblock,
+ * CLPF and padding of the whole frame.  Rows are packed Y (nrows x W) | U |
+ * V (nrows/2 x W/2 each); put_rows needs y0 on an SB row and also refreshes
+ * the SB-row edge rows the intra chains read.  Rows past the frame are
+ * skipped. */
+int thor_dec_set_band(thor_dec_t *d, int sb_row0, int sb_row1);
+int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_frame_in_t *in);
+int thor_dec_frame_end(thor_dec_t *d);
+int thor_dec_get_rows(thor_dec_t *d, int frame_num, int y0, int nrows, void *dst);
+int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const void *src);
+
 /* Host helper: write the decode-order indices of the intra CUs of a frame
  * (host descriptors) to `out` (may be NULL to count); returns the count. */
 int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);

@@ -1,0 +1,69 @@
+"""Row-band sharding on the GPU: two ranks (two processes, each with its own
+decoder context on cuda:0 -- the GPU box has one card) split a stream's SB
+rows; k_recon reconstructs only the rank's band, the bands are exchanged
+(gloo, host-staged: RCCL needs one card per rank) and intra / deblock / CLPF /
+pad run on the whole frame.  Every rank's every frame must match the
+reference decoder."""
+import json
+import os
+
+import pytest
+
+from conftest import GOLD
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, name, nframes, q):
+    import hashlib
+
+    import torch.distributed as dist
+
+    from conftest import trace_path
+    from thor_amd.decoder import GpuDecoder
+    from thor_amd.shard import RowShard
+    from thor_amd.trace import load_trace
+
+    dec = None
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        meta = json.load(open(os.path.join(GOLD, "streams.json")))[name]
+        seq, frames = load_trace(trace_path(name))
+        frames = frames[:nframes]
+        dec = GpuDecoder(seq)
+        sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=False)
+        bad = []
+        for fr in frames:
+            sh.decode(dec.upload(fr), fr.frame_num)
+            got = hashlib.md5(dec.read_i420(fr.frame_num)).hexdigest()
+            if got != meta["stage_md5"][fr.decode_order]["final"]:
+                bad.append(fr.decode_order)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, bad))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        if dec is not None:
+            dec.close()
+
+
+@pytest.mark.parametrize("name,nframes,world", [("cif_high", 10, 2), ("hd_low", 6, 2), ("cif_med", 10, 3)])
+def test_row_sharded_decode_matches_reference(name, nframes, world):
+    import random
+    import sys
+
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, nframes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=110) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    assert res == [(r, []) for r in range(world)], res

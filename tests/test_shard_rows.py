@@ -1,0 +1,124 @@
+"""Row-band sharding of one stream (thor_amd/shard.py):
+the band partition and the all-gather exchange protocol, on CPU with the
+gloo backend at world size 2 and 3.  A numpy stand-in for the decoder context
+(same begin / get_rows / put_rows / end surface as GpuDecoder) reconstructs
+only its band; after the exchange every rank must hold the whole frame.  The
+same RowShard drives the GPU contexts in tests/test_gpu_shard.py."""
+import os
+
+import numpy as np
+import pytest
+
+
+def test_band_partition():
+    from thor_amd.shard import band_of, band_rows
+
+    for H in (64, 288, 1080, 2160):
+        nsb = (H + 63) // 64
+        for world in (1, 2, 3, 4, 8):
+            rows = band_rows(H, world)
+            assert rows % 64 == 0 and rows * world >= nsb * 64
+            covered = []
+            for r in range(world):
+                b0, b1 = band_of(H, world, r)
+                covered += list(range(b0, b1))
+            assert covered == list(range(nsb)), (H, world)
+
+
+class NumpyContext:
+    """Decoder-context stand-in: frames are dicts of numpy planes."""
+
+    def __init__(self, W, H, truth):
+        self.W, self.H, self.truth = W, H, truth
+        self.band = None
+        self.cur = None
+        self.bufs = {}
+
+    def set_band(self, b0, b1):
+        self.band = (b0, b1)
+
+    def begin(self, fnum):  # the "device frame" is the frame number here
+        y, u, v = (np.zeros_like(p) for p in self.truth[fnum])
+        r0, r1 = 64 * self.band[0], min(64 * self.band[1], self.H)
+        y[r0:r1] = self.truth[fnum][0][r0:r1]
+        u[r0 // 2:r1 // 2] = self.truth[fnum][1][r0 // 2:r1 // 2]
+        v[r0 // 2:r1 // 2] = self.truth[fnum][2][r0 // 2:r1 // 2]
+        self.cur = (fnum, [y, u, v])
+
+    def scratch(self, nbytes):
+        k = len(self.bufs) + 1
+        self.bufs[k] = np.zeros(nbytes, np.uint8)
+        return k
+
+    def get_rows(self, fnum, y0, n, key):
+        assert fnum == self.cur[0]
+        buf, (y, u, v) = self.bufs[key], self.cur[1]
+        m = max(0, min(n, self.H - y0))
+        W = self.W
+        buf[:m * W] = y[y0:y0 + m].reshape(-1)
+        o = n * W
+        for p in (u, v):
+            buf[o:o + (m // 2) * (W // 2)] = p[y0 // 2:y0 // 2 + m // 2].reshape(-1)
+            o += (n // 2) * (W // 2)
+
+    def put_rows(self, fnum, y0, n, key):
+        assert fnum == self.cur[0] and y0 % 64 == 0
+        buf, (y, u, v) = self.bufs[key], self.cur[1]
+        m = max(0, min(n, self.H - y0))
+        W = self.W
+        y[y0:y0 + m] = buf[:m * W].reshape(m, W)
+        o = n * W
+        for p in (u, v):
+            p[y0 // 2:y0 // 2 + m // 2] = buf[o:o + (m // 2) * (W // 2)].reshape(m // 2, W // 2)
+            o += (n // 2) * (W // 2)
+
+    def d2h(self, out, key):
+        out[:] = self.bufs[key]
+
+    def h2d(self, key, arr):
+        self.bufs[key][:] = arr
+
+    def end(self):
+        fnum, planes = self.cur
+        for got, want in zip(planes, self.truth[fnum]):
+            assert np.array_equal(got, want), fnum
+
+
+def _worker(rank, world, port, W, H, q):
+    import torch.distributed as dist
+
+    from thor_amd.shard import RowShard
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(7)  # same frames on every rank
+        truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
+                     rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(3)}
+        ctx = NumpyContext(W, H, truth)
+        sh = RowShard(ctx, dist, W, H, device_exchange=False)
+        for f in range(3):
+            sh.decode(f, f)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 352, 288), (3, 256, 200), (2, 128, 64)])
+def test_row_shard_exchange_gloo(world, W, H):
+    import random
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(r, "ok") for r in range(world)], res

@@ -62,6 +62,8 @@ struct thor_dec {
   int dbg_flags;
   int stop_stage;
   hipEvent_t xev[2];  // cross-stream ordering when a batch mixes contexts on different streams
+  int band0, band1;    // SB rows k_recon reconstructs (row sharding); band1 0 = all
+  void *pending;       // Batch of a thor_dec_frame_begin awaiting its _end
   // optional per-stage timing (hipEvents on the decode stream)
   int timing;
   std::vector<hipEvent_t> ev_pool;
@@ -159,6 +161,8 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->dbg_flags = 0;
   d->timing = 0;
   d->xev[0] = d->xev[1] = nullptr;
+  d->band0 = d->band1 = 0;
+  d->pending = nullptr;
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
   d->stream = d->own_stream;
@@ -310,7 +314,15 @@ int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, 
   return THOR_OK;
 }
 
-static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins) {
+// A prepared batch: FrameCtx per frame + launch geometry.
+struct Batch {
+  FrameBatch fb;
+  int n, cur[THOR_MAX_BATCH], frame_num[THOR_MAX_BATCH];
+  int max_prep, any_intra, any_clpf, any_deblock;
+};
+
+static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins,
+                         Batch &b) {
   thor_dec *lead = ds[0];
   if (!lead) return THOR_ERR_ARG;
   const int W = lead->seq.width, H = lead->seq.height;
@@ -318,24 +330,22 @@ static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t
     const thor_dec *d = ds[i];
     const thor_frame_in_t &in = ins[i];
     if (!d || d->device != lead->device || d->seq.width != W || d->seq.height != H) return THOR_ERR_ARG;
+    if (d->pending) return THOR_ERR_ARG;  // a thor_dec_frame_begin without its _end
     if (in.nblocks < 0 || (in.nblocks > 0 && !in.blocks)) return THOR_ERR_ARG;
     if (in.n_intra < 0 || (in.n_intra > 0 && !in.intra_list)) return THOR_ERR_ARG;
     if (in.n_tu < 0 || (in.n_tu > 0 && (!in.tu_list || !in.coeffs))) return THOR_ERR_ARG;
   }
-  HIPCHK(hipSetDevice(lead->device));
-  hipStream_t st = lead->stream;
-  // FrameCtx of every frame, passed by value (kernel argument segment)
-  FrameBatch fb;
-  memset(&fb, 0, sizeof(fb));
-  FrameCtx *hp = fb.f;
-  int cur[THOR_MAX_BATCH];
-  int max_prep = 1, any_intra = 0, any_clpf = 0, any_deblock = 0;
+  memset(&b.fb, 0, sizeof(b.fb));
+  b.n = n;
+  b.max_prep = 1;
+  b.any_intra = b.any_clpf = b.any_deblock = 0;
   for (int i = 0; i < n; i++) {
     thor_dec *d = ds[i];
     const thor_frame_in_t &in = ins[i];
-    cur[i] = pick_slot(d, hdrs[i].frame_num);
-    FrameCtx &f = hp[i];
-    if (!make_ctx(d, cur[i], hdrs[i].frame_num, f)) return THOR_ERR_REF;
+    b.cur[i] = pick_slot(d, hdrs[i].frame_num);
+    b.frame_num[i] = hdrs[i].frame_num;
+    FrameCtx &f = b.fb.f[i];
+    if (!make_ctx(d, b.cur[i], hdrs[i].frame_num, f)) return THOR_ERR_REF;
     f.blk = in.blocks;
     f.coeffs = in.coeffs;
     f.tus = in.tu_list;
@@ -351,57 +361,93 @@ static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t
     f.qpc = chroma_qp_host(hdrs[i].qp);
     f.deblock = d->stop_stage >= 1 && d->seq.deblocking;
     f.clpf_on = d->stop_stage >= 2 && d->seq.clpf && hdrs[i].clpf_on && in.clpf_flags;
-    max_prep = max_prep > f.nprep + f.nres + 1 ? max_prep : f.nprep + f.nres + 1;
-    any_intra |= in.n_intra > 0;
-    any_clpf |= f.clpf_on;
-    any_deblock |= f.deblock;
+    f.band0 = d->band0;
+    f.band1 = d->band1 > 0 ? d->band1 : f.nsbrows;
+    b.max_prep = b.max_prep > f.nprep + f.nres + 1 ? b.max_prep : f.nprep + f.nres + 1;
+    b.any_intra |= in.n_intra > 0;
+    b.any_clpf |= f.clpf_on;
+    b.any_deblock |= f.deblock;
   }
+  return THOR_OK;
+}
+
+// Phase A: side info, residuals, intra setup, inter reconstruction (the SB
+// rows of each context's band).
+static int batch_phase_a(thor_dec *lead, const Batch &b) {
+  const int W = lead->seq.width, H = lead->seq.height, n = b.n;
+  hipStream_t st = lead->stream;
+  const int nsb = ((W + 63) / 64) * ((H + 63) / 64);
+  {
+    // side info + residuals of every coded transform block + intra chain setup
+    StageMark m(lead, ST_PREP);
+    k_frame_prep<<<dim3(b.max_prep, n), 256, 0, st>>>(b.fb);
+    HIPCHK(hipGetLastError());
+  }
+  {
+    StageMark m(lead, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
+    k_recon<<<dim3(8 * ((2 * nsb + 7) / 8), n), 64, 0, st>>>(b.fb, lead->dbg_recon);
+    HIPCHK(hipGetLastError());
+  }
+  return THOR_OK;
+}
+
+// Phase B: intra, deblock, CLPF, reference padding.
+static int batch_phase_b(thor_dec *lead, const Batch &b) {
+  const int W = lead->seq.width, H = lead->seq.height, n = b.n;
+  hipStream_t st = lead->stream;
+  const int nrows = (H + 63) / 64;
+  if (b.any_intra) {
+    StageMark m(lead, ST_INTRA);
+    // one single-wave chain per (SB row, component); LDS holds the row's CU words
+    size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
+    k_intra<<<dim3(3 * nrows, n), 64, lds, st>>>(b.fb, lead->dbg, lead->dbg_flags);
+    HIPCHK(hipGetLastError());
+  }
+  if (b.any_deblock) {
+    StageMark m(lead, ST_DEBLOCK);
+    int nv = ((W >> 3) - 1) * (H >> 3);
+    int nh = (W >> 3) * ((H >> 3) - 1);
+    // luma and both chroma planes of one edge direction per launch
+    const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
+    k_deblock_v<<<dim3(3 * bv, n), 256, 0, st>>>(b.fb, bv);
+    k_deblock_h<<<dim3(3 * bh, n), 256, 0, st>>>(b.fb, bh);
+    HIPCHK(hipGetLastError());
+  }
+  if (b.any_clpf && (W / 64) * (H / 64) > 0) {
+    StageMark m(lead, ST_CLPF);
+    k_clpf<<<dim3(((W / 64) * (H / 64) + CLPF_SBS - 1) / CLPF_SBS, n), 256, 0, st>>>(b.fb);
+    HIPCHK(hipGetLastError());
+  }
+  {
+    StageMark m(lead, ST_PAD);
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(b.fb);
+    HIPCHK(hipGetLastError());
+  }
+  return THOR_OK;
+}
+
+static void batch_commit(thor_dec_t *const *ds, const Batch &b) {
+  for (int i = 0; i < b.n; i++) {
+    ds[i]->slot_fnum[b.cur[i]] = b.frame_num[i];
+    ds[i]->slot_age[b.cur[i]] = ds[i]->decode_count++;
+  }
+}
+
+static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins) {
+  thor_dec *lead = ds[0];
+  Batch b;
+  int rc = batch_prepare(ds, n, hdrs, ins, b);
+  if (rc != THOR_OK) return rc;
+  HIPCHK(hipSetDevice(lead->device));
+  hipStream_t st = lead->stream;
   // order the batch after each member context's earlier work on other streams
   for (int i = 1; i < n; i++)
     if (ds[i]->stream != st) {
       HIPCHK(hipEventRecord(lead->xev[0], ds[i]->stream));
       HIPCHK(hipStreamWaitEvent(st, lead->xev[0], 0));
     }
-  const int nsb = ((W + 63) / 64) * ((H + 63) / 64);
-  const int nrows = (H + 63) / 64;
-  {
-    // side info + residuals of every coded transform block + intra chain setup
-    StageMark m(lead, ST_PREP);
-    k_frame_prep<<<dim3(max_prep, n), 256, 0, st>>>(fb);
-    HIPCHK(hipGetLastError());
-  }
-  {
-    StageMark m(lead, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
-    k_recon<<<dim3(8 * ((2 * nsb + 7) / 8), n), 64, 0, st>>>(fb, lead->dbg_recon);
-    HIPCHK(hipGetLastError());
-  }
-  if (any_intra) {
-    StageMark m(lead, ST_INTRA);
-    // one single-wave chain per (SB row, component); LDS holds the row's CU words
-    size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
-    k_intra<<<dim3(3 * nrows, n), 64, lds, st>>>(fb, lead->dbg, lead->dbg_flags);
-    HIPCHK(hipGetLastError());
-  }
-  if (any_deblock) {
-    StageMark m(lead, ST_DEBLOCK);
-    int nv = ((W >> 3) - 1) * (H >> 3);
-    int nh = (W >> 3) * ((H >> 3) - 1);
-    // luma and both chroma planes of one edge direction per launch
-    const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
-    k_deblock_v<<<dim3(3 * bv, n), 256, 0, st>>>(fb, bv);
-    k_deblock_h<<<dim3(3 * bh, n), 256, 0, st>>>(fb, bh);
-    HIPCHK(hipGetLastError());
-  }
-  if (any_clpf && (W / 64) * (H / 64) > 0) {
-    StageMark m(lead, ST_CLPF);
-    k_clpf<<<dim3(((W / 64) * (H / 64) + CLPF_SBS - 1) / CLPF_SBS, n), 256, 0, st>>>(fb);
-    HIPCHK(hipGetLastError());
-  }
-  {
-    StageMark m(lead, ST_PAD);
-    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(fb);
-    HIPCHK(hipGetLastError());
-  }
+  if ((rc = batch_phase_a(lead, b)) != THOR_OK) return rc;
+  if ((rc = batch_phase_b(lead, b)) != THOR_OK) return rc;
   // later work a member context enqueues on its own stream follows this batch
   bool rec = false;
   for (int i = 1; i < n; i++)
@@ -410,11 +456,110 @@ static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t
       rec = true;
       HIPCHK(hipStreamWaitEvent(ds[i]->stream, lead->xev[1], 0));
     }
-  for (int i = 0; i < n; i++) {
-    ds[i]->slot_fnum[cur[i]] = hdrs[i].frame_num;
-    ds[i]->slot_age[cur[i]] = ds[i]->decode_count++;
+  batch_commit(ds, b);
+  return THOR_OK;
+}
+
+// ---- row-band sharding ------------------------------
+int thor_dec_set_band(thor_dec_t *d, int sb_row0, int sb_row1) {
+  if (!d) return THOR_ERR_ARG;
+  const int nrows = (d->seq.height + 63) / 64;
+  if (sb_row0 < 0 || sb_row1 < sb_row0 || sb_row1 > nrows) return THOR_ERR_ARG;
+  d->band0 = sb_row0;
+  d->band1 = sb_row1 == 0 && sb_row0 == 0 ? 0 : sb_row1;
+  return THOR_OK;
+}
+
+int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_frame_in_t *in) {
+  if (!d || !hdr || !in) return THOR_ERR_ARG;
+  Batch *b = new Batch();
+  thor_dec_t *ds[1] = {d};
+  int rc = batch_prepare(ds, 1, hdr, in, *b);
+  if (rc == THOR_OK) {
+    if (hipSetDevice(d->device) != hipSuccess) rc = THOR_ERR_HIP;
+    else rc = batch_phase_a(d, *b);
   }
-  (void)nsb;
+  if (rc != THOR_OK) {
+    delete b;
+    return rc;
+  }
+  d->pending = b;
+  return THOR_OK;
+}
+
+int thor_dec_frame_end(thor_dec_t *d) {
+  if (!d || !d->pending) return THOR_ERR_ARG;
+  Batch *b = (Batch *)d->pending;
+  HIPCHK(hipSetDevice(d->device));
+  int rc = batch_phase_b(d, *b);
+  thor_dec_t *ds[1] = {d};
+  if (rc == THOR_OK) batch_commit(ds, *b);
+  d->pending = nullptr;
+  delete b;
+  return rc;
+}
+
+// Rows [y0, y0 + nrows) of luma (and the matching chroma rows) of the frame in
+// `frame_num`'s slot, or of the frame begun and not yet ended, packed as
+// Y (nrows x W) | U (nrows/2 x W/2) | V; rows past the frame are skipped.
+static int band_slot(thor_dec *d, int frame_num) {
+  if (d->pending) {
+    Batch *b = (Batch *)d->pending;
+    if (b->frame_num[0] == frame_num) return b->cur[0];
+  }
+  return find_slot_host(d, frame_num);
+}
+
+int thor_dec_get_rows(thor_dec_t *d, int frame_num, int y0, int nrows, void *dst) {
+  if (!d || !dst || y0 < 0 || nrows <= 0 || (y0 & 1) || (nrows & 1)) return THOR_ERR_ARG;
+  const int s = band_slot(d, frame_num);
+  if (s < 0) return THOR_ERR_REF;
+  const int W = d->seq.width, H = d->seq.height;
+  const int n = y0 + nrows > H ? H - y0 : nrows;
+  if (n <= 0) return THOR_OK;
+  const uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  uint8_t *o = (uint8_t *)dst;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipMemcpy2DAsync(o, W, base + d->offy + (long long)y0 * d->sy, d->sy, W, n, hipMemcpyDeviceToDevice, d->stream));
+  o += (long long)nrows * W;
+  for (int c = 0; c < 2; c++) {
+    const long long off = (c ? d->offv : d->offu) + (long long)(y0 / 2) * d->sc;
+    HIPCHK(hipMemcpy2DAsync(o, W / 2, base + off, d->sc, W / 2, n / 2, hipMemcpyDeviceToDevice, d->stream));
+    o += (long long)(nrows / 2) * (W / 2);
+  }
+  return THOR_OK;
+}
+
+int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const void *src) {
+  if (!d || !src || y0 < 0 || nrows <= 0 || (y0 & 63) || (nrows & 1)) return THOR_ERR_ARG;
+  const int s = band_slot(d, frame_num);
+  if (s < 0) return THOR_ERR_REF;
+  const int W = d->seq.width, H = d->seq.height;
+  const int n = y0 + nrows > H ? H - y0 : nrows;
+  if (n <= 0) return THOR_OK;
+  uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  const uint8_t *i = (const uint8_t *)src;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipMemcpy2DAsync(base + d->offy + (long long)y0 * d->sy, d->sy, i, W, W, n, hipMemcpyDeviceToDevice, d->stream));
+  // the intra chains read SB-row bottom rows from the edge buffer (k_recon
+  // writes the inter pixels there for its own band): refresh every SB row
+  // whose bottom row this band carries
+  const int sb0 = y0 / 64, sb1 = (y0 + n) / 64;  // SB rows whose row 63 lies inside [y0, y0 + n)
+  if (sb1 > sb0)
+    HIPCHK(hipMemcpy2DAsync(d->edge + (long long)sb0 * d->ewy + EDGE_MARGIN, d->ewy, i + (long long)(63) * W, 64LL * W,
+                            W, sb1 - sb0, hipMemcpyDeviceToDevice, d->stream));
+  i += (long long)nrows * W;
+  const int nsbrows = (H + 63) / 64;
+  for (int c = 0; c < 2; c++) {
+    const long long off = (c ? d->offv : d->offu) + (long long)(y0 / 2) * d->sc;
+    HIPCHK(hipMemcpy2DAsync(base + off, d->sc, i, W / 2, W / 2, n / 2, hipMemcpyDeviceToDevice, d->stream));
+    if (sb1 > sb0)
+      HIPCHK(hipMemcpy2DAsync(d->edge + (long long)nsbrows * d->ewy + (long long)c * nsbrows * d->ewc +
+                                  (long long)sb0 * d->ewc + EDGE_MARGIN,
+                              d->ewc, i + 31LL * (W / 2), 32LL * (W / 2), W / 2, sb1 - sb0, hipMemcpyDeviceToDevice,
+                              d->stream));
+    i += (long long)(nrows / 2) * (W / 2);
+  }
   return THOR_OK;
 }
 

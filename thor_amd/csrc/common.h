@@ -46,6 +46,7 @@ struct FrameCtx {
   int *rowstart;
   int nblocks, ntus, nintra, nprep, nres, full_sb;
   int qp, qpc, deblock, clpf_on;
+  int band0, band1;  // SB rows k_recon reconstructs (row-band sharding); all by default
 };
 // A batch of frames travels in the kernel argument segment (8 x 384 B, under
 // the 4 KB kernarg limit): the host fills it per call, no upload copy.  Every

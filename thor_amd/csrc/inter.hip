@@ -528,6 +528,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   if (hsb >= nh) return;
   const int sb = hsb >> 1, h = hsb & 1;
   const int sby = sb / sbw, sbx = sb - sby * sbw;
+  if (sby < f.band0 || sby >= f.band1) return;  // another shard's rows (row-band sharding)
   const int cs = f.W >> 2;
 
   // reference lookup table (packed by the host)

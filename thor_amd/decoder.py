@@ -111,6 +111,34 @@ class GpuDecoder:
     def frame_in(self, d: DeviceFrame) -> L.ThorFrameIn:
         return L.ThorFrameIn(d.blocks, d.nblocks, d.coeffs, d.clpf or None, d.intra, d.n_intra, d.tus, d.n_tu)
 
+    # ---- row-band sharding (thor_amd/shard.py) ----
+    def set_band(self, sb_row0: int, sb_row1: int):
+        L.check(self.lib.thor_dec_set_band(self.h, sb_row0, sb_row1), "thor_dec_set_band")
+
+    def begin(self, d: DeviceFrame):
+        fi = self.frame_in(d)
+        L.check(self.lib.thor_dec_frame_begin(self.h, C.byref(d.hdr), C.byref(fi)), "thor_dec_frame_begin")
+
+    def end(self):
+        L.check(self.lib.thor_dec_frame_end(self.h), "thor_dec_frame_end")
+
+    def get_rows(self, frame_num: int, y0: int, nrows: int, dst_ptr):
+        L.check(self.lib.thor_dec_get_rows(self.h, frame_num, y0, nrows, dst_ptr), "thor_dec_get_rows")
+
+    def put_rows(self, frame_num: int, y0: int, nrows: int, src_ptr):
+        L.check(self.lib.thor_dec_put_rows(self.h, frame_num, y0, nrows, src_ptr), "thor_dec_put_rows")
+
+    def scratch(self, nbytes: int) -> int:
+        return self._buf(np.zeros(max(nbytes, 16), np.uint8)).ptr
+
+    def d2h(self, out: np.ndarray, ptr: int):
+        self.sync()
+        L.check(self.lib.thor_d2h(out.ctypes.data, ptr, out.nbytes), "thor_d2h")
+
+    def h2d(self, ptr: int, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        L.check(self.lib.thor_h2d(ptr, a.ctypes.data, a.nbytes), "thor_h2d")
+
     def set_stop_stage(self, stage: int):
         L.check(self.lib.thor_dec_set_stop_stage(self.h, stage), "thor_dec_set_stop_stage")
 

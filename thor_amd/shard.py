@@ -1,0 +1,85 @@
+"""Row-band sharding of ONE stream across ranks.
+
+Every rank holds a full decoder context for the stream.  Per frame:
+
+  1. thor_dec_frame_begin: side info, residuals, intra setup for the whole
+     frame, inter reconstruction (k_recon) of the rank's band of SB rows only;
+  2. all-gather of the bands' pre-deblock rows (thor_dec_get_rows /
+     thor_dec_put_rows; put_rows also refreshes the SB-row edge rows the intra
+     chains read) -- RCCL over xGMI with the nccl backend, host-staged with gloo;
+  3. thor_dec_frame_end: intra (it reads neighbours across bands), deblock,
+     CLPF and padding of the whole frame, replicated on every rank, so every
+     rank ends the frame with the identical full reference.
+
+Band b covers SB rows [b*R, (b+1)*R), R = ceil(SB rows / world); the last band
+may run past the frame (those rows are not copied).
+"""
+from __future__ import annotations
+
+
+
+def band_rows(height: int, world: int) -> int:
+    """Luma rows per band: whole SB rows, equal for every rank (all-gather)."""
+    nsb = (height + 63) // 64
+    return ((nsb + world - 1) // world) * 64
+
+
+def band_of(height: int, world: int, rank: int):
+    """(first SB row, end SB row) of `rank`'s band (end clamped to the frame)."""
+    nsb = (height + 63) // 64
+    r = band_rows(height, world) // 64
+    return min(rank * r, nsb), min((rank + 1) * r, nsb)
+
+
+def band_bytes(width: int, height: int, world: int) -> int:
+    rows = band_rows(height, world)
+    return rows * width + 2 * (rows // 2) * (width // 2)
+
+
+class RowShard:
+    """Drives one rank's decoder context through band-sharded frames.
+
+    `dec` is a thor_amd.decoder.GpuDecoder (or any object with the same
+    begin/get_rows/put_rows/end methods, as the CPU tests use); `dist` is
+    torch.distributed, initialised; `device_exchange` selects device buffers
+    (nccl/RCCL) or host staging (gloo)."""
+
+    def __init__(self, dec, dist, width: int, height: int, device_exchange: bool):
+        self.dec, self.dist = dec, dist
+        self.W, self.H = width, height
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.rows = band_rows(height, self.world)
+        self.nbytes = band_bytes(width, height, self.world)
+        self.device_exchange = device_exchange
+        b0, b1 = band_of(height, self.world, self.rank)
+        dec.set_band(b0, b1)
+        import torch
+
+        if device_exchange:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            self.send = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
+            self.recv = torch.empty(self.world * self.nbytes, dtype=torch.uint8, device=dev)
+        else:
+            self.send = torch.empty(self.nbytes, dtype=torch.uint8)
+            self.recv = [torch.empty(self.nbytes, dtype=torch.uint8) for _ in range(self.world)]
+            self.scratch = [dec.scratch(self.nbytes) for _ in range(self.world)]
+
+    def decode(self, devframe, frame_num: int):
+        d = self.dec
+        d.begin(devframe)
+        y0 = self.rank * self.rows
+        if self.device_exchange:
+            d.get_rows(frame_num, y0, self.rows, self.send.data_ptr())
+            self.dist.all_gather_into_tensor(self.recv, self.send)
+            for r in range(self.world):
+                if r != self.rank:
+                    d.put_rows(frame_num, r * self.rows, self.rows, self.recv.data_ptr() + r * self.nbytes)
+        else:
+            d.get_rows(frame_num, y0, self.rows, self.scratch[self.rank])
+            d.d2h(self.send.numpy(), self.scratch[self.rank])  # waits for the decoder's stream
+            self.dist.all_gather(self.recv, self.send)
+            for r in range(self.world):
+                if r != self.rank:
+                    d.h2d(self.scratch[r], self.recv[r].numpy())
+                    d.put_rows(frame_num, r * self.rows, self.rows, self.scratch[r])
+        d.end()
