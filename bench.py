@@ -72,6 +72,88 @@ def recon_alg_bytes(fr, width: int, height: int) -> float:
     return total
 
 
+TU_DTYPE = np.dtype([("orig_off", "<i4"), ("pred_off", "<i4"), ("rec_off", "<i4"), ("coeff_off", "<i4"),
+                     ("orig_stride", "<i4"), ("pred_stride", "<i4"), ("rec_stride", "<i4"), ("size", "u1"),
+                     ("qp", "u1"), ("type", "u1"), ("fast", "u1")])
+
+
+def encoder_leg(torch, lib, reps: int = 10):
+    """Encoder-side transform-block chain (SURVEY.md sec. 8(a) a4-a6, a8-a12;
+    BASELINE config 3: 1080p, config_LDB_high_efficiency => encoder_speed 0,
+    fast transforms off, qp 32): the RD evaluation of one inter candidate per
+    CU at every quadtree level (64, 32, 16, 8) over a whole 1080p frame --
+    orig = synthetic frame 1, pred = frame 0 co-located -- residual -> forward
+    T -> quantize -> dequant -> inverse T -> recon -> SSD per TU
+    (thor_enc_tu_batch), then cost_calc per CU (thor_enc_cost_batch).  The
+    serial RD search that would issue these batches is not on the GPU
+    (SURVEY.md sec. 8(f) #4)."""
+    from thor_amd import synth
+
+    W, H, qp = 1920, 1080, 32
+    chroma_qp = [min(q, 29) if q < 30 else [29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42,
+                                            43, 44, 45][q - 30] for q in range(52)]
+    org = synth.synth_frame(W, H, 1, 3)
+    prd = synth.synth_frame(W, H, 0, 3)
+    planes = [np.concatenate([p.reshape(-1) for p in fr]) for fr in (org, prd)]
+    offs = [0, W * H, W * H + (W // 2) * (H // 2)]
+    tus, cu_first, cu_count = [], [], []
+    coff = 0
+    for S in (64, 32, 16, 8):
+        for y in range(0, H - S + 1, S):
+            for x in range(0, W - S + 1, S):
+                cu_first.append(len(tus))
+                for c in range(3):
+                    n = S if c == 0 else S // 2
+                    st = W if c == 0 else W // 2
+                    yy, xx = (y, x) if c == 0 else (y // 2, x // 2)
+                    o = offs[c] + yy * st + xx
+                    q = min(n, 16)
+                    tus.append((o, o, o, coff, st, st, st, n, qp if c == 0 else chroma_qp[qp], c != 0, 0))
+                    coff += q * q
+                cu_count.append(3)
+    tus = np.array(tus, TU_DTYPE)
+    ncu, ntu = len(cu_first), len(tus)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t_org = torch.from_numpy(planes[0]).to(dev)
+    t_prd = torch.from_numpy(planes[1]).to(dev)
+    t_rec = torch.empty_like(t_org)
+    t_tus = torch.from_numpy(tus.view(np.uint8)).to(dev)
+    t_cq = torch.empty(coff, dtype=torch.int16, device=dev)
+    t_cbp = torch.empty(ntu, dtype=torch.uint8, device=dev)
+    t_ssd = torch.empty(ntu, dtype=torch.int32, device=dev)
+    t_first = torch.tensor(cu_first, dtype=torch.int32, device=dev)
+    t_count = torch.tensor(cu_count, dtype=torch.int32, device=dev)
+    t_bits = torch.full((ncu,), 100, dtype=torch.int32, device=dev)
+    t_cost = torch.empty(ncu, dtype=torch.int32, device=dev)
+    lam = 0.57 * 2 ** ((qp - 12) / 3.0)
+
+    def run():
+        rc = lib.thor_enc_tu_batch(t_tus.data_ptr(), ntu, t_org.data_ptr(), t_prd.data_ptr(), t_rec.data_ptr(),
+                                   t_cq.data_ptr(), t_cbp.data_ptr(), t_ssd.data_ptr(), None)
+        rc |= lib.thor_enc_cost_batch(t_ssd.data_ptr(), t_first.data_ptr(), t_count.data_ptr(), t_bits.data_ptr(),
+                                      lam, t_cost.data_ptr(), ncu, None)
+        assert rc == 0
+
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    px = 4 * W * H  # luma px evaluated (one candidate per CU at 4 levels)
+    q2 = sum(min(int(t), 16) ** 2 for t in tus["size"])
+    alg = 4 * 3 * W * H * 1.5 + 2.0 * q2  # orig + pred + rec bytes (4:2:0) + levels
+    return {"workload": "1080p, one inter candidate per CU at 64/32/16/8 over the whole frame, qp 32, "
+                        "LDB_high_efficiency transform flags; %d TUs, %d CUs per pass" % (ntu, ncu),
+            "ms_per_pass": round(ms, 4), "mpx_evaluated_s": round(px / ms / 1e3, 1),
+            "cbp_fraction": round(float(t_cbp.float().mean().item()), 3),
+            "alg_bytes": int(alg), "achieved_gb_s": round(alg / ms / 1e6, 1),
+            "note": "RD candidate evaluation throughput of the encoder TU chain; not part of `value`"}
+
+
 def cpu_baseline(meta, gold, budget_s: float = 20.0):
     """Reference decoder (oracle/_ref/Thordec, SIMD build, 1 thread) on the
     same .bit, repeated up to ~budget_s; falls back to the oracle port."""
@@ -317,6 +399,8 @@ def main():
                 "launches": "batched P-frame launches of group 0 alone; hipEvents on its stream",
             },
         }
+        if world == 1:
+            out["encoder_tu_chain"] = encoder_leg(torch, lib)
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(meta, gold)
         print(json.dumps(out), flush=True)
