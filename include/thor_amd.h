@@ -111,6 +111,8 @@ typedef struct thor_frame_in {
   int32_t n_intra;
   const uint32_t *tu_list;
   int32_t n_tu;
+  const uint32_t *clpf_list; /* indices of the SBs whose CLPF flag is set (thor_build_clpf_list) */
+  int32_t n_clpf;            /* -1: no list, scan every SB's flag */
 } thor_frame_in_t;
 
 /* Decode one frame in each of `n` DIFFERENT contexts with one launch per stage
@@ -140,6 +142,9 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
 /* Host helper: write the decode-order indices of the intra CUs of a frame
  * (host descriptors) to `out` (may be NULL to count); returns the count. */
 int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);
+/* Host helper: indices of the SBs whose CLPF decision flag is set (the CLPF
+ * launch is as wide as this list; `out` may be NULL to count). */
+int thor_build_clpf_list(const uint8_t *host_flags, int nsb, uint32_t *out);
 /* Host helper: the frame's coded transform blocks (the residual work list the
  * parser knows from the cbp flags, dec/decode_block.c:90-120): one entry
  * block << 4 | component << 2 | tb-split quarter per coded TU, in any order.

@@ -111,3 +111,25 @@ def test_batched_contexts_match_reference(streams):
     finally:
         for d in decs:
             d.close()
+
+
+def test_single_frame_api_without_lists(streams):
+    """thor_dec_frame (the one-frame C entry, no CLPF work list: every SB's
+    flag is scanned) reproduces the reference too."""
+    import ctypes as C
+    import hashlib
+
+    from thor_amd.decoder import GpuDecoder
+
+    seq, frames = load_trace(trace_path("cif_high"))
+    d = GpuDecoder(seq)
+    try:
+        for fr in frames:
+            x = d.upload(fr)
+            rc = d.lib.thor_dec_frame(d.h, C.byref(x.hdr), x.blocks, x.nblocks, x.coeffs, x.clpf or None, x.intra,
+                                      x.n_intra, x.tus, x.n_tu)
+            assert rc == 0
+            got = hashlib.md5(d.read_i420(fr.frame_num)).hexdigest()
+            assert got == streams["cif_high"]["stage_md5"][fr.decode_order]["final"], fr.decode_order
+    finally:
+        d.close()

@@ -318,7 +318,7 @@ int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, 
 struct Batch {
   FrameBatch fb;
   int n, cur[THOR_MAX_BATCH], frame_num[THOR_MAX_BATCH];
-  int max_prep, any_intra, any_clpf, any_deblock;
+  int max_prep, any_intra, any_clpf, any_deblock, clpf_grid;
 };
 
 static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins,
@@ -339,6 +339,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
   b.n = n;
   b.max_prep = 1;
   b.any_intra = b.any_clpf = b.any_deblock = 0;
+  b.clpf_grid = 0;
   for (int i = 0; i < n; i++) {
     thor_dec *d = ds[i];
     const thor_frame_in_t &in = ins[i];
@@ -351,6 +352,8 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.tus = in.tu_list;
     f.ilist = in.intra_list;
     f.clpf_flags = in.clpf_flags;
+    f.clpf_list = in.clpf_list;
+    f.n_clpf = in.clpf_list ? in.n_clpf : -1;
     f.nblocks = in.nblocks;
     f.ntus = in.n_tu;
     f.nintra = in.n_intra;
@@ -365,6 +368,10 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.band1 = d->band1 > 0 ? d->band1 : f.nsbrows;
     b.max_prep = b.max_prep > f.nprep + f.nres + 1 ? b.max_prep : f.nprep + f.nres + 1;
     b.any_intra |= in.n_intra > 0;
+    if (f.clpf_on) {
+      const int w = f.n_clpf >= 0 ? f.n_clpf : (W / 64) * (H / 64);
+      b.clpf_grid = b.clpf_grid > w ? b.clpf_grid : w;
+    }
     b.any_clpf |= f.clpf_on;
     b.any_deblock |= f.deblock;
   }
@@ -413,9 +420,9 @@ static int batch_phase_b(thor_dec *lead, const Batch &b) {
     k_deblock_h<<<dim3(3 * bh, n), 256, 0, st>>>(b.fb, bh);
     HIPCHK(hipGetLastError());
   }
-  if (b.any_clpf && (W / 64) * (H / 64) > 0) {
+  if (b.any_clpf && b.clpf_grid > 0) {
     StageMark m(lead, ST_CLPF);
-    k_clpf<<<dim3(((W / 64) * (H / 64) + CLPF_SBS - 1) / CLPF_SBS, n), 256, 0, st>>>(b.fb);
+    k_clpf<<<dim3(b.clpf_grid, n), 256, 0, st>>>(b.fb);
     HIPCHK(hipGetLastError());
   }
   {
@@ -567,7 +574,7 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
                    const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
                    const uint32_t *tu_list, int n_tu) {
   if (!d || !hdr) return THOR_ERR_ARG;
-  thor_frame_in_t in = {blocks, nblocks, coeffs, clpf_flags, intra_list, n_intra, tu_list, n_tu};
+  thor_frame_in_t in = {blocks, nblocks, coeffs, clpf_flags, intra_list, n_intra, tu_list, n_tu, nullptr, -1};
   return thor_dec_frames(&d, 1, hdr, &in);
 }
 
@@ -621,6 +628,17 @@ int thor_dec_stage_marks(thor_dec_t *d, int *stage, double *ms, int cap) {
   }
   d->ev_marks.clear();
   d->ev_used = 0;
+  return n;
+}
+
+int thor_build_clpf_list(const uint8_t *host_flags, int nsb, uint32_t *out) {
+  if (nsb < 0 || (nsb > 0 && !host_flags)) return THOR_ERR_ARG;
+  int n = 0;
+  for (int i = 0; i < nsb; i++)
+    if (host_flags[i]) {
+      if (out) out[n] = (uint32_t)i;
+      n++;
+    }
   return n;
 }
 

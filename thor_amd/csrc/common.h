@@ -39,6 +39,8 @@ struct FrameCtx {
   const int16_t *coeffs;
   const uint32_t *tus, *ilist;
   const uint8_t *clpf_flags;
+  const uint32_t *clpf_list;  // flagged SBs (n_clpf >= 0) or every SB (n_clpf < 0)
+  int n_clpf;
   uint16_t *cellinfo;
   int32_t *cellmap;
   int16_t *resid;

@@ -272,20 +272,18 @@ __device__ __forceinline__ void k_clpf_body(int bx, uint8_t *Y, uint8_t *U, uint
     (pl ? v0 : u0)[(long long)r * sc + c] = (uint8_t)(X + delta);
   }
 }
-#define CLPF_SBS 1
 __global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];
   __shared__ int cand;
   const FrameCtx &f = F[blockIdx.y];
   if (!f.clpf_on) return;
-  const int nsb = (f.W >> 6) * (f.H >> 6);
-  for (int r = 0; r < CLPF_SBS; r++) {  // CLPF_SBS SBs per workgroup (most are not flagged)
-    const int sb = blockIdx.x * CLPF_SBS + r;
-    if (sb >= nsb) break;
-    k_clpf_body(sb, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, cand);
-    __syncthreads();  // the next SB reuses the LDS copies
-  }
+  // one workgroup per flagged SB (the host's list), or per SB without a list
+  const int nwork = f.n_clpf >= 0 ? f.n_clpf : (f.W >> 6) * (f.H >> 6);
+  if ((int)blockIdx.x >= nwork) return;
+  const int sb = f.n_clpf >= 0 ? (int)f.clpf_list[blockIdx.x] : (int)blockIdx.x;
+  if (sb >= (f.W >> 6) * (f.H >> 6)) return;
+  k_clpf_body(sb, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, cand);
 }
 
 

@@ -32,6 +32,8 @@ class DeviceFrame:
     n_intra: int
     tus: int
     n_tu: int
+    clpfl: int
+    n_clpf: int
     nbytes: int  # bytes uploaded (descriptors + coefficients + flags + list)
 
 
@@ -96,20 +98,25 @@ class GpuDecoder:
         n_tu = self.lib.thor_build_tu_list(blocks.ctypes.data, len(blocks), None)
         tlist = np.zeros(max(n_tu, 1), np.uint32)
         self.lib.thor_build_tu_list(blocks.ctypes.data, len(blocks), tlist.ctypes.data)
+        n_clpf = self.lib.thor_build_clpf_list(flags.ctypes.data, len(flags), None) if flags.size else 0
+        clist = np.zeros(max(n_clpf, 1), np.uint32)
+        if flags.size:
+            self.lib.thor_build_clpf_list(flags.ctypes.data, len(flags), clist.ctypes.data)
         bb, cb, fb, ib = self._buf(blocks), self._buf(coeffs), self._buf(flags), self._buf(ilist)
-        tb = self._buf(tlist)
+        tb, lb = self._buf(tlist), self._buf(clist)
         hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
         nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + 4 * n_tu
         return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, tb.ptr,
-                           n_tu, nbytes)
+                           n_tu, lb.ptr, n_clpf, nbytes)
 
     def decode(self, d: DeviceFrame):
-        rc = self.lib.thor_dec_frame(self.h, C.byref(d.hdr), d.blocks, d.nblocks, d.coeffs, d.clpf or None,
-                                     d.intra, d.n_intra, d.tus, d.n_tu)
-        L.check(rc, "thor_dec_frame")
+        fi = self.frame_in(d)
+        hs = (C.c_void_p * 1)(self.h)
+        L.check(self.lib.thor_dec_frames(hs, 1, C.byref(d.hdr), C.byref(fi)), "thor_dec_frames")
 
     def frame_in(self, d: DeviceFrame) -> L.ThorFrameIn:
-        return L.ThorFrameIn(d.blocks, d.nblocks, d.coeffs, d.clpf or None, d.intra, d.n_intra, d.tus, d.n_tu)
+        return L.ThorFrameIn(d.blocks, d.nblocks, d.coeffs, d.clpf or None, d.intra, d.n_intra, d.tus, d.n_tu,
+                             d.clpfl if d.clpf else None, d.n_clpf if d.clpf else -1)
 
     # ---- row-band sharding (thor_amd/shard.py) ----
     def set_band(self, sb_row0: int, sb_row1: int):
