@@ -597,21 +597,35 @@ __device__ __forceinline__ unsigned long long intra_chain(IntraChain &L, const F
 // Per-frame setup before k_intra: each SB row's segment of the intra list
 // (decode order is raster SB order) into rowstart[0..nrows]; progress words
 // and the task head cleared.
+// Row segments of the intra list (decode order is SB-row major, so each SB
+// row's CUs are contiguous): rowstart[r] = first list index in SB row >= r.
+// With few intra CUs, element-parallel (every element's row and its
+// predecessor's: one round of independent loads); with many, a binary search
+// per row (rows in parallel).
 __device__ __forceinline__ void intra_setup_body(const thor_block_t *__restrict__ blk,
                                                  const uint32_t *__restrict__ list, int n_intra, unsigned *ctl,
                                                  unsigned *progress, int *rowstart, int nrows) {
-  if (threadIdx.x >= 64) return;
-  for (int r = threadIdx.x; r <= nrows; r += 64) {
-    int lo = 0, hi = n_intra;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if ((blk[list[mid]].ypos >> 6) < r) lo = mid + 1;
-      else hi = mid;
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (n_intra < nt) {  // few intra CUs (P frames): one round of independent loads
+    const int i = t;
+    if (i <= n_intra) {
+      const int ri = i < n_intra ? (blk[list[i]].ypos >> 6) : nrows;  // nrows: sentinel past the last element
+      const int rp = i > 0 ? (blk[list[i - 1]].ypos >> 6) : -1;
+      for (int r = rp + 1; r <= ri && r <= nrows; r++) rowstart[r] = i;
     }
-    rowstart[r] = lo;
+  } else {  // many (I frames): a binary search per row, rows in parallel
+    for (int r = t; r <= nrows; r += nt) {
+      int lo = 0, hi = n_intra;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((blk[list[mid]].ypos >> 6) < r) lo = mid + 1;
+        else hi = mid;
+      }
+      rowstart[r] = lo;
+    }
   }
-  for (int q = threadIdx.x; q < 3 * nrows; q += 64) progress[q] = 0;
-  if (threadIdx.x == 0) ctl[0] = 0;
+  for (int q = t; q < 3 * nrows; q += nt) progress[q] = 0;
+  if (t == 0) ctl[0] = 0;
 }
 
 // k_frame_prep: everything a frame needs before reconstruction, in one launch

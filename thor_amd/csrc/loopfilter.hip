@@ -214,68 +214,98 @@ __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl
   }
 }
 
+// One flagged SB per workgroup.  The SB's pixels and its 64 8x8-block side
+// info words are loaded speculatively together with the flag (one round
+// trip), then staged in LDS; each lane filters 16 consecutive pixels of a row
+// and writes them back as one 16-byte store.
+__device__ __forceinline__ int clpf_px(const uint8_t *s, int pitch, int n, int r, int c) {
+  const int X = s[r * pitch + c];
+  const int A = r == 0 ? X : s[(r - 1) * pitch + c];
+  const int Bv = c == 0 ? X : s[r * pitch + c - 1];
+  const int Cv = c == n - 1 ? X : s[r * pitch + c + 1];
+  const int D = r == n - 1 ? X : s[(r + 1) * pitch + c];
+  const int delta = ((A > X) + (Bv > X) + (Cv > X) + (D > X) > 2) - ((A < X) + (Bv < X) + (Cv < X) + (D < X) > 2);
+  return (X + delta) & 255;
+}
 __device__ __forceinline__ void k_clpf_body(int bx, uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
                                             const uint16_t *cell, const uint8_t *flags, uint8_t *sY, uint8_t *sU,
-                                            uint8_t *sV, int &cand) {
-  int nh = W >> 6;
-  int k = bx / nh, l = bx - (bx / nh) * nh;
-  if (!flags[bx]) return;
-  int tid = threadIdx.x;
-  int cs = W >> 2;
-  if (tid == 0) cand = 0;
-  __syncthreads();
-  if (tid < 64) {
-    int m = tid >> 3, n = tid & 7;
-    uint16_t c = cell[((k * 64 + m * 8) >> 2) * cs + ((l * 64 + n * 8) >> 2)];
-    if (CI_MODE(c) != 3 && (CI_CBPY(c) | CI_CBPU(c) | CI_CBPV(c))) atomicOr(&cand, 1);
-  }
-  __syncthreads();
-  if (!cand) return;
+                                            uint8_t *sV, uint16_t *sC) {
+  const int nh = W >> 6;
+  const int k = bx / nh, l = bx - (bx / nh) * nh;
+  const int tid = threadIdx.x;
+  const int cs = W >> 2;
   uint8_t *y0 = Y + (long long)(k * 64) * sy + l * 64;
   uint8_t *u0 = U + (long long)(k * 32) * sc + l * 32;
   uint8_t *v0 = V + (long long)(k * 32) * sc + l * 32;
-  for (int p = tid; p < 64 * 16; p += 256) {
-    int r = p >> 4, c4 = (p & 15) * 4;
-    *(uint32_t *)&sY[r * 64 + c4] = *(uint32_t *)(y0 + (long long)r * sy + c4);
-  }
-  for (int p = tid; p < 32 * 8; p += 256) {
-    int r = p >> 3, c4 = (p & 7) * 4;
-    *(uint32_t *)&sU[r * 32 + c4] = *(uint32_t *)(u0 + (long long)r * sc + c4);
-    *(uint32_t *)&sV[r * 32 + c4] = *(uint32_t *)(v0 + (long long)r * sc + c4);
-  }
+  // speculative loads: flag, the lane's 16 luma bytes, 4 U + 4 V bytes, one side-info word
+  const int fl = flags[bx];
+  const int ry = tid >> 2, cy = (tid & 3) * 16;
+  const uint4 py = *(const uint4 *)(y0 + (long long)ry * sy + cy);
+  const int rc = tid >> 3, cc = (tid & 7) * 4;
+  const uint32_t pu = *(const uint32_t *)(u0 + (long long)rc * sc + cc);
+  const uint32_t pv = *(const uint32_t *)(v0 + (long long)rc * sc + cc);
+  uint16_t ci = 0;
+  if (tid < 64) ci = cell[((k * 64 + (tid >> 3) * 8) >> 2) * cs + ((l * 64 + (tid & 7) * 8) >> 2)];
+  if (!fl) return;  // uniform
+  *(uint4 *)&sY[ry * 64 + cy] = py;
+  *(uint32_t *)&sU[rc * 32 + cc] = pu;
+  *(uint32_t *)&sV[rc * 32 + cc] = pv;
+  if (tid < 64) sC[tid] = ci;
   __syncthreads();
-  // luma: 4096 px, 16 per thread
-  for (int p = tid; p < 4096; p += 256) {
-    int r = p >> 6, c = p & 63;
-    uint16_t ci = cell[((k * 64 + (r & ~7)) >> 2) * cs + ((l * 64 + (c & ~7)) >> 2)];
-    if (CI_MODE(ci) == 3 || !CI_CBPY(ci)) continue;
-    int X = sY[r * 64 + c];
-    int A = r == 0 ? X : sY[(r - 1) * 64 + c];
-    int Bv = c == 0 ? X : sY[r * 64 + c - 1];
-    int Cv = c == 63 ? X : sY[r * 64 + c + 1];
-    int D = r == 63 ? X : sY[(r + 1) * 64 + c];
-    int delta = ((A > X) + (Bv > X) + (Cv > X) + (D > X) > 2) - ((A < X) + (Bv < X) + (Cv < X) + (D < X) > 2);
-    y0[(long long)r * sy + c] = (uint8_t)(X + delta);
+  // candidate SB: some 8x8 block not BIPRED with any cbp (clpf_frame, common/common_frame.c:498-508)
+  int cand = 0;
+  for (int b = 0; b < 64; b++) {
+    const uint16_t c = sC[b];
+    cand |= CI_MODE(c) != 3 && (CI_CBPY(c) | CI_CBPU(c) | CI_CBPV(c));
   }
-  for (int p = tid; p < 2048; p += 256) {
-    int pl = p >> 10, q = p & 1023;
-    int r = q >> 5, c = q & 31;
+  if (!cand) return;  // uniform (every lane read the same 64 words)
+  // luma: 16 pixels of row ry from column cy (two 8x8 blocks)
+  {
+    uint32_t o[4];
+    const uint16_t c0 = sC[(ry >> 3) * 8 + (cy >> 3)], c1 = sC[(ry >> 3) * 8 + (cy >> 3) + 1];
+    const bool f0 = CI_MODE(c0) != 3 && CI_CBPY(c0), f1 = CI_MODE(c1) != 3 && CI_CBPY(c1);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int c = cy + 4 * q + j;
+        const bool f = (4 * q + j) < 8 ? f0 : f1;
+        const int v = f ? clpf_px(sY, 64, 64, ry, c) : sY[ry * 64 + c];
+        w |= (uint32_t)v << (8 * j);
+      }
+      o[q] = w;
+    }
+    if (f0 || f1) *(uint4 *)(y0 + (long long)ry * sy + cy) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  // chroma: lanes 0-63 U, 64-127 V; 16 pixels of row r from column c0 (four 4x4 blocks)
+  if (tid < 128) {
+    const int pl = tid >> 6, t = tid & 63;
+    const int r = t >> 1, c0 = (t & 1) * 16;
     const uint8_t *s = pl ? sV : sU;
-    uint16_t ci = cell[((k * 64 + 2 * (r & ~3)) >> 2) * cs + ((l * 64 + 2 * (c & ~3)) >> 2)];
-    if (CI_MODE(ci) == 3 || !(pl ? CI_CBPV(ci) : CI_CBPU(ci))) continue;
-    int X = s[r * 32 + c];
-    int A = r == 0 ? X : s[(r - 1) * 32 + c];
-    int Bv = c == 0 ? X : s[r * 32 + c - 1];
-    int Cv = c == 31 ? X : s[r * 32 + c + 1];
-    int D = r == 31 ? X : s[(r + 1) * 32 + c];
-    int delta = ((A > X) + (Bv > X) + (Cv > X) + (D > X) > 2) - ((A < X) + (Bv < X) + (Cv < X) + (D < X) > 2);
-    (pl ? v0 : u0)[(long long)r * sc + c] = (uint8_t)(X + delta);
+    uint32_t o[4];
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // 4x4 chroma block q of the 16 columns = 8x8 luma block (r/4, c0/4 + q)
+      const uint16_t c = sC[(r >> 2) * 8 + (c0 >> 2) + q];
+      const bool f = CI_MODE(c) != 3 && (pl ? CI_CBPV(c) : CI_CBPU(c));
+      any |= f;
+      uint32_t w = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int cc2 = c0 + 4 * q + j;
+        const int v = f ? clpf_px(s, 32, 32, r, cc2) : s[r * 32 + cc2];
+        w |= (uint32_t)v << (8 * j);
+      }
+      o[q] = w;
+    }
+    if (any) *(uint4 *)((pl ? v0 : u0) + (long long)r * sc + c0) = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 __global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ uint8_t sY[64 * 64], sU[32 * 32], sV[32 * 32];
-  __shared__ int cand;
+  __shared__ uint16_t sC[64];
   const FrameCtx &f = F[blockIdx.y];
   if (!f.clpf_on) return;
   // one workgroup per flagged SB (the host's list), or per SB without a list
@@ -283,7 +313,7 @@ __global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
   if ((int)blockIdx.x >= nwork) return;
   const int sb = f.n_clpf >= 0 ? (int)f.clpf_list[blockIdx.x] : (int)blockIdx.x;
   if (sb >= (f.W >> 6) * (f.H >> 6)) return;
-  k_clpf_body(sb, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, cand);
+  k_clpf_body(sb, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, sC);
 }
 
 
