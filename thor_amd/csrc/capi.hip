@@ -51,7 +51,8 @@ struct thor_dec {
   std::vector<long long> slot_age;
   long long decode_count;
   uint16_t *cellinfo;
-  int32_t *cellmap;
+  uint2 *cellmc;
+  int32_t *cellmv1;
   unsigned *ctl;       // [0] intra row head, [1] timeout flag
   unsigned *progress;  // intra wavefront progress per (SB row, component)
   int16_t *resid;      // residual planes (Y, U, V; int16), written by k_prep_resid, read by k_recon / k_intra
@@ -170,8 +171,10 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   ok = ok && hipMemset(d->slots, 0, d->slot_bytes * num_slots) == hipSuccess;
   size_t ncell = (size_t)(W / 4) * (H / 4);
   ok = ok && hipMalloc(&d->cellinfo, ncell * sizeof(uint16_t)) == hipSuccess;
-  ok = ok && hipMalloc(&d->cellmap, ncell * sizeof(int32_t)) == hipSuccess;
-  ok = ok && hipMemset(d->cellmap, 0, ncell * sizeof(int32_t)) == hipSuccess;
+  ok = ok && hipMalloc(&d->cellmc, ncell * sizeof(uint2)) == hipSuccess;
+  ok = ok && hipMemset(d->cellmc, 0, ncell * sizeof(uint2)) == hipSuccess;
+  ok = ok && hipMalloc(&d->cellmv1, ncell * sizeof(int32_t)) == hipSuccess;
+  ok = ok && hipMemset(d->cellmv1, 0, ncell * sizeof(int32_t)) == hipSuccess;
   ok = ok && hipMemset(d->cellinfo, 0, ncell * sizeof(uint16_t)) == hipSuccess;
   ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
   ok = ok && hipMalloc(&d->resid, (size_t)W * H * 3) == hipSuccess;  // 1.5 px/luma px x 2 B
@@ -201,7 +204,8 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
   if (d->slots) (void)hipFree(d->slots);
   if (d->cellinfo) (void)hipFree(d->cellinfo);
-  if (d->cellmap) (void)hipFree(d->cellmap);
+  if (d->cellmc) (void)hipFree(d->cellmc);
+  if (d->cellmv1) (void)hipFree(d->cellmv1);
   if (d->ctl) (void)hipFree(d->ctl);
   if (d->progress) (void)hipFree(d->progress);
   if (d->resid) (void)hipFree(d->resid);
@@ -281,7 +285,8 @@ static bool make_ctx(const thor_dec *d, int cur_slot, int frame_num, FrameCtx &f
   f.ewc = d->ewc;
   f.nsbrows = (d->seq.height + 63) / 64;
   f.cellinfo = d->cellinfo;
-  f.cellmap = d->cellmap;
+  f.cellmc = d->cellmc;
+  f.cellmv1 = d->cellmv1;
   f.resid = d->resid;
   f.ctl = d->ctl;
   f.progress = d->progress;

@@ -42,7 +42,8 @@ struct FrameCtx {
   const uint32_t *clpf_list;  // flagged SBs (n_clpf >= 0) or every SB (n_clpf < 0)
   int n_clpf;
   uint16_t *cellinfo;
-  int32_t *cellmap;
+  uint2 *cellmc;    // per 4x4 cell: (mv0 with `sign` applied, MC meta word) -- k_recon's P0 input
+  int32_t *cellmv1; // per 4x4 cell: mv1 (written for bi-pred cells only)
   int16_t *resid;
   unsigned *ctl, *progress;
   int *rowstart;
@@ -55,6 +56,11 @@ struct FrameCtx {
 // batched kernel takes it as its FIRST argument and reads the per-frame
 // contexts straight from the kernarg segment (scalar loads, dynamic index).
 #define THOR_MAX_BATCH 8
+
+// MC meta word of a 4x4 cell (cellmc.y): reference slots and flags
+#define CELL_ACT 0x10000u
+#define CELL_BI 0x20000u
+#define CELL_RES(c) (0x40000u << (c))  // inter cell with a coded residual in component c
 struct FrameBatch {
   FrameCtx f[THOR_MAX_BATCH];
 };

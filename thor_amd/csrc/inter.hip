@@ -39,9 +39,6 @@
 #include "common.h"
 
 #define SB_CELLS 256
-#define CELL_ACT 0x10000u
-#define CELL_BI 0x20000u
-#define CELL_RES(c) (0x40000u << (c))  // inter cell with a coded residual in component c
 
 // reference window for one (mv, slot) key and one half SB
 #define WL_P 96  // luma pitch: 64 + 5 taps + 15 alignment, rounded to 16 B
@@ -506,8 +503,6 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   const FrameCtx &f = F[blockIdx.y];
   if (f.nblocks <= 0) return;
   if (blockIdx.y) dbg = nullptr;
-  const thor_block_t *__restrict__ blk = f.blk;
-  const int32_t *__restrict__ cellmap = f.cellmap;
   int16_t *__restrict__ resid = f.resid;
   const int lane = threadIdx.x;
   // debug only (null in the product path): s_memrealtime stamps, 8 u64 per wave
@@ -534,44 +529,27 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   // reference lookup table (packed by the host)
   if (lane < 32) *(int *)&L.lut[4 * lane] = f.slot_lut[lane];
 
-  // ---- P0: lane = cell row cr of 8x8 unit uu of the half ----
+  // ---- P0: lane = cell row cr of 8x8 unit uu of the half: the two cells' MC
+  // words that k_frame_prep resolved (quarter MV with the `sign` negation,
+  // inter_prediction.c:78-79 / :125-126, reference slots, bi-pred, coded
+  // residual per component), one 16-byte load ----
   const int uu = lane >> 1, cr = lane & 1;
   const int ur = uu >> 3, uc = uu & 7;
   const int uy = sby * 64 + 32 * h + 8 * ur, ux = sbx * 64 + 8 * uc;
-  int b = -1;
-  if (uy < f.H && ux < f.W) b = cellmap[(uy >> 2) * cs + (ux >> 2)];
-  bool inter = false, bi_any = false;
-  wave_lds_sync();  // lut
   const int lrow = 2 * ur + cr;  // cell row inside the half
-  if (b >= 0) {
-    const thor_block_t &B = blk[b];
-    const int mode = B.mode, S = B.size, by = B.ypos, bx = B.xpos;
-    const unsigned resbits = mode == M_SKIP ? 0u : ((unsigned)(B.coeff_mask & 7) << 18);
-    const bool bi = mode == M_BIPRED || ((mode == M_SKIP || mode == M_MERGE) && B.dir == 2);
-    const int ref0 = B.ref0, ref1 = B.ref1;
-    const int sg0 = bi ? (ref0 >= f.frame_num) : (ref0 > f.frame_num);
-    const int sg1 = ref1 >= f.frame_num;
-    const int s0 = L.lut[ref0 & 127], s1 = bi ? L.lut[ref1 & 127] : 0;
+  uint4 mc = make_uint4(0, 0, 0, 0);
+  const int cidx = ((uy >> 2) + cr) * cs + (ux >> 2);
+  if (uy < f.H && ux < f.W) mc = *(const uint4 *)&f.cellmc[cidx];
+  bool inter = false, bi_any = false;
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
-      const int cy = uy + 4 * cr, cx = ux + 4 * c;
-      bool act = mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0);
-      if (mode == M_SKIP) act = act && cx < bx + B.bwidth && cy < by + B.bheight;
-      const int q = (mode == M_INTER || mode == M_BIPRED) ? 2 * (cy - by >= (S >> 1)) + (cx - bx >= (S >> 1)) : 0;
-      int m0x = B.mv0[2 * q], m0y = B.mv0[2 * q + 1], m1x = B.mv1[2 * q], m1y = B.mv1[2 * q + 1];
-      if (sg0) { m0x = -m0x; m0y = -m0y; }
-      if (sg1) { m1x = -m1x; m1y = -m1y; }
-      const int cell = lrow * 16 + 2 * uc + c;
-      L.mv0[cell] = (m0x & 0xffff) | (m0y << 16);
-      L.mv1[cell] = bi ? ((m1x & 0xffff) | (m1y << 16)) : 0;
-      L.meta[cell] = act ? ((unsigned)s0 | ((unsigned)(bi ? s1 : 0) << 8) | CELL_ACT | (bi ? CELL_BI : 0u) | resbits)
-                         : 0u;
-      inter |= act;
-      bi_any |= act && bi;
-    }
-  } else {
-    L.meta[lrow * 16 + 2 * uc] = 0;
-    L.meta[lrow * 16 + 2 * uc + 1] = 0;
+  for (int c = 0; c < 2; c++) {
+    const unsigned meta = c ? mc.w : mc.y;
+    const int cell = lrow * 16 + 2 * uc + c;
+    L.mv0[cell] = (int)(c ? mc.z : mc.x);
+    L.mv1[cell] = (meta & CELL_BI) ? f.cellmv1[cidx + c] : 0;
+    L.meta[cell] = meta;
+    inter |= (meta & CELL_ACT) != 0;
+    bi_any |= (meta & CELL_BI) != 0;
   }
   const bool any_inter = __ballot(inter) != 0, any_bi = __ballot(bi_any) != 0;
   wave_lds_sync();

@@ -640,7 +640,7 @@ __global__ __launch_bounds__(256) void k_frame_prep(const FrameBatch fb_) {
   const FrameCtx &f = F[blockIdx.y];
   const int b = blockIdx.x;
   if (f.nblocks <= 0) return;
-  if (b < f.nprep) prep_body(b, f.blk, f.nblocks, f.cellinfo, f.cellmap, f.W >> 2);
+  if (b < f.nprep) prep_body(b, f);
   else if (b < f.nprep + f.nres) {
     const int w = threadIdx.x >> 6;
     resid_tu(RL[w], (b - f.nprep) * 4 + w, f.blk, f.tus, f.ntus, f.coeffs, f.resid, f.W, f.H);

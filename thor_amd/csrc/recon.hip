@@ -12,12 +12,12 @@
 // the packed side-info that copy_deblock_data (dec/decode_block.c:122-156)
 // stores for deblocking/CLPF.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void prep_body(int bx, const thor_block_t *__restrict__ blk, int nblocks,
-                                          uint16_t *__restrict__ cellinfo, int32_t *__restrict__ cellmap, int cstride) {
-  int b = bx * 4 + (threadIdx.x >> 6);
-  int lane = threadIdx.x & 63;
-  if (b >= nblocks) return;
-  const thor_block_t &B = blk[b];
+__device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
+  const int b = bx * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= f.nblocks) return;
+  const int cstride = f.W >> 2;
+  const thor_block_t &B = f.blk[b];
   int S = B.size;
   int mode = B.mode;
   int bw = B.bwidth >> 2, bh = B.bheight >> 2;
@@ -28,6 +28,18 @@ __device__ __forceinline__ void prep_body(int bx, const thor_block_t *__restrict
   int lqh = lsz - (((tb || pb == 1 || pb == 3) && S > 8) ? 1 : 0);  // PART_HOR / PART_QUAD, :183
   uint16_t base = (uint16_t)((mode & 7) | ((B.cbp_y != 0) << 3) | ((B.cbp_u != 0) << 4) | ((B.cbp_v != 0) << 5) |
                              (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
+  // the MC words k_recon reads (dec/decode_block.c:213-451): bi-pred for BIPRED
+  // and bi-directional SKIP / MERGE; `sign` = reference after the current frame
+  // (uni-pred: >, each bi-pred leg: >=, :259-260, :291, :328-329, :358, :377,
+  // :416-417); reference slot by frame number
+  const bool bi = mode == M_BIPRED || ((mode == M_SKIP || mode == M_MERGE) && B.dir == 2);
+  const int ref0 = B.ref0, ref1 = B.ref1;
+  const int sg0 = bi ? (ref0 >= f.frame_num) : (ref0 > f.frame_num);
+  const int sg1 = ref1 >= f.frame_num;
+  const int8_t *lut = (const int8_t *)f.slot_lut;
+  const int s0 = lut[ref0 & 127], s1 = bi ? lut[ref1 & 127] : 0;
+  const unsigned resbits = mode == M_SKIP ? 0u : ((unsigned)(B.coeff_mask & 7) << 18);
+  const bool quarters = mode == M_INTER || mode == M_BIPRED;  // four size/2 quarters with mv_arr[i], :381-392
   int div = S >> 3;
   int y4 = B.ypos >> 2, x4 = B.xpos >> 2;
   for (int c = lane; c < bw * bh; c += 64) {
@@ -36,8 +48,17 @@ __device__ __forceinline__ void prep_body(int bx, const thor_block_t *__restrict
     int a0 = B.mv0[2 * q], a1 = B.mv0[2 * q + 1], a2 = B.mv1[2 * q], a3 = B.mv1[2 * q + 1];
     int big = (abs(a0) >= 4) | (abs(a1) >= 4) | (abs(a2) >= 4) | (abs(a3) >= 4);
     int idx = (y4 + m) * cstride + x4 + n;
-    cellinfo[idx] = base | (uint16_t)(big << 6);
-    cellmap[idx] = b;
+    f.cellinfo[idx] = base | (uint16_t)(big << 6);
+    // MC word (the SKIP rectangle is already clipped to the frame: bwidth / bheight)
+    const int qq = quarters ? q : 0;
+    int m0x = B.mv0[2 * qq], m0y = B.mv0[2 * qq + 1], m1x = B.mv1[2 * qq], m1y = B.mv1[2 * qq + 1];
+    if (sg0) { m0x = -m0x; m0y = -m0y; }
+    if (sg1) { m1x = -m1x; m1y = -m1y; }
+    const bool act = mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0);
+    const unsigned meta =
+        act ? ((unsigned)s0 | ((unsigned)(bi ? s1 : 0) << 8) | CELL_ACT | (bi ? CELL_BI : 0u) | resbits) : 0u;
+    f.cellmc[idx] = make_uint2((uint32_t)((m0x & 0xffff) | (m0y << 16)), meta);
+    if (act && bi) f.cellmv1[idx] = (m1x & 0xffff) | (m1y << 16);
   }
 }
 

@@ -37,12 +37,40 @@ struct Dct32Table {
 __constant__ Dct32Table g_dct32 = Dct32Table();
 
 struct ResidLds {
-  int8_t M[1024];
   int16_t D[256];      // dequantised q x q tile, transposed: D[k][m]
   int16_t T[16 * 32];  // pass-1 output, transposed: T[y][k]
 };
 
 __device__ __forceinline__ int sx8(int w, int i) { return __builtin_amdgcn_sbfe(w, 8 * i, 8); }
+
+// Basis columns as int16 pairs for the inverse passes: for an n-point TU (n =
+// 4, 8, 16, 32), column p holds (M[2j*step][p], M[(2j+1)*step][p]) for the q =
+// min(n,16) coefficient rows, step = 32/n.  4 KB; each lane loads its 8 words.
+struct MColTable {
+  uint32_t v[4][32][8];
+  constexpr MColTable() : v() {
+    const int c[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                       61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+    for (int s = 0; s < 4; s++) {
+      const int n = 4 << s, step = 32 / n, q = n < 16 ? n : 16;
+      for (int p = 0; p < n; p++)
+        for (int j = 0; j < 8; j++) {
+          int e[2] = {0, 0};
+          for (int h = 0; h < 2; h++) {
+            const int k = (2 * j + h) * step;
+            if (2 * j + h >= q) continue;
+            if (k == 0) e[h] = 64;
+            else {
+              const int t = (k * (2 * p + 1)) & 127;
+              e[h] = t <= 32 ? c[t] : (t <= 64 ? -c[64 - t] : (t <= 96 ? -c[t - 64] : c[128 - t]));
+            }
+          }
+          v[s][p][j] = ((uint32_t)e[0] & 0xffffu) | ((uint32_t)e[1] << 16);
+        }
+    }
+  }
+};
+__constant__ MColTable g_mcol = MColTable();
 
 typedef short s16x2_r __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int rdot2(uint32_t a, uint32_t b, int c) {  // a.lo*b.lo + a.hi*b.hi + c (int16 pairs)
@@ -66,12 +94,10 @@ __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int nt
     L.D[k * q + m] = (int16_t)wrap16(((coef[e] * scale) * (1 << lshift) + add) >> rshift);
   }
   const int p = lane & (n - 1), grp = lane / n, ngrp = 64 / n;
-  uint32_t mc[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++)
-    mc[j] = 2 * j < q ? ((uint32_t)(int)L.M[(2 * j * step) * 32 + p] & 0xffffu) |
-                            ((uint32_t)(int)L.M[((2 * j + 1) * step) * 32 + p] << 16)
-                      : 0u;
+  const uint4 *mp = (const uint4 *)g_mcol.v[ilog2i(n) - 2][p];
+  const uint4 m0 = mp[0], m1 = mp[1];
+  const uint32_t mc[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+  (void)step;
   wave_lds_sync();
   for (int k = grp; k < q; k += ngrp) {  // pass 1, transform.c:455-463: T[k][p]
     const uint32_t *dk = (const uint32_t *)&L.D[k * q];
@@ -107,12 +133,10 @@ __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int nt
 __device__ __forceinline__ void resid_tu(ResidLds &L, int idx, const thor_block_t *__restrict__ blk,
                                          const uint32_t *__restrict__ tus, int ntus, const int16_t *__restrict__ coeffs,
                                          int16_t *__restrict__ resid, int W, int H) {
-  const int lane = threadIdx.x & 63;
   if (idx >= ntus) return;
   const uint32_t e = tus[idx];
   const thor_block_t &B = blk[e >> 4];
   const int c = (e >> 2) & 3, t = e & 3;
-  *(uint4 *)&L.M[16 * lane] = *(const uint4 *)&g_dct32.v[16 * lane];
   const int S = B.size, tb = B.tb_split != 0;
   const int size = c ? S >> 1 : S;
   const int tbc = c ? (tb && S > 8) : tb;  // chroma of an 8x8 CU is not split, dec/decode_block.c:449-450
