@@ -185,7 +185,7 @@ struct GlobChroma {
 // column -2 inside the fetched dwords.  Vertical taps as int16 pairs.
 template <int R0, int N, class Src>
 __device__ __forceinline__ void luma_rows(const Src &src, uint32_t sh, int tw0, int tw1, int v01, int v23, int v45,
-                                          uint32_t out[8]) {
+                                          uint32_t out[8], bool acc) {
   constexpr int NR = N + 5;
   uint32_t pre[Src::PF ? NR : 1][3];
   if (Src::PF) {
@@ -219,7 +219,7 @@ __device__ __forceinline__ void luma_rows(const Src &src, uint32_t sh, int tw0, 
       acc = dot2(pa[(i + 2 + 6) % 6][j], v45, acc);
       o |= mc_pack(acc, j);
     }
-    out[i] = o;
+    out[i] = acc ? avg_bytes(out[i], o) : o;  // bi-pred: truncating average with pass 0
   }
 }
 
@@ -230,7 +230,7 @@ __device__ __forceinline__ void luma_rows(const Src &src, uint32_t sh, int tw0, 
 // packed int16 -> four v_dot2 per pixel; (S + 8) >> 4 with the bias
 // 128 * 16 = 2048 folded in.
 template <int R0, int N, class Src>
-__device__ __forceinline__ void luma_rows_ctr(const Src &src, uint32_t sh, uint32_t out[8]) {
+__device__ __forceinline__ void luma_rows_ctr(const Src &src, uint32_t sh, uint32_t out[8], bool acc) {
   constexpr int NR = N + 3;
   uint32_t pre[Src::PF ? NR : 1][3];
   if (Src::PF) {
@@ -266,13 +266,14 @@ __device__ __forceinline__ void luma_rows_ctr(const Src &src, uint32_t sh, uint3
       acc = dot2(q[(i + 2 + 6) % 6][j], 0x00010000, acc);
       o |= put_byte(clip255(acc >> 4), j);
     }
-    out[i] = o;
+    out[i] = acc ? avg_bytes(out[i], o) : o;  // bi-pred: truncating average with pass 0
   }
 }
 
 // Chroma rows R0 .. R0+N-1 (of 4) of the lane's 2-px column, U and V.
 template <int R0, int N, class Src>
-__device__ __forceinline__ void chroma_rows(const Src &src, uint32_t sh, int tw, int v01, int v23, uint32_t out[4]) {
+__device__ __forceinline__ void chroma_rows(const Src &src, uint32_t sh, int tw, int v01, int v23, uint32_t out[4],
+                                            bool acc) {
   constexpr int NR = N + 3;
   uint32_t preu[Src::PF ? NR : 1][2], prev_[Src::PF ? NR : 1][2];
   if (Src::PF) {
@@ -319,7 +320,8 @@ __device__ __forceinline__ void chroma_rows(const Src &src, uint32_t sh, int tw,
       ou |= mc_pack(au, j);
       ov |= mc_pack(av, j);
     }
-    out[i] = ou | (ov << 16);  // U in the low half, V in the high half
+    const uint32_t uv = ou | (ov << 16);  // U in the low half, V in the high half
+    out[i] = acc ? avg_bytes(out[i], uv) : uv;
   }
 }
 
@@ -329,21 +331,21 @@ template <class LSrc, class CSrc>
 __device__ __forceinline__ void filter_items(bool m0, bool m1, const LSrc &l0, const LSrc &l1, uint32_t lsh0, uint32_t lsh1,
                                              const CSrc &c0, const CSrc &c1, uint32_t csh0, uint32_t csh1,
                                              const Key &K0, const Key &K1, bool same, int bipred, uint32_t ty[8],
-                                             uint32_t tc[4]) {
+                                             uint32_t tc[4], bool acc) {
   auto luma = [&](auto r0c, auto nc, const LSrc &src, uint32_t sh, const Key &K) {
     constexpr int R0 = decltype(r0c)::value, N = decltype(nc)::value;
-    if (K.fx == 2 && K.fy == 2) luma_rows_ctr<R0, N>(src, sh, ty);
+    if (K.fx == 2 && K.fy == 2) luma_rows_ctr<R0, N>(src, sh, ty, acc);
     else {
       int v01, v23, v45;
       tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45);
-      luma_rows<R0, N>(src, sh, g_taps.luma[bipred][K.fx][0], g_taps.luma[bipred][K.fx][1], v01, v23, v45, ty);
+      luma_rows<R0, N>(src, sh, g_taps.luma[bipred][K.fx][0], g_taps.luma[bipred][K.fx][1], v01, v23, v45, ty, acc);
     }
   };
   auto chroma = [&](auto r0c, auto nc, const CSrc &src, uint32_t sh, const Key &K) {
     constexpr int R0 = decltype(r0c)::value, N = decltype(nc)::value;
     const int cvt = g_taps.chroma[K.cfy];
     chroma_rows<R0, N>(src, sh, g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
-                       (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc);
+                       (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc, acc);
   };
   using I0 = std::integral_constant<int, 0>;
   using I2 = std::integral_constant<int, 2>;
@@ -445,7 +447,7 @@ __device__ __forceinline__ bool first_key(const Items &it, Key &K) {
 
 // Filter every pending item whose key is K from the staged window; clears them.
 __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bipred, int x0, Items &it, uint32_t ty[8],
-                                           uint32_t tc[4]) {
+                                           uint32_t tc[4], bool acc) {
   const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
   const bool m0 = (it.pend & 1) && it.mv[0] == K.mv && it.slot[0] == K.slot;
   const bool m1 = (it.pend & 2) && it.mv[1] == K.mv && it.slot[1] == K.slot;
@@ -454,14 +456,14 @@ __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bi
   const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
   const LdsChroma c{w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3)};
   filter_items(m0, m1, l, l, (uint32_t)(lwb & 3), (uint32_t)(lwb & 3), c, c, (uint32_t)(cwb & 3), (uint32_t)(cwb & 3),
-               K, K, true, bipred, ty, tc);
+               K, K, true, bipred, ty, tc, acc);
   it.pend &= ~((m0 ? 1u : 0u) | (m1 ? 2u : 0u));
 }
 
 // Waves whose items need several keys: every item straight from the ring,
 // per-lane keys (one pass, no per-key staging round trips).
 __device__ __forceinline__ void filter_direct(const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, int bipred, int x0,
-                                              int y0, Items &it, uint32_t ty[8], uint32_t tc[4]) {
+                                              int y0, Items &it, uint32_t ty[8], uint32_t tc[4], bool acc) {
   const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
   const Key K0 = make_key(it.mv[0], it.slot[0]), K1 = make_key(it.mv[1], it.slot[1]);
   const bool m0 = it.pend & 1, m1 = (it.pend >> 1) & 1;
@@ -478,7 +480,7 @@ __device__ __forceinline__ void filter_direct(const FrameCtx &f, __amdgpu_buffer
   const GlobLuma g0{ring, l0 & ~3, f.sy}, g1{ring, l1 & ~3, f.sy};
   const GlobChroma h0{ring, c0 & ~3, uvd, f.sc}, h1{ring, c1 & ~3, uvd, f.sc};
   filter_items(m0, m1, g0, g1, (uint32_t)(l0 & 3), (uint32_t)(l1 & 3), h0, h1, (uint32_t)(c0 & 3), (uint32_t)(c1 & 3), K0,
-               K1, same, bipred, ty, tc);
+               K1, same, bipred, ty, tc, acc);
   it.pend = 0;
 }
 
@@ -563,7 +565,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   const __amdgpu_buffer_rsrc_t ring =  // one descriptor over the whole ring (< 2 GiB: 32-bit offsets)
       __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
   const int x0 = sbx * 64, y0 = sby * 64 + 32 * h, cc = lane & 15, gr = lane >> 4;
-  uint32_t ly[8], lc[4], ty[8], tc[4];
+  uint32_t ly[8], lc[4];  // the lane's prediction: 8 luma rows x 4 px, 4 chroma rows x 2 px x (U, V)
   for (int pass = 0; pass <= (int)any_bi; pass++) {
     Items it = job_items(L, pass);
     Key K;
@@ -576,21 +578,11 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
         win_commit(W, L.win);
         wave_lds_sync();
         if (pass == 0) STAMP(4);
-        filter_key(L.win, K, f.bipred, x0, it, ty, tc);
+        filter_key(L.win, K, f.bipred, x0, it, ly, lc, pass != 0);
       } else {
         if (pass == 0) STAMP(4);
-        filter_direct(f, ring, f.bipred, x0, y0, it, ty, tc);
+        filter_direct(f, ring, f.bipred, x0, y0, it, ly, lc, pass != 0);
       }
-    }
-    // merge: pass 0 result, or the truncating bi-pred average
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const unsigned meta = L.meta[(2 * gr + s) * 16 + cc];
-      if (!((meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI)))) continue;
-#pragma unroll
-      for (int i = 4 * s; i < 4 * s + 4; i++) ly[i] = pass ? avg_bytes(ly[i], ty[i]) : ty[i];
-#pragma unroll
-      for (int i = 2 * s; i < 2 * s + 2; i++) lc[i] = pass ? avg_bytes(lc[i], tc[i]) : tc[i];
     }
     wave_lds_sync();
   }
