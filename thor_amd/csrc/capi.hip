@@ -17,8 +17,8 @@
 __global__ void k_frame_prep(const FrameBatch);
 __global__ void k_recon(const FrameBatch, unsigned long long *);
 __global__ void k_intra(const FrameBatch, unsigned long long *, int);
-__global__ void k_deblock_v(const FrameBatch, int);
-__global__ void k_deblock_h(const FrameBatch, int);
+__global__ void k_deblock_v(const FrameBatch, int, int);
+__global__ void k_deblock_h(const FrameBatch, int, int);
 __global__ void k_clpf(const FrameBatch);
 __global__ void k_pad(const FrameBatch);
 
@@ -323,7 +323,7 @@ int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, 
 struct Batch {
   FrameBatch fb;
   int n, cur[THOR_MAX_BATCH], frame_num[THOR_MAX_BATCH];
-  int max_prep, any_intra, any_clpf, any_deblock, clpf_grid;
+  int max_prep, any_intra, any_clpf, any_deblock, clpf_grid, max_intra;
 };
 
 static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins,
@@ -345,6 +345,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
   b.max_prep = 1;
   b.any_intra = b.any_clpf = b.any_deblock = 0;
   b.clpf_grid = 0;
+  b.max_intra = 0;
   for (int i = 0; i < n; i++) {
     thor_dec *d = ds[i];
     const thor_frame_in_t &in = ins[i];
@@ -373,6 +374,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.band1 = d->band1 > 0 ? d->band1 : f.nsbrows;
     b.max_prep = b.max_prep > f.nprep + f.nres + 1 ? b.max_prep : f.nprep + f.nres + 1;
     b.any_intra |= in.n_intra > 0;
+    b.max_intra = b.max_intra > in.n_intra ? b.max_intra : in.n_intra;
     if (f.clpf_on) {
       const int w = f.n_clpf >= 0 ? f.n_clpf : (W / 64) * (H / 64);
       b.clpf_grid = b.clpf_grid > w ? b.clpf_grid : w;
@@ -421,8 +423,12 @@ static int batch_phase_b(thor_dec *lead, const Batch &b) {
     int nh = (W >> 3) * ((H >> 3) - 1);
     // luma and both chroma planes of one edge direction per launch
     const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
-    k_deblock_v<<<dim3(3 * bv, n), 256, 0, st>>>(b.fb, bv);
-    k_deblock_h<<<dim3(3 * bh, n), 256, 0, st>>>(b.fb, bh);
+    // chroma: with few intra CUs (P frames) one (intra CU, plane) item per wave,
+    // else every chroma edge segment like luma
+    const int clist = b.max_intra <= 1024;
+    const int bc = clist ? (2 * b.max_intra + 3) / 4 : 0;
+    k_deblock_v<<<dim3(clist ? bv + bc : 3 * bv, n), 256, 0, st>>>(b.fb, bv, clist);
+    k_deblock_h<<<dim3(clist ? bh + bc : 3 * bh, n), 256, 0, st>>>(b.fb, bh, clist);
     HIPCHK(hipGetLastError());
   }
   if (b.any_clpf && b.clpf_grid > 0) {

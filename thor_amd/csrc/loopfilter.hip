@@ -183,35 +183,73 @@ __device__ __forceinline__ void k_deblock_chroma_h_body(int t, int by, uint8_t *
 // side info, never luma pixels, so the planes are independent within a pass;
 // vertical edges of all planes before horizontal ones, deblock_frame_y /
 // deblock_frame_uv, common/common_frame.c:46-321).
-// DB_ITEMS edge segments per lane (grid-stride): the launch is a quarter as
-// many waves, and most segments of a skip-dominated frame end after two
-// side-info reads.
-#define DB_ITEMS 4
-__global__ __launch_bounds__(256) void k_deblock_v(const FrameBatch fb_, int nbl) {
-  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
-  const FrameCtx &f = F[blockIdx.y];
-  if (!f.deblock) return;
-  const int b = blockIdx.x;
-  const int c = b < nbl ? -1 : ((b - nbl) >= nbl);
-  const int bb = c < 0 ? b : b - nbl - c * nbl;
-  for (int r = 0; r < DB_ITEMS; r++) {
-    const int t = bb * 256 + (int)threadIdx.x + r * nbl * 256;
-    if (c < 0) k_deblock_luma_v_body(t, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
-    else k_deblock_chroma_v_body(t, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
-  }
+// Chroma edges filter only where P or Q is intra (deblock_frame_uv,
+// common/common_frame.c:243-321), so they are enumerated from the frame's
+// intra CU list: one wave per (intra CU, plane), one lane per 8-luma-pixel
+// segment of its left / right (vertical pass) or top / bottom (horizontal
+// pass) boundary.  An edge between two intra CUs is filtered once, by the CU
+// on its Q side.
+__device__ __forceinline__ void chroma_intra_edges(const FrameCtx &f, int item, bool vertical) {
+  const int lane = threadIdx.x & 63;
+  if (item >= 2 * f.nintra) return;
+  const int plane = item & 1;
+  const thor_block_t &B = f.blk[f.ilist[item >> 1]];
+  const int S = B.size, x = B.xpos, y = B.ypos, nseg = S >> 3;
+  if (lane >= 2 * nseg) return;
+  const int side = lane >= nseg, k = lane - side * nseg;  // side 0: this CU is Q, 1: this CU is P
+  const int cs = f.W >> 2;
+  const int i = vertical ? y + 8 * k : (side ? y + S : y);
+  const int j = vertical ? (side ? x + S : x) : x + 8 * k;
+  if (i >= f.H || j >= f.W || (vertical ? j : i) < 8) return;
+  if (side && CI_MODE(f.cellinfo[(i >> 2) * cs + (j >> 2)]) == M_INTRA) return;  // the intra Q CU owns it
+  if (vertical)
+    k_deblock_chroma_v_body((i >> 3) * ((f.W >> 3) - 1) + (j >> 3) - 1, plane, f.cu, f.cv, f.sc, f.W, f.H,
+                            f.cellinfo, f.qpc);
+  else
+    k_deblock_chroma_h_body(((i >> 3) - 1) * (f.W >> 3) + (j >> 3), plane, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo,
+                            f.qpc);
 }
-__global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl) {
+
+// DB_ITEMS luma edge segments per lane (grid-stride): a quarter as many
+// waves, and most segments of a skip-dominated frame end after two side-info
+// reads.  Blocks [0, nbl): luma; [nbl, ...): chroma of the intra CUs (four
+// (CU, plane) items per workgroup).
+#define DB_ITEMS 4
+__global__ __launch_bounds__(256) void k_deblock_v(const FrameBatch fb_, int nbl, int clist) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   const FrameCtx &f = F[blockIdx.y];
   if (!f.deblock) return;
   const int b = blockIdx.x;
-  const int c = b < nbl ? -1 : ((b - nbl) >= nbl);
-  const int bb = c < 0 ? b : b - nbl - c * nbl;
-  for (int r = 0; r < DB_ITEMS; r++) {
-    const int t = bb * 256 + (int)threadIdx.x + r * nbl * 256;
-    if (c < 0) k_deblock_luma_h_body(t, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
-    else k_deblock_chroma_h_body(t, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+  if (b >= nbl) {
+    if (clist) {  // few intra CUs: enumerate their boundaries
+      chroma_intra_edges(f, (b - nbl) * 4 + (threadIdx.x >> 6), true);
+      return;
+    }
+    const int c = (b - nbl) >= nbl, bb = b - nbl - c * nbl;  // every chroma edge segment, per plane
+    for (int r = 0; r < DB_ITEMS; r++)
+      k_deblock_chroma_v_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+    return;
   }
+  for (int r = 0; r < DB_ITEMS; r++)
+    k_deblock_luma_v_body(b * 256 + (int)threadIdx.x + r * nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+}
+__global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl, int clist) {
+  const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
+  const FrameCtx &f = F[blockIdx.y];
+  if (!f.deblock) return;
+  const int b = blockIdx.x;
+  if (b >= nbl) {
+    if (clist) {  // few intra CUs: enumerate their boundaries
+      chroma_intra_edges(f, (b - nbl) * 4 + (threadIdx.x >> 6), false);
+      return;
+    }
+    const int c = (b - nbl) >= nbl, bb = b - nbl - c * nbl;  // every chroma edge segment, per plane
+    for (int r = 0; r < DB_ITEMS; r++)
+      k_deblock_chroma_h_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+    return;
+  }
+  for (int r = 0; r < DB_ITEMS; r++)
+    k_deblock_luma_h_body(b * 256 + (int)threadIdx.x + r * nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
 }
 
 // One flagged SB per workgroup.  The SB's pixels and its 64 8x8-block side
