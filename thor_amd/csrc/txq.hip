@@ -53,7 +53,9 @@ __device__ __forceinline__ int quant_scale(int r) {
 
 // Working set of one transform block (one wavefront, ~14 KB of LDS).
 struct TxLds {
-  int16_t R[64 * 64];  // residual in / reconstructed residual out (row-major, stride = size)
+  int16_t R[32 * 32];  // residual in / reconstructed residual out (row-major, stride = min(size, 32);
+                       // a 64x64 TU's input is pre-summed straight into A, its output is the
+                       // 32x32 inverse before the 2x2 replication)
   int16_t A[32 * 32];  // 2x2 / 4x4 pre-summed input of the 32/64 paths
   int16_t T[16 * 32];  // forward pass-1 output / inverse pass-1 output
   int C[256];          // q x q coefficients (raster), then quantised levels (raster)
@@ -102,7 +104,22 @@ __device__ __forceinline__ int fwd8_simd(const int16_t *s, int k, int shift) {
   return wrap16((v + (1 << (shift - 1))) >> shift);
 }
 
-// Forward transform of L.R (size x size, stride size) into L.C (q x q raster,
+// Pre-summed input of a 64x64 TU into L.A from element accessor v(y, x):
+// 4x4 sums -> 16x16 (fast) or 2x2 sums -> 32x32 (transform.c:273-307), int16 stores.
+template <class V>
+__device__ __forceinline__ void presum64(TxLds &L, int fast, V v) {
+  const int lane = threadIdx.x & 63;
+  const int f = fast ? 4 : 2, n = 64 / f;
+  for (int e = lane; e < n * n; e += 64) {
+    const int i = e / n, j = e - i * n;
+    int s = 0;
+    for (int a = 0; a < f; a++)
+      for (int b = 0; b < f; b++) s += v(i * f + a, j * f + b);
+    L.A[e] = (int16_t)wrap16(s);
+  }
+}
+
+// Forward transform of L.R (size x size, stride size; size 64: L.A pre-summed) into L.C (q x q raster,
 // q = min(size, 16)), the low-frequency corner transform / transform_simd
 // compute (common/transform.c:249-330; 32/64 `fast` pre-sum 2x2 / 4x4 into a
 // 16-point transform, :273-293; 64 non-fast pre-sums 2x2 into a 32-point
@@ -116,24 +133,18 @@ __device__ void fwd_tx(TxLds &L, int size, int fast) {
     N = 16;
     sh1 += 1 + (size == 64);
     sh2 = 9;
-    const int f = size >> 4;
-    for (int e = lane; e < 256; e += 64) {
-      const int i = e >> 4, j = e & 15;
-      int s = 0;
-      for (int a = 0; a < f; a++)
-        for (int b = 0; b < f; b++) s += L.R[(i * f + a) * size + j * f + b];
-      L.A[e] = (int16_t)wrap16(s);
+    if (size == 32) {  // 2x2 pre-sum (a 64x64 TU arrives pre-summed 4x4 in A)
+      for (int e = lane; e < 256; e += 64) {
+        const int i = e >> 4, j = e & 15;
+        const int16_t *r = &L.R[(2 * i) * 32 + 2 * j];
+        L.A[e] = (int16_t)wrap16(r[0] + r[1] + r[32] + r[33]);
+      }
     }
     in = L.A;
-  } else if (size == 64) {
+  } else if (size == 64) {  // pre-summed 2x2 into A by the caller
     N = 32;
     sh1 = 7;
     sh2 = 10;
-    for (int e = lane; e < 1024; e += 64) {
-      const int i = e >> 5, j = e & 31;
-      const int16_t *r = &L.R[(2 * i) * 64 + 2 * j];
-      L.A[e] = (int16_t)wrap16(r[0] + r[1] + r[64] + r[65]);
-    }
     in = L.A;
   }
   wave_lds_sync();
@@ -243,8 +254,8 @@ __device__ void dequant_tu(TxLds &L, int qp, int size) {
 }
 
 // Inverse transform (common/transform.c:432-518) of the q x q coefficients in
-// L.C into L.R (size x size, stride size): pass 1 clip16((s + 64) >> 7), pass 2
-// clip16((s + 2048) >> 12); 64 = 32-point + 2x2 replication.
+// L.C into L.R (n x n, n = min(size, 32)): pass 1 clip16((s + 64) >> 7), pass 2
+// clip16((s + 2048) >> 12); 64 = 32-point, the caller replicates 2x2.
 __device__ void inv_tx(TxLds &L, int size) {
   const int lane = threadIdx.x & 63;
   const int rep = size == 64, n = rep ? 32 : size, q = n < 16 ? n : 16, step = 32 / n;
@@ -259,15 +270,7 @@ __device__ void inv_tx(TxLds &L, int size) {
     const int yp = e / n, xp = e - yp * n;
     int s = 0;
     for (int k = 0; k < q; k++) s += (int)L.M[(k * step) * 32 + xp] * (int)L.T[k * n + yp];
-    const int16_t r = (int16_t)clip16((s + 2048) >> 12);
-    if (rep) {
-      L.R[(2 * yp) * 64 + 2 * xp] = r;
-      L.R[(2 * yp) * 64 + 2 * xp + 1] = r;
-      L.R[(2 * yp + 1) * 64 + 2 * xp] = r;
-      L.R[(2 * yp + 1) * 64 + 2 * xp + 1] = r;
-    } else {
-      L.R[yp * n + xp] = r;
-    }
+    L.R[yp * n + xp] = (int16_t)clip16((s + 2048) >> 12);  // 64: before the 2x2 replication
   }
   wave_lds_sync();
 }
@@ -291,10 +294,15 @@ __global__ __launch_bounds__(64) void k_enc_tu(const thor_enc_tu_t *__restrict__
   }
   tx_load_basis(L);
   const uint8_t *po = orig + U.orig_off, *pp = pred + U.pred_off;
-  for (int e = lane; e < size * size; e += 64) {  // get_residual, enc/encode_block.c:484-493
-    const int y = e / size, x = e - y * size;
-    L.R[e] = (int16_t)((int)po[(long long)y * U.orig_stride + x] - (int)pp[(long long)y * U.pred_stride + x]);
-  }
+  auto res = [&](int y, int x) {  // get_residual, enc/encode_block.c:484-493
+    return (int)(int16_t)((int)po[(long long)y * U.orig_stride + x] - (int)pp[(long long)y * U.pred_stride + x]);
+  };
+  if (size == 64) presum64(L, U.fast, res);
+  else
+    for (int e = lane; e < size * size; e += 64) {
+      const int y = e / size, x = e - y * size;
+      L.R[e] = (int16_t)res(y, x);
+    }
   wave_lds_sync();
   fwd_tx(L, size, U.fast);
   const int cbp = quant_tu(L, U.qp, size, U.type);
@@ -308,7 +316,8 @@ __global__ __launch_bounds__(64) void k_enc_tu(const thor_enc_tu_t *__restrict__
   for (int e = lane; e < size * size; e += 64) {  // reconstruct_block / memcpy(rec, pblock), :1512-1517
     const int y = e / size, x = e - y * size;
     const int p = pp[(long long)y * U.pred_stride + x];
-    const int r = cbp ? clip255(L.R[e] + p) : p;
+    const int rv = size == 64 ? L.R[(y >> 1) * 32 + (x >> 1)] : L.R[e];  // 64: 2x2 replication
+    const int r = cbp ? clip255(rv + p) : p;
     pr[(long long)y * U.rec_stride + x] = (uint8_t)r;
     const int d = (int)po[(long long)y * U.orig_stride + x] - r;
     ssd += (unsigned)(d * d);
@@ -346,7 +355,9 @@ __global__ __launch_bounds__(64) void k_ftx_call(const int16_t *__restrict__ blo
   __shared__ TxLds L;
   const int lane = threadIdx.x;
   tx_load_basis(L);
-  for (int e = lane; e < size * size; e += 64) L.R[e] = block[e];
+  if (size == 64) presum64(L, fast, [&](int y, int x) { return (int)block[y * 64 + x]; });
+  else
+    for (int e = lane; e < size * size; e += 64) L.R[e] = block[e];
   wave_lds_sync();
   fwd_tx(L, size, fast);
   const int q = size < 16 ? size : 16;
@@ -364,7 +375,10 @@ __global__ __launch_bounds__(64) void k_itx_call(const int16_t *__restrict__ coe
   for (int e = lane; e < q * q; e += 64) L.C[e] = coeff[(e / q) * size + (e % q)];
   wave_lds_sync();
   inv_tx(L, size);
-  for (int e = lane; e < size * size; e += 64) block[e] = L.R[e];
+  for (int e = lane; e < size * size; e += 64) {
+    const int y = e / size, x = e - y * size;
+    block[e] = size == 64 ? L.R[(y >> 1) * 32 + (x >> 1)] : L.R[e];
+  }
 }
 
 extern "C" {
