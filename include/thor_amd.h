@@ -79,6 +79,17 @@ typedef struct thor_frame_hdr {
   int32_t clpf_on;     /* CLPF signalled on for this frame (dec/decode_frame.c:130) */
 } thor_frame_hdr_t;
 
+/* One coded transform block of a frame (thor_build_tu_list): everything the
+ * residual kernel needs, so it reads no block descriptor.  12 bytes. */
+typedef struct thor_tu {
+  uint32_t coeff_off; /* int16 offset of the TU's q x q tile in the coefficient pool */
+  uint16_t y, x;      /* TU origin in its plane (chroma planes: chroma pixels)     */
+  uint8_t size;       /* 4..64                                                     */
+  uint8_t comp;       /* 0 Y, 1 U, 2 V                                             */
+  uint8_t qp;         /* component qp (chroma: chroma_qp[qp])                      */
+  uint8_t rsv;
+} thor_tu_t;
+
 /* ---- batched decoder context ------------------------------------------ */
 typedef struct thor_dec thor_dec_t;
 
@@ -99,7 +110,8 @@ void thor_dec_destroy(thor_dec_t *d);
  * padding.  The reconstructed frame becomes reference `frame_num`. */
 int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
                    const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
-                   const uint32_t *tu_list, int n_tu);
+                   const thor_tu_t *tu_list, int n_tu);
+
 
 /* One frame's parse output (DEVICE pointers), as thor_dec_frame takes it. */
 typedef struct thor_frame_in {
@@ -109,7 +121,7 @@ typedef struct thor_frame_in {
   const uint8_t *clpf_flags;
   const uint32_t *intra_list;
   int32_t n_intra;
-  const uint32_t *tu_list;
+  const thor_tu_t *tu_list;
   int32_t n_tu;
   const uint32_t *clpf_list; /* indices of the SBs whose CLPF flag is set (thor_build_clpf_list) */
   int32_t n_clpf;            /* -1: no list, scan every SB's flag */
@@ -146,10 +158,10 @@ int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t
  * launch is as wide as this list; `out` may be NULL to count). */
 int thor_build_clpf_list(const uint8_t *host_flags, int nsb, uint32_t *out);
 /* Host helper: the frame's coded transform blocks (the residual work list the
- * parser knows from the cbp flags, dec/decode_block.c:90-120): one entry
- * block << 4 | component << 2 | tb-split quarter per coded TU, in any order.
- * `out` may be NULL to count; returns the count. */
-int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out);
+ * parser knows from the cbp flags, dec/decode_block.c:90-120), tb-split
+ * quarters in raster order, chroma of 8x8 CUs unsplit.  `out` may be NULL to
+ * count; returns the count. */
+int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, thor_tu_t *out);
 
 /* Stage control for parity debugging: 0 recon only, 1 +deblock, 2 +CLPF (default 2). */
 int thor_dec_set_stop_stage(thor_dec_t *d, int stage);

@@ -49,3 +49,32 @@ def test_build_intra_list_host_helper():
     out = np.zeros(5, np.uint32)
     n = lib.thor_build_intra_list(b.ctypes.data, 5, out.ctypes.data)
     assert n == 2 and out[:2].tolist() == [1, 3]
+
+
+def test_build_tu_list_host_helper():
+    """thor_build_tu_list: one 12-byte entry per coded TU (tb-split quarters in
+    raster order, 8x8 chroma unsplit, chroma qp mapped), SKIP never listed."""
+    import numpy as np
+    from thor_amd.decoder import TU_DTYPE
+    from thor_amd.trace import BLOCK_DTYPE
+
+    assert TU_DTYPE.itemsize == 12
+    lib = L.load()
+    b = np.zeros(3, BLOCK_DTYPE)
+    b[0] = 0
+    b["mode"] = [0, 2, 1]
+    b["coeff_mask"] = [7, 7, 1]
+    b["size"] = [64, 16, 8]
+    b["tb_split"] = [0, 1, 1]
+    b["ypos"], b["xpos"] = [0, 64, 80], [0, 32, 48]
+    b["qp"] = [40, 40, 20]
+    b["coeff_off"] = [[0, 0, 0], [100, 400, 500], [900, 0, 0]]
+    n = lib.thor_build_tu_list(b.ctypes.data, 3, None)
+    out = np.zeros(n, TU_DTYPE)
+    assert lib.thor_build_tu_list(b.ctypes.data, 3, out.ctypes.data) == n == 4 + 4 + 4 + 4
+    # CU 1 (16x16, tb split): luma quarters 8x8 with q = 8 -> offsets 100 + 64 t
+    assert out[:4]["coeff_off"].tolist() == [100, 164, 228, 292]
+    assert [(int(t["y"]), int(t["x"])) for t in out[:4]] == [(64, 32), (64, 40), (72, 32), (72, 40)]
+    assert out[4]["comp"] == 1 and out[4]["size"] == 4 and out[4]["qp"] == 36 and (out[4]["y"], out[4]["x"]) == (32, 16)
+    # CU 2 (8x8 intra, tb split): four 4x4 luma TUs, q = 4
+    assert out[12:]["coeff_off"].tolist() == [900, 916, 932, 948] and set(out[12:]["size"]) == {4}

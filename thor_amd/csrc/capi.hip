@@ -583,7 +583,7 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
 
 int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_t *blocks, int nblocks,
                    const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
-                   const uint32_t *tu_list, int n_tu) {
+                   const thor_tu_t *tu_list, int n_tu) {
   if (!d || !hdr) return THOR_ERR_ARG;
   thor_frame_in_t in = {blocks, nblocks, coeffs, clpf_flags, intra_list, n_intra, tu_list, n_tu, nullptr, -1};
   return thor_dec_frames(&d, 1, hdr, &in);
@@ -653,9 +653,8 @@ int thor_build_clpf_list(const uint8_t *host_flags, int nsb, uint32_t *out) {
   return n;
 }
 
-int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out) {
+int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, thor_tu_t *out) {
   if (nblocks < 0 || (nblocks > 0 && !host_blocks)) return THOR_ERR_ARG;
-  if (nblocks >= (1 << 27)) return THOR_ERR_ARG;
   int n = 0;
   for (int b = 0; b < nblocks; b++) {
     const thor_block_t &B = host_blocks[b];
@@ -664,8 +663,20 @@ int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, uint32_t *o
       if (!((B.coeff_mask >> c) & 1)) continue;
       // tb-split gives 4 quarters; chroma of an 8x8 CU is not split (dec/decode_block.c:449-450)
       const int split = B.tb_split && (c == 0 || B.size > 8);
-      for (int t = 0; t < (split ? 4 : 1); t++) {
-        if (out) out[n] = ((uint32_t)b << 4) | ((uint32_t)c << 2) | (uint32_t)t;
+      const int size = c ? B.size >> 1 : B.size, ntu = split ? size >> 1 : size;
+      const int nt = ntu == 64 ? 32 : ntu, q = nt < 16 ? nt : 16;
+      const int py = c ? B.ypos >> 1 : B.ypos, px = c ? B.xpos >> 1 : B.xpos;
+      for (int t = 0; t < (split ? 4 : 1); t++) {  // quarters in raster order, :101-102
+        if (out) {
+          thor_tu_t &T = out[n];
+          T.coeff_off = B.coeff_off[c] + (uint32_t)(t * q * q);
+          T.y = (uint16_t)(py + (t >> 1) * ntu);
+          T.x = (uint16_t)(px + (t & 1) * ntu);
+          T.size = (uint8_t)ntu;
+          T.comp = (uint8_t)c;
+          T.qp = (uint8_t)(c ? chroma_qp_host(B.qp) : B.qp);
+          T.rsv = 0;
+        }
         n++;
       }
     }

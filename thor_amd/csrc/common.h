@@ -37,7 +37,8 @@ struct FrameCtx {
   // (grid y / z = frame of the batch).
   const thor_block_t *blk;
   const int16_t *coeffs;
-  const uint32_t *tus, *ilist;
+  const thor_tu_t *tus;
+  const uint32_t *ilist;
   const uint8_t *clpf_flags;
   const uint32_t *clpf_list;  // flagged SBs (n_clpf >= 0) or every SB (n_clpf < 0)
   int n_clpf;

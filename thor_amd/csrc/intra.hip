@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) void k_frame_prep(const FrameBatch fb_) {
   if (b < f.nprep) prep_body(b, f);
   else if (b < f.nprep + f.nres) {
     const int w = threadIdx.x >> 6;
-    resid_tu(RL[w], (b - f.nprep) * 4 + w, f.blk, f.tus, f.ntus, f.coeffs, f.resid, f.W, f.H);
+    resid_tu(RL[w], (b - f.nprep) * 4 + w, f.tus, f.ntus, f.coeffs, f.resid, f.W, f.H);
   } else if (b == f.nprep + f.nres && f.nintra > 0) {
     intra_setup_body(f.blk, f.ilist, f.nintra, f.ctl, f.progress, f.rowstart, f.nsbrows);
   }

@@ -127,26 +127,16 @@ __device__ void tu_inverse(ResidLds &L, const int16_t *__restrict__ coef, int nt
 }
 
 // resid_tu: one wavefront per coded transform block, from the frame's TU list
-// (thor_build_tu_list: entry = block << 4 | component << 2 | tb-split quarter).
+// (thor_build_tu_list: coefficient offset, position, size, component, qp).
 // Every TU is independent, so the launch is as wide as the frame's coded
 // residual and a skip-dominated P frame launches only a handful of waves.
-__device__ __forceinline__ void resid_tu(ResidLds &L, int idx, const thor_block_t *__restrict__ blk,
-                                         const uint32_t *__restrict__ tus, int ntus, const int16_t *__restrict__ coeffs,
-                                         int16_t *__restrict__ resid, int W, int H) {
+__device__ __forceinline__ void resid_tu(ResidLds &L, int idx, const thor_tu_t *__restrict__ tus, int ntus,
+                                         const int16_t *__restrict__ coeffs, int16_t *__restrict__ resid, int W, int H) {
   if (idx >= ntus) return;
-  const uint32_t e = tus[idx];
-  const thor_block_t &B = blk[e >> 4];
-  const int c = (e >> 2) & 3, t = e & 3;
-  const int S = B.size, tb = B.tb_split != 0;
-  const int size = c ? S >> 1 : S;
-  const int tbc = c ? (tb && S > 8) : tb;  // chroma of an 8x8 CU is not split, dec/decode_block.c:449-450
-  const int ntu = tbc ? size >> 1 : size;
-  const int nt = ntu == 64 ? 32 : ntu, q = nt < 16 ? nt : 16;
-  const int qp = c ? chroma_qp(B.qp) : B.qp;
+  const thor_tu_t T = tus[idx];
+  const int c = T.comp, ntu = T.size;
   const int pw = c ? W >> 1 : W;
-  const int py = c ? B.ypos >> 1 : B.ypos, px = c ? B.xpos >> 1 : B.xpos;
   int16_t *plane = resid + (c == 0 ? 0 : (long long)W * H + (c == 2 ? (long long)(W >> 1) * (H >> 1) : 0));
-  const int oy = (t >> 1) * ntu, ox = (t & 1) * ntu;  // tb-split quarters in raster order, :101-102
   wave_lds_sync();
-  tu_inverse(L, coeffs + B.coeff_off[c] + t * q * q, ntu, qp, plane + (long long)(py + oy) * pw + px + ox, pw);
+  tu_inverse(L, coeffs + T.coeff_off, ntu, T.qp, plane + (long long)T.y * pw + T.x, pw);
 }

@@ -20,6 +20,10 @@ import numpy as np
 from . import lib as L
 from .trace import BLOCK_DTYPE
 
+# thor_tu_t (include/thor_amd.h): one coded transform block, 12 bytes
+TU_DTYPE = np.dtype([("coeff_off", "<u4"), ("y", "<u2"), ("x", "<u2"), ("size", "u1"), ("comp", "u1"), ("qp", "u1"),
+                     ("rsv", "u1")])
+
 
 @dataclass
 class DeviceFrame:
@@ -96,7 +100,7 @@ class GpuDecoder:
         ilist = np.zeros(max(n_intra, 1), np.uint32)
         self.lib.thor_build_intra_list(blocks.ctypes.data, len(blocks), ilist.ctypes.data)
         n_tu = self.lib.thor_build_tu_list(blocks.ctypes.data, len(blocks), None)
-        tlist = np.zeros(max(n_tu, 1), np.uint32)
+        tlist = np.zeros(max(n_tu, 1), TU_DTYPE)
         self.lib.thor_build_tu_list(blocks.ctypes.data, len(blocks), tlist.ctypes.data)
         n_clpf = self.lib.thor_build_clpf_list(flags.ctypes.data, len(flags), None) if flags.size else 0
         clist = np.zeros(max(n_clpf, 1), np.uint32)
@@ -105,7 +109,7 @@ class GpuDecoder:
         bb, cb, fb, ib = self._buf(blocks), self._buf(coeffs), self._buf(flags), self._buf(ilist)
         tb, lb = self._buf(tlist), self._buf(clist)
         hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
-        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + 4 * n_tu
+        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + TU_DTYPE.itemsize * n_tu
         return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, tb.ptr,
                            n_tu, lb.ptr, n_clpf, nbytes)
 
