@@ -36,88 +36,138 @@ __device__ __forceinline__ void filt4(int &p1, int &p0, int &q0, int &q1, int tc
   p1 = np1; p0 = np0; q0 = nq0; q1 = nq1;
 }
 
-// Vertical luma edges: one thread per (edge column j = 8e, 8-row group).
-__device__ __forceinline__ void k_deblock_luma_v_body(int t, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
-                                                        int qp) {
-  int ne = (W >> 3) - 1;
-  int g = t / ne, e = t - g * ne + 1;
-  if (g >= (H >> 3)) return;
-  int i = g * 8, j = e * 8;
-  int beta = beta_of(qp), tc = tc_of(qp);
-  // the two 4-row segments' edge decisions first (side info only): most edges of
-  // a skip-dominated frame are off and need no pixel reads at all
-  const int cs = W >> 2;
-  const int qa = (i >> 2) * cs + (j >> 2), qb = qa + cs;
-  const bool on0 = luma_edge_on(cell[qa - 1], cell[qa], j, true);
-  const bool on1 = luma_edge_on(cell[qb - 1], cell[qb], j, true);
-  if (!on0 && !on1) return;
-  uint8_t *base = Y + (long long)i * sy + j - 4;
-  uint32_t A[8], Bv[8];
-  for (int r = 0; r < 8; r++) {
-    A[r] = *(uint32_t *)(base + (long long)r * sy);
-    Bv[r] = *(uint32_t *)(base + (long long)r * sy + 4);
-  }
-  // p1 = A byte2, p0 = A byte3, q0 = B byte0, q1 = B byte1
-#define P1(r) ((int)((A[r] >> 16) & 255))
-#define P0(r) ((int)(A[r] >> 24))
-#define Q0(r) ((int)(Bv[r] & 255))
-#define Q1(r) ((int)((Bv[r] >> 8) & 255))
-  int d = abs(P1(2) - P0(2)) + abs(Q1(2) - Q0(2)) + abs(P1(5) - P0(5)) + abs(Q1(5) - Q0(5));
-  if (d >= beta) return;
-  for (int m = 0; m < 8; m += 4) {
-    if (!(m ? on1 : on0)) continue;
-    for (int r = m; r < m + 4; r++) {
-      int p1 = P1(r), p0 = P0(r), q0 = Q0(r), q1 = Q1(r);
-      filt4(p1, p0, q0, q1, tc);
-      A[r] = (A[r] & 0xffffu) | ((uint32_t)p1 << 16) | ((uint32_t)p0 << 24);
-      Bv[r] = (Bv[r] & 0xffff0000u) | (uint32_t)q0 | ((uint32_t)q1 << 8);
+// R luma edge segments per lane in three phases, so every phase's global
+// loads are in flight together: (1) the side-info decisions of all items,
+// (2) the pixels of the items that are on, (3) activity test, filter, store.
+template <int R>
+__device__ __forceinline__ void luma_v_items(int t0, int tstep, uint8_t *Y, int sy, int W, int H,
+                                             const uint16_t *cell, int qp) {
+  const int ne = (W >> 3) - 1, cs = W >> 2;
+  const int beta = beta_of(qp), tc = tc_of(qp);
+  int ii[R], jj[R];
+  uint16_t cq[R][4];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int t = t0 + r * tstep, g = t / ne, e = t - g * ne + 1;
+    ii[r] = g * 8;
+    jj[r] = e * 8;
+    cq[r][0] = cq[r][1] = cq[r][2] = cq[r][3] = 0;
+    if (g < (H >> 3)) {
+      const int qa = (ii[r] >> 2) * cs + (jj[r] >> 2);
+      cq[r][0] = cell[qa - 1];
+      cq[r][1] = cell[qa];
+      cq[r][2] = cell[qa + cs - 1];
+      cq[r][3] = cell[qa + cs];
     }
   }
+  bool on0[R], on1[R];
+  uint32_t A[R][8], Bv[R][8];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    on0[r] = cq[r][1] && luma_edge_on(cq[r][0], cq[r][1], jj[r], true);  // cq 0: past the frame
+    on1[r] = cq[r][3] && luma_edge_on(cq[r][2], cq[r][3], jj[r], true);
+    if (on0[r] || on1[r]) {
+      const uint8_t *base = Y + (long long)ii[r] * sy + jj[r] - 4;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        A[r][k] = *(const uint32_t *)(base + (long long)k * sy);
+        Bv[r][k] = *(const uint32_t *)(base + (long long)k * sy + 4);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (!(on0[r] || on1[r])) continue;
+    // p1 = A byte2, p0 = A byte3, q0 = B byte0, q1 = B byte1
+#define P1(k) ((int)((A[r][k] >> 16) & 255))
+#define P0(k) ((int)(A[r][k] >> 24))
+#define Q0(k) ((int)(Bv[r][k] & 255))
+#define Q1(k) ((int)((Bv[r][k] >> 8) & 255))
+    const int d = abs(P1(2) - P0(2)) + abs(Q1(2) - Q0(2)) + abs(P1(5) - P0(5)) + abs(Q1(5) - Q0(5));
+    if (d >= beta) continue;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (!(k < 4 ? on0[r] : on1[r])) continue;
+      int p1 = P1(k), p0 = P0(k), q0 = Q0(k), q1 = Q1(k);
+      filt4(p1, p0, q0, q1, tc);
+      A[r][k] = (A[r][k] & 0xffffu) | ((uint32_t)p1 << 16) | ((uint32_t)p0 << 24);
+      Bv[r][k] = (Bv[r][k] & 0xffff0000u) | (uint32_t)q0 | ((uint32_t)q1 << 8);
+    }
 #undef P1
 #undef P0
 #undef Q0
 #undef Q1
-  for (int r = 0; r < 8; r++) {
-    *(uint32_t *)(base + (long long)r * sy) = A[r];
-    *(uint32_t *)(base + (long long)r * sy + 4) = Bv[r];
+    uint8_t *base = Y + (long long)ii[r] * sy + jj[r] - 4;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      *(uint32_t *)(base + (long long)k * sy) = A[r][k];
+      *(uint32_t *)(base + (long long)k * sy + 4) = Bv[r][k];
+    }
   }
 }
 
-// Horizontal luma edges: one thread per (edge row i = 8k >= 8, 8-column group).
-__device__ __forceinline__ void k_deblock_luma_h_body(int t, uint8_t *Y, int sy, int W, int H, const uint16_t *cell,
-                                                        int qp) {
-  int ng = W >> 3;
-  int k = t / ng, gcol = t - k * ng;
-  int i = (k + 1) * 8, j = gcol * 8;
-  if (i >= H) return;
-  int beta = beta_of(qp), tc = tc_of(qp);
-  const int cs = W >> 2;
-  const int qa = (i >> 2) * cs + (j >> 2);
-  const bool on0 = luma_edge_on(cell[qa - cs], cell[qa], i, false);
-  const bool on1 = luma_edge_on(cell[qa + 1 - cs], cell[qa + 1], i, false);
-  if (!on0 && !on1) return;
-  uint8_t *base = Y + (long long)(i - 2) * sy + j;
-  uint2 rows[4];  // rows i-2 .. i+1 (p1, p0, q0, q1)
-  for (int r = 0; r < 4; r++) rows[r] = *(uint2 *)(base + (long long)r * sy);
-  auto px = [&](int r, int c) -> int { return (int)(((c < 4 ? rows[r].x : rows[r].y) >> (8 * (c & 3))) & 255); };
-  int d = abs(px(0, 2) - px(1, 2)) + abs(px(3, 2) - px(2, 2)) + abs(px(0, 5) - px(1, 5)) + abs(px(3, 5) - px(2, 5));
-  if (d >= beta) return;
-  uint32_t out[4][2] = {{rows[0].x, rows[0].y}, {rows[1].x, rows[1].y}, {rows[2].x, rows[2].y}, {rows[3].x, rows[3].y}};
-  for (int n = 0; n < 8; n += 4) {
-    if (!(n ? on1 : on0)) continue;
-    int w = n >> 2;
-    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-    for (int c = 0; c < 4; c++) {
-      int p1 = px(0, n + c), p0 = px(1, n + c), q0 = px(2, n + c), q1 = px(3, n + c);
-      filt4(p1, p0, q0, q1, tc);
-      o0 |= (uint32_t)p1 << (8 * c);
-      o1 |= (uint32_t)p0 << (8 * c);
-      o2 |= (uint32_t)q0 << (8 * c);
-      o3 |= (uint32_t)q1 << (8 * c);
+template <int R>
+__device__ __forceinline__ void luma_h_items(int t0, int tstep, uint8_t *Y, int sy, int W, int H,
+                                             const uint16_t *cell, int qp) {
+  const int ng = W >> 3, cs = W >> 2;
+  const int beta = beta_of(qp), tc = tc_of(qp);
+  int ii[R], jj[R];
+  uint16_t cq[R][4];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int t = t0 + r * tstep, k = t / ng, gcol = t - k * ng;
+    ii[r] = (k + 1) * 8;
+    jj[r] = gcol * 8;
+    cq[r][0] = cq[r][1] = cq[r][2] = cq[r][3] = 0;
+    if (ii[r] < H) {
+      const int qa = (ii[r] >> 2) * cs + (jj[r] >> 2);
+      cq[r][0] = cell[qa - cs];
+      cq[r][1] = cell[qa];
+      cq[r][2] = cell[qa + 1 - cs];
+      cq[r][3] = cell[qa + 1];
     }
-    out[0][w] = o0; out[1][w] = o1; out[2][w] = o2; out[3][w] = o3;
   }
-  for (int r = 0; r < 4; r++) *(uint2 *)(base + (long long)r * sy) = make_uint2(out[r][0], out[r][1]);
+  bool on0[R], on1[R];
+  uint2 rows[R][4];  // rows i-2 .. i+1 (p1, p0, q0, q1)
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    on0[r] = cq[r][1] && luma_edge_on(cq[r][0], cq[r][1], ii[r], false);
+    on1[r] = cq[r][3] && luma_edge_on(cq[r][2], cq[r][3], ii[r], false);
+    if (on0[r] || on1[r]) {
+      const uint8_t *base = Y + (long long)(ii[r] - 2) * sy + jj[r];
+#pragma unroll
+      for (int k = 0; k < 4; k++) rows[r][k] = *(const uint2 *)(base + (long long)k * sy);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (!(on0[r] || on1[r])) continue;
+    auto px = [&](int k, int c) -> int { return (int)(((c < 4 ? rows[r][k].x : rows[r][k].y) >> (8 * (c & 3))) & 255); };
+    const int d =
+        abs(px(0, 2) - px(1, 2)) + abs(px(3, 2) - px(2, 2)) + abs(px(0, 5) - px(1, 5)) + abs(px(3, 5) - px(2, 5));
+    if (d >= beta) continue;
+    uint32_t out[4][2] = {{rows[r][0].x, rows[r][0].y}, {rows[r][1].x, rows[r][1].y}, {rows[r][2].x, rows[r][2].y},
+                          {rows[r][3].x, rows[r][3].y}};
+#pragma unroll
+    for (int n = 0; n < 8; n += 4) {
+      if (!(n ? on1[r] : on0[r])) continue;
+      const int w = n >> 2;
+      uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        int p1 = px(0, n + c), p0 = px(1, n + c), q0 = px(2, n + c), q1 = px(3, n + c);
+        filt4(p1, p0, q0, q1, tc);
+        o0 |= (uint32_t)p1 << (8 * c);
+        o1 |= (uint32_t)p0 << (8 * c);
+        o2 |= (uint32_t)q0 << (8 * c);
+        o3 |= (uint32_t)q1 << (8 * c);
+      }
+      out[0][w] = o0; out[1][w] = o1; out[2][w] = o2; out[3][w] = o3;
+    }
+    uint8_t *base = Y + (long long)(ii[r] - 2) * sy + jj[r];
+#pragma unroll
+    for (int k = 0; k < 4; k++) *(uint2 *)(base + (long long)k * sy) = make_uint2(out[k][0], out[k][1]);
+  }
 }
 
 // Chroma (deblock_frame_uv): intra-only edges, p0/q0 modified.  One thread
@@ -230,8 +280,7 @@ __global__ __launch_bounds__(256) void k_deblock_v(const FrameBatch fb_, int nbl
       k_deblock_chroma_v_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
     return;
   }
-  for (int r = 0; r < DB_ITEMS; r++)
-    k_deblock_luma_v_body(b * 256 + (int)threadIdx.x + r * nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+  luma_v_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
 }
 __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl, int clist) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
@@ -248,8 +297,7 @@ __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl
       k_deblock_chroma_h_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
     return;
   }
-  for (int r = 0; r < DB_ITEMS; r++)
-    k_deblock_luma_h_body(b * 256 + (int)threadIdx.x + r * nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+  luma_h_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
 }
 
 // One flagged SB per workgroup.  The SB's pixels and its 64 8x8-block side
