@@ -130,7 +130,18 @@ __device__ __forceinline__ void luma_h4(uint32_t d0, uint32_t d1, uint32_t d2, u
   }
 }
 
-__device__ __forceinline__ uint32_t mc_pack(int v, int j) { return put_byte(clip255(v >> 12), j); }  // v includes MC_RND
+// clip255 of four ints packed as bytes a | b << 8 | c << 16 | d << 24:
+// saturate to int16 pairs (v_cvt_pk_i16_i32), then to u8 (v_sat_pk_u8_i16),
+// then one byte permute -- 5 instructions instead of 4 x (clamp, shift, or).
+__device__ __forceinline__ uint32_t sat_u8x2(int a, int b) {
+  const s16x2 p = __builtin_amdgcn_cvt_pk_i16(a, b);
+  uint32_t r;
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(p));
+  return r;  // bytes 0, 1 (the upper half is not relied upon)
+}
+__device__ __forceinline__ uint32_t pack4_u8(int a, int b, int c, int d) {
+  return __builtin_amdgcn_perm(sat_u8x2(c, d), sat_u8x2(a, b), 0x05040100u);
+}
 __device__ __forceinline__ uint32_t avg_bytes(uint32_t a, uint32_t b) {  // (p0 + p1) >> 1 per byte
   return (a & b) + (((a ^ b) >> 1) & 0x7f7f7f7fu);
 }
@@ -211,14 +222,15 @@ __device__ __forceinline__ void luma_rows(const Src &src, uint32_t sh, int tw0, 
 #pragma unroll
   for (int i = R0; i < R0 + N; i++) {
     hrow(i + 3);
-    uint32_t o = 0;
+    int v[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      int acc = dot2(pa[(i - 2 + 6) % 6][j], v01, MC_RND);
-      acc = dot2(pa[(i + 6) % 6][j], v23, acc);
-      acc = dot2(pa[(i + 2 + 6) % 6][j], v45, acc);
-      o |= mc_pack(acc, j);
+      int a = dot2(pa[(i - 2 + 6) % 6][j], v01, MC_RND);
+      a = dot2(pa[(i + 6) % 6][j], v23, a);
+      a = dot2(pa[(i + 2 + 6) % 6][j], v45, a);
+      v[j] = a >> 12;
     }
+    const uint32_t o = pack4_u8(v[0], v[1], v[2], v[3]);
     out[i] = acc ? avg_bytes(out[i], o) : o;  // bi-pred: truncating average with pass 0
   }
 }
@@ -257,15 +269,16 @@ __device__ __forceinline__ void luma_rows_ctr(const Src &src, uint32_t sh, uint3
 #pragma unroll
   for (int i = R0; i < R0 + N; i++) {
     if (i > R0) hrow(i + 2);
-    uint32_t o = 0;
+    int v[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      int acc = dot2(q[(i - 1 + 6) % 6][j], 0x00010000, 2048 + 8);
-      acc = dot2(q[(i + 6) % 6][j], 0x00010001, acc);
-      acc = dot2(q[(i + 1 + 6) % 6][j], 0x00010001, acc);
-      acc = dot2(q[(i + 2 + 6) % 6][j], 0x00010000, acc);
-      o |= put_byte(clip255(acc >> 4), j);
+      int a = dot2(q[(i - 1 + 6) % 6][j], 0x00010000, 2048 + 8);
+      a = dot2(q[(i + 6) % 6][j], 0x00010001, a);
+      a = dot2(q[(i + 1 + 6) % 6][j], 0x00010001, a);
+      a = dot2(q[(i + 2 + 6) % 6][j], 0x00010000, a);
+      v[j] = a >> 4;
     }
+    const uint32_t o = pack4_u8(v[0], v[1], v[2], v[3]);
     out[i] = acc ? avg_bytes(out[i], o) : o;  // bi-pred: truncating average with pass 0
   }
 }
@@ -312,15 +325,13 @@ __device__ __forceinline__ void chroma_rows(const Src &src, uint32_t sh, int tw,
 #pragma unroll
   for (int i = R0; i < R0 + N; i++) {
     hrow(i + 2);
-    uint32_t ou = 0, ov = 0;
+    int au[2], av[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
-      const int au = dot2(pu[(i + 1) % 4][j], v23, dot2(pu[(i + 3) % 4][j], v01, MC_RND));
-      const int av = dot2(pv[(i + 1) % 4][j], v23, dot2(pv[(i + 3) % 4][j], v01, MC_RND));
-      ou |= mc_pack(au, j);
-      ov |= mc_pack(av, j);
+      au[j] = dot2(pu[(i + 1) % 4][j], v23, dot2(pu[(i + 3) % 4][j], v01, MC_RND)) >> 12;
+      av[j] = dot2(pv[(i + 1) % 4][j], v23, dot2(pv[(i + 3) % 4][j], v01, MC_RND)) >> 12;
     }
-    const uint32_t uv = ou | (ov << 16);  // U in the low half, V in the high half
+    const uint32_t uv = pack4_u8(au[0], au[1], av[0], av[1]);  // U in the low half, V in the high half
     out[i] = acc ? avg_bytes(out[i], uv) : uv;
   }
 }
@@ -455,8 +466,34 @@ __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bi
   const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
   const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
   const LdsChroma c{w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3)};
-  filter_items(m0, m1, l, l, (uint32_t)(lwb & 3), (uint32_t)(lwb & 3), c, c, (uint32_t)(cwb & 3), (uint32_t)(cwb & 3),
-               K, K, true, bipred, ty, tc, acc);
+  // The key is uniform, so every lane filters its whole strip (8 luma, 4
+  // chroma rows) with ONE instantiation per filter shape, and each segment
+  // keeps the result only where it matches: a small code footprint for the
+  // common path (k_recon's code otherwise overflows the instruction cache).
+  uint32_t ny[8], nc[4];
+  if (K.fx == 2 && K.fy == 2) {
+    luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ny, false);
+  } else {
+    int v01, v23, v45;
+    tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45);
+    luma_rows<0, 8>(l, (uint32_t)(lwb & 3), g_taps.luma[bipred][K.fx][0], g_taps.luma[bipred][K.fx][1], v01, v23, v45,
+                    ny, false);
+  }
+  {
+    const int cvt = g_taps.chroma[K.cfy];
+    chroma_rows<0, 4>(c, (uint32_t)(cwb & 3), g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
+                      (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), nc, false);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const bool m = i < 4 ? m0 : m1;
+    ty[i] = m ? (acc ? avg_bytes(ty[i], ny[i]) : ny[i]) : ty[i];  // bi-pred: truncating average with pass 0
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const bool m = i < 2 ? m0 : m1;
+    tc[i] = m ? (acc ? avg_bytes(tc[i], nc[i]) : nc[i]) : tc[i];
+  }
   it.pend &= ~((m0 ? 1u : 0u) | (m1 ? 2u : 0u));
 }
 
