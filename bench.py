@@ -12,7 +12,7 @@ intra list, CLPF flags) is resident in HBM before timing starts; bit parsing
 is CPU work outside the hot path.  The decoded frames are checked bit-exact
 against the reference decoder's md5s (every context) after warmup.
 
-Per GPU, --streams K (default 15) independent decoder contexts each decode
+Per GPU, --streams K (default 24: 3 groups of 8, THOR_MAX_BATCH) independent decoder contexts each decode
 their own copy of the stream on their own HIP stream, interleaved frame by
 frame (a server decoding K streams): value = K x stream pixels / time.  The
 single-stream latency of one pass is reported next to it
@@ -192,7 +192,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=15, help="independent decoder contexts per GPU")
+    ap.add_argument("--streams", type=int, default=24, help="independent decoder contexts per GPU")
     ap.add_argument("--groups", type=int, default=3,
                     help="batches per frame slot (contexts of a group share one launch per stage)")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",

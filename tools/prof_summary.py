@@ -98,7 +98,7 @@ def main():
         pw = [v for i, v in enumerate(wr) if i % 8 != 0]
         traffic["recon_hbm_bytes_per_p_launch"] = round((sum(pf) * 2 + sum(pw)) * 1024 / len(pf))
         traffic["recon_p_launches"] = len(pf)
-        traffic["recon_note"] = "bench.py --streams 4 --groups 1: one k_recon launch = 5 frames"
+        traffic["recon_note"] = "bench.py --streams 8 --groups 1: one k_recon launch = 8 frames (THOR_MAX_BATCH)"
     json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
     # the GPU box does not receive profiles/ (.gpurunignore): bench.py reads this copy
     json.dump(traffic, open(os.path.join(root, "tools", "traffic_latest.json"), "w"), indent=1)
