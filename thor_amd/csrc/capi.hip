@@ -385,6 +385,16 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
   return THOR_OK;
 }
 
+// Diagnostic: extra dynamic LDS per k_recon workgroup (bytes) to cap its
+// occupancy (THOR_RECON_LDS_PAD; 0 in the product path).
+static int recon_lds_pad() {
+  static int v = [] {
+    const char *e = getenv("THOR_RECON_LDS_PAD");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Phase A: side info, residuals, intra setup, inter reconstruction (the SB
 // rows of each context's band).
 static int batch_phase_a(thor_dec *lead, const Batch &b) {
@@ -399,7 +409,7 @@ static int batch_phase_a(thor_dec *lead, const Batch &b) {
   }
   {
     StageMark m(lead, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
-    k_recon<<<dim3(8 * ((2 * nsb + 7) / 8), n), 64, 0, st>>>(b.fb, lead->dbg_recon);
+    k_recon<<<dim3(8 * ((2 * nsb + 7) / 8), n), 64, recon_lds_pad(), st>>>(b.fb, lead->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   return THOR_OK;

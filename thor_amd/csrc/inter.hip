@@ -567,6 +567,10 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
 
   // reference lookup table (packed by the host)
   if (lane < 32) *(int *)&L.lut[4 * lane] = f.slot_lut[lane];
+  if (stamp) {  // debug: the frame context's scalar loads have returned
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    STAMP(1);
+  }
 
   // ---- P0: lane = cell row cr of 8x8 unit uu of the half: the two cells' MC
   // words that k_frame_prep resolved (quarter MV with the `sign` negation,

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: k_recon phase timing from in-kernel s_memrealtime stamps (100 MHz)
-on a stream's P frames.  Stamps: 0 start, 1 init, 2 P0 (MC params), 4 first
+on a stream's P frames.  Stamps: 0 start, 1 frame context loaded, 2 P0 (MC params), 4 first
 window staged, 3 prediction done, 5 end; 7 = HW_ID | XCC_ID << 32."""
 import ctypes as C, os, sys
 import numpy as np
