@@ -154,6 +154,48 @@ def encoder_leg(torch, lib, reps: int = 10):
             "note": "RD candidate evaluation throughput of the encoder TU chain; not part of `value`"}
 
 
+def pyramid_leg(torch, lib, reps: int = 50):
+    """Temporal-interpolation luma pyramid (thor_scale_pyramid, the chain of
+    scale_frame_down2x2_simd calls of common/temporal_interp.c:1011-1019) on
+    one 4K reference frame: 3 levels + their 32-px padding.  Not part of
+    `value`.  Algorithmic bytes: level 0 read once (W*H) + every level byte
+    written once, padding included."""
+    W, H, n = 3840, 2160, 3
+    pad = 32
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = torch.randint(0, 256, (H, W), dtype=torch.uint8, device=dev)
+    bufs, ptrs, strides, wr = [], [], [], 0
+    for l in range(1, n + 1):
+        wl, hl = W >> l, H >> l
+        s = (wl + 2 * pad + 15) & ~15
+        b = torch.empty((hl + 2 * pad) * s, dtype=torch.uint8, device=dev)
+        bufs.append(b)
+        ptrs.append(b.data_ptr() + pad * s + pad)
+        strides.append(s)
+        wr += (hl + 2 * pad) * (wl + 2 * pad)
+    parr = (C.c_void_p * 3)(*ptrs)
+    sarr = (C.c_int * 3)(*strides)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        assert lib.thor_scale_pyramid(src.data_ptr(), W, W, H, C.cast(parr, C.c_void_p),
+                                      C.cast(sarr, C.c_void_p), n, st) == 0
+
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    alg = W * H + wr
+    return {"workload": "4K luma reference frame -> 3 down-sampled, padded levels (k_down_pyramid + k_pad_pyramid)",
+            "us_per_frame": round(ms * 1e3, 2), "alg_bytes": int(alg), "achieved_gb_s": round(alg / ms / 1e6, 1),
+            "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
+
+
 def cpu_baseline(meta, gold, budget_s: float = 20.0):
     """Reference decoder (oracle/_ref/Thordec, SIMD build, 1 thread) on the
     same .bit, repeated up to ~budget_s; falls back to the oracle port."""
@@ -401,6 +443,7 @@ def main():
         }
         if world == 1:
             out["encoder_tu_chain"] = encoder_leg(torch, lib)
+            out["temporal_pyramid"] = pyramid_leg(torch, lib)
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(meta, gold)
         print(json.dumps(out), flush=True)

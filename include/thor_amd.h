@@ -224,6 +224,28 @@ int thor_enc_tu_batch(const thor_enc_tu_t *tus, int n, const uint8_t *orig, cons
 int thor_enc_cost_batch(const uint32_t *ssd, const int32_t *tu_first, const int32_t *tu_count, const int32_t *nbits,
                         double lambda, uint32_t *cost, int ncu, void *stream);
 
+/* ---- temporal interpolation: luma down-sampling pyramid ----------------- */
+
+/* Number of down-sampled levels interpolate_frames builds for a width x height
+ * reference: max_levels - 1 with max_levels = min(MAX_LEVELS = 4,
+ * (int)(log10(min(w, h)) / log10(2) - 4)) (common/temporal_interp.c:20,977). */
+int thor_pyramid_levels(int width, int height);
+
+/* Replaces the chain of scale_frame_down2x2_simd calls on one reference frame
+ * (common/temporal_interp.c:1011-1019, kernel :187-245): level l (1-based,
+ * l <= nlevels <= 3) is (width >> l) x (height >> l) luma, each pixel
+ * (avg(v0,v1) + avg(h0,h1)) >> 1 of the 2x2 block below it, then padded by
+ * edge replication over a 32-pixel margin (pad_yuv_frame,
+ * common/common_frame.c:405-462).  Chroma is not produced: USE_CHROMA is 0
+ * (temporal_interp.c:19), so the SIMD path leaves level chroma unwritten and
+ * nothing reads it.  DEVICE pointers: `src` is level 0's (0,0) (8-byte
+ * aligned, stride % 8 == 0); levels[l-1] is level l's (0,0) in a
+ * create_yuv_frame(.., 32, 32, ..) plane (16-byte aligned, stride % 16 == 0,
+ * stride >= w + 64, 32 rows above and below).  One launch computes every
+ * level, a second pads them.  Enqueued on `stream`. */
+int thor_scale_pyramid(const uint8_t *src, int src_stride, int width, int height, uint8_t *const *levels,
+                       const int *level_strides, int nlevels, void *stream);
+
 /* ---- device memory helpers (so the C-ABI is usable without torch) ------ */
 void *thor_dev_alloc(size_t bytes);
 int thor_dev_free(void *p);

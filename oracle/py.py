@@ -71,6 +71,8 @@ def load(build: bool = True):
                                      C.POINTER(OrFrame), i, P, i, P, P, i]
     _lib.or_decode_frame.restype = i
     _lib.or_pad_frame.argtypes = [C.POINTER(OrFrame), i, i, i, i]
+    _lib.or_scale_down2x2.argtypes = [P, i, P, i, i, i]
+    _lib.or_pad_plane.argtypes = [P, i, i, i, i]
     return _lib
 
 

@@ -897,3 +897,24 @@ int or_encode_tu(const uint8_t *orig, int os, const uint8_t *pred, int ps, uint8
   *ssd = or_ssd(orig, out, os, size, size, size);
   return cbp;
 }
+
+/* scale_frame_down2x2 luma loop (common/temporal_interp.c:161-168; the SIMD
+ * variant :196-210 computes the same bytes) on one plane, no padding. */
+void or_scale_down2x2(const uint8_t *in, int si, uint8_t *out, int so, int wo, int ho) {
+  for (int i = 0; i < ho; i++)
+    for (int j = 0; j < wo; j++) {
+      const int a = (in[(2 * i) * si + 2 * j] + in[(2 * i + 1) * si + 2 * j] + 1) >> 1;
+      const int b = (in[(2 * i) * si + 2 * j + 1] + in[(2 * i + 1) * si + 2 * j + 1] + 1) >> 1;
+      out[i * so + j] = (uint8_t)((a + b) >> 1);
+    }
+}
+
+/* pad_yuv_frame's luma part (common/common_frame.c:414-430) on one plane */
+void or_pad_plane(uint8_t *p, int s, int w, int h, int pad) {
+  for (int i = 0; i < h; i++) {
+    memset(p + i * s - pad, p[i * s], pad);
+    memset(p + i * s + w, p[i * s + w - 1], pad);
+  }
+  for (int i = -pad; i < 0; i++) memcpy(p + i * s - pad, p - pad, w + 2 * pad);
+  for (int i = h; i < h + pad; i++) memcpy(p + i * s - pad, p + (h - 1) * s - pad, w + 2 * pad);
+}

@@ -57,4 +57,9 @@ int or_decode_frame(const thor_seq_t *seq, const thor_frame_hdr_t *hdr, or_frame
                     const uint8_t *clpf_flags, int stop_stage);
 /* pad_yuv_frame (common/common_frame.c:405-462), pad 96 luma / 48 chroma */
 void or_pad_frame(or_frame_t *f, int width, int height, int pad_y, int pad_c);
+/* temporal interpolation pyramid: scale_frame_down2x2 luma (common/temporal_interp.c:151-168)
+ * and pad_yuv_frame's luma part (common/common_frame.c:414-430) */
+void or_scale_down2x2(const uint8_t *in, int si, uint8_t *out, int so, int wo, int ho);
+void or_pad_plane(uint8_t *p, int s, int w, int h, int pad);
+
 #endif

@@ -101,6 +101,10 @@ def load(path: str = LIB_PATH):
     L.thor_enc_tu_batch.restype = i
     L.thor_enc_cost_batch.argtypes = [P, P, P, P, C.c_double, P, i, P]
     L.thor_enc_cost_batch.restype = i
+    L.thor_pyramid_levels.argtypes = [i, i]
+    L.thor_pyramid_levels.restype = i
+    L.thor_scale_pyramid.argtypes = [P, i, i, i, P, P, i, P]
+    L.thor_scale_pyramid.restype = i
     # the reference's SIMD kernel surface (include/thor_kernels.h)
     u8p = P
     L.transform_simd.argtypes = [P, P, i, i]
