@@ -238,7 +238,8 @@ int thor_pyramid_levels(int width, int height);
  * edge replication over a 32-pixel margin (pad_yuv_frame,
  * common/common_frame.c:405-462).  Chroma is not produced: USE_CHROMA is 0
  * (temporal_interp.c:19), so the SIMD path leaves level chroma unwritten and
- * nothing reads it.  DEVICE pointers: `src` is level 0's (0,0) (8-byte
+ * nothing reads it.  `levels` / `level_strides` are HOST arrays of DEVICE
+ * pointers / strides; `src` is level 0's (0,0) (8-byte
  * aligned, stride % 8 == 0); levels[l-1] is level l's (0,0) in a
  * create_yuv_frame(.., 32, 32, ..) plane (16-byte aligned, stride % 16 == 0,
  * stride >= w + 64, 32 rows above and below).  One launch computes every
