@@ -196,6 +196,48 @@ def pyramid_leg(torch, lib, reps: int = 50):
             "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
 
 
+def interp_leg(torch, lib, reps: int = 50):
+    """Temporal-interpolation compensation (thor_interp_comp: interpolate_comp
+    + mot_comp_avg, common/temporal_interp.c:387-441,920-944) of one 4K frame,
+    Y + U + V, from a random 8x8-block MV field (±50 px).  Not part of
+    `value`.  Algorithmic bytes: two reference reads + one write per pixel
+    + the MV field (8 B per block, read by the luma and both chroma passes)."""
+    W, H, pf, pfc = 3840, 2160, 96, 48
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bw, bh = 2 * ((W + 15) // 16), 2 * ((H + 15) // 16)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    mv = torch.randint(-400, 401, (2, bh * bw, 2), generator=g, dtype=torch.int16).to(dev)
+    planes = []
+    for (pw, ph, pad) in ((W, H, pf), (W // 2, H // 2, pfc), (W // 2, H // 2, pfc)):
+        s = (pw + 2 * pad + 15) & ~15
+        r0 = torch.randint(0, 256, ((ph + 2 * pad) * s,), dtype=torch.uint8, device=dev)
+        r1 = torch.randint(0, 256, ((ph + 2 * pad) * s,), dtype=torch.uint8, device=dev)
+        o = torch.empty((ph + 2 * pad) * s, dtype=torch.uint8, device=dev)
+        org = pad * s + pad
+        planes.append((r0.data_ptr() + org, r1.data_ptr() + org, o.data_ptr() + org, s, pw == W, (r0, r1, o)))
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        for p0, p1, po, s, luma, _ in planes:
+            bs, pad, wP, hP = (8, 4, W + 4, H + 4) if luma else (4, 2, (W + 4) // 2, (H + 4) // 2)
+            assert lib.thor_interp_comp(p0, s, p1, s, po, s, mv[0].data_ptr(), mv[1].data_ptr(), bw, bh, bs, wP,
+                                        hP, pad, 0 if luma else 1, 3, 1, st) == 0
+
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    alg = 3 * W * H * 1.5 + 3 * 8 * bw * bh
+    return {"workload": "4K frame (Y, U, V: 3 launches of k_interp_comp), 8x8 luma blocks, random MVs",
+            "us_per_frame": round(ms * 1e3, 2), "alg_bytes": int(alg), "achieved_gb_s": round(alg / ms / 1e6, 1),
+            "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
+
+
 def cpu_baseline(meta, gold, budget_s: float = 20.0):
     """Reference decoder (oracle/_ref/Thordec, SIMD build, 1 thread) on the
     same .bit, repeated up to ~budget_s; falls back to the oracle port."""
@@ -444,6 +486,7 @@ def main():
         if world == 1:
             out["encoder_tu_chain"] = encoder_leg(torch, lib)
             out["temporal_pyramid"] = pyramid_leg(torch, lib)
+            out["temporal_interp_comp"] = interp_leg(torch, lib)
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(meta, gold)
         print(json.dumps(out), flush=True)

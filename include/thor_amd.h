@@ -247,6 +247,21 @@ int thor_pyramid_levels(int width, int height);
 int thor_scale_pyramid(const uint8_t *src, int src_stride, int width, int height, uint8_t *const *levels,
                        const int *level_strides, int nlevels, void *stream);
 
+/* Replaces interpolate_comp (common/temporal_interp.c:920-944) on one plane:
+ * for each of the bw x bh blocks of bs x bs pixels, mot_comp_avg (:387-441)
+ * with the block's vectors (1/8 pel, rounded to integer: ACC_BITS 3) --
+ * (ref0 + ref1 + 1) / 2 when both displaced blocks lie inside
+ * [-pad, wP) x [-pad, hP), else a copy of the one that does (ref1 first;
+ * ref0 rows read with s1, as :420-422 does), else the clamped average.
+ * chroma != 0: mv1 is halved and mv0 = scale_mv(mv1, -wt1, wt0) (:934-938),
+ * the mv0 array is then not read.  mv0/mv1: bw*bh (x, y) int16 pairs
+ * (mv_data->mv[0], mv[1]).  p0/p1 are the (0,0) of pic[0]/pic[1] (already
+ * swapped by mv_data->reversed, :950-951).  All DEVICE pointers; enqueued on
+ * `stream`. */
+int thor_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
+                     const int16_t *mv1, int bw, int bh, int bs, int wP, int hP, int pad, int chroma, int wt0, int wt1,
+                     void *stream);
+
 /* ---- device memory helpers (so the C-ABI is usable without torch) ------ */
 void *thor_dev_alloc(size_t bytes);
 int thor_dev_free(void *p);

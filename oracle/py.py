@@ -73,6 +73,7 @@ def load(build: bool = True):
     _lib.or_pad_frame.argtypes = [C.POINTER(OrFrame), i, i, i, i]
     _lib.or_scale_down2x2.argtypes = [P, i, P, i, i, i]
     _lib.or_pad_plane.argtypes = [P, i, i, i, i]
+    _lib.or_interp_comp.argtypes = [P, i, P, i, P, i, P, P] + [i] * 9
     return _lib
 
 

@@ -918,3 +918,57 @@ void or_pad_plane(uint8_t *p, int s, int w, int h, int pad) {
   for (int i = -pad; i < 0; i++) memcpy(p + i * s - pad, p - pad, w + 2 * pad);
   for (int i = h; i < h + pad; i++) memcpy(p + i * s - pad, p + (h - 1) * s - pad, w + 2 * pad);
 }
+
+/* scale_val / scale_mv (common/temporal_interp.c:66-91) */
+static int or_scale_val(int v, int numer, int denom) {
+  if (denom == 0) return 0;
+  int prod = v * numer;
+  if (denom < 0) {
+    denom = -denom;
+    prod = -prod;
+  }
+  return prod >= 0 ? (prod + denom / 2) / denom : -((-prod + denom / 2) / denom);
+}
+
+/* interpolate_comp (common/temporal_interp.c:920-944) with mot_comp_avg
+ * (:387-441) inlined; mv arrays are (x, y) int16 pairs, 1/8 pel. */
+void or_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
+                    const int16_t *mv1, int bw, int bh, int bs, int wP, int hP, int pad, int chroma, int wt0, int wt1) {
+  for (int yp = 0; yp < bh; yp++)
+    for (int xp = 0; xp < bw; xp++) {
+      const int b = yp * bw + xp;
+      int16_t m0x = mv0[2 * b], m0y = mv0[2 * b + 1], m1x = mv1[2 * b], m1y = mv1[2 * b + 1];
+      if (chroma) {
+        m1x >>= 1;
+        m1y >>= 1;
+        if (-wt1 == wt0) {
+          m0x = m1x;
+          m0y = m1y;
+        } else if (-wt1 == -wt0) {
+          m0x = (int16_t)-m1x;
+          m0y = (int16_t)-m1y;
+        } else {
+          m0x = (int16_t)or_scale_val(m1x, -wt1, wt0);
+          m0y = (int16_t)or_scale_val(m1y, -wt1, wt0);
+        }
+      }
+      const int xs0 = xp * bs + ((m0x + 4) >> 3), xs1 = xp * bs + ((m1x + 4) >> 3);
+      const int ys0 = yp * bs + ((m0y + 4) >> 3), ys1 = yp * bs + ((m1y + 4) >> 3);
+      const int in0 = xs0 >= -pad && xs0 + bs <= wP && ys0 >= -pad && ys0 + bs <= hP;
+      const int in1 = xs1 >= -pad && xs1 + bs <= wP && ys1 >= -pad && ys1 + bs <= hP;
+      uint8_t *p = out + (yp * bs) * so + xp * bs;
+      for (int i = 0; i < bs; i++)
+        for (int j = 0; j < bs; j++) {
+          int v;
+          if (in0 && in1) v = (p0[(ys0 + i) * s0 + xs0 + j] + p1[(ys1 + i) * s1 + xs1 + j] + 1) / 2;
+          else if (in1) v = p1[(ys1 + i) * s1 + xs1 + j];
+          else if (in0) v = p0[ys0 * s0 + xs0 + i * s1 + j];
+          else {
+            const int x0 = MIN(wP - 1, MAX(-pad, j + xs0)), x1 = MIN(wP - 1, MAX(-pad, j + xs1));
+            const int y0 = MIN(hP - 1, MAX(-pad, i + ys0)), y1 = MIN(hP - 1, MAX(-pad, i + ys1));
+            v = (p0[y0 * s0 + x0] + p1[y1 * s1 + x1] + 1) / 2;
+          }
+          p[i * so + j] = (uint8_t)v;
+        }
+    }
+}

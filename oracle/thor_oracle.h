@@ -62,4 +62,8 @@ void or_pad_frame(or_frame_t *f, int width, int height, int pad_y, int pad_c);
 void or_scale_down2x2(const uint8_t *in, int si, uint8_t *out, int so, int wo, int ho);
 void or_pad_plane(uint8_t *p, int s, int w, int h, int pad);
 
+/* temporal interpolation: interpolate_comp + mot_comp_avg (common/temporal_interp.c:387-441,920-944) */
+void or_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
+                    const int16_t *mv1, int bw, int bh, int bs, int wP, int hP, int pad, int chroma, int wt0, int wt1);
+
 #endif
