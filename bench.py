@@ -233,7 +233,7 @@ def interp_leg(torch, lib, reps: int = 50):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     alg = 3 * W * H * 1.5 + 3 * 8 * bw * bh
-    return {"workload": "4K frame (Y, U, V: 3 launches of k_interp_comp), 8x8 luma blocks, random MVs",
+    return {"workload": "4K frame (Y, U, V: 3 launches of k_interp_rows), 8x8 luma blocks, random MVs",
             "us_per_frame": round(ms * 1e3, 2), "alg_bytes": int(alg), "achieved_gb_s": round(alg / ms / 1e6, 1),
             "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
 

@@ -102,8 +102,10 @@ def test_gpu_interp_vs_reference_goldens():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("comp", [0, 1])
-def test_gpu_interp_4k_vs_oracle(comp):
+@pytest.mark.parametrize("comp,pitch_pad", [(0, 0), (1, 0), (0, 1), (1, 3)])
+def test_gpu_interp_4k_vs_oracle(comp, pitch_pad):
+    """pitch_pad != 0: an output stride not a multiple of the block width
+    takes the per-pixel kernel instead of the row-per-lane one."""
     from thor_amd import lib as tl
 
     L = tl.load()
@@ -119,7 +121,7 @@ def test_gpu_interp_4k_vs_oracle(comp):
     c = dict(w=w, h=h, wt0=3, wt1=1, bw=bw, bh=bh, comp=comp, mv=mv,
              r0=rng.integers(0, 256, (ph + 2 * pf, s), dtype=np.uint8),
              r1=rng.integers(0, 256, (ph + 2 * pf, s), dtype=np.uint8),
-             out=np.zeros((bh * bs, (bw * bs + 15) & ~15), np.uint8))
+             out=np.zeros((bh * bs, ((bw * bs + 15) & ~15) + pitch_pad), np.uint8))
     got = _gpu_interp(L, c)
     want = oracle_interp(c)
     assert np.array_equal(got, want), "%d bytes differ" % int((got != want).sum())

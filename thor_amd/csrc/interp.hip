@@ -65,6 +65,106 @@ __global__ __launch_bounds__(256) void k_interp_comp(const uint8_t *__restrict__
   out[(long long)y * so + x] = (uint8_t)v;
 }
 
+// Fast path for the reference's block sizes (bs = 8 luma / 4 chroma,
+// BLOCK_STEP/2, temporal_interp.c:12,994): one lane per block row.  Consecutive
+// lanes are consecutive blocks of a pixel row, so the 4/8-byte stores are
+// contiguous across the wave; each displaced reference row segment is read as
+// 2-3 aligned dwords and realigned with v_alignbyte (every dword read holds at
+// least one byte of the segment, so it lies inside the plane's allocation).
+template <int BS>
+struct InterpRow;
+template <>
+struct InterpRow<8> {
+  typedef uint2 T;
+  static __device__ __forceinline__ uint2 load(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t d0 = q[0], d1 = q[1], d2 = sh ? q[2] : 0u;
+    return make_uint2(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh));
+  }
+  static __device__ __forceinline__ uint2 avg(uint2 a, uint2 b) {
+    return make_uint2((a.x | b.x) - (((a.x ^ b.x) >> 1) & 0x7f7f7f7fu), (a.y | b.y) - (((a.y ^ b.y) >> 1) & 0x7f7f7f7fu));
+  }
+  static __device__ __forceinline__ void put(uint8_t *o, uint2 v) { *(uint2 *)o = v; }
+  static __device__ __forceinline__ void set(uint2 &v, int j, uint32_t b) {
+    if (j < 4) v.x |= b << (8 * j);
+    else v.y |= b << (8 * (j - 4));
+  }
+};
+template <>
+struct InterpRow<4> {
+  typedef uint32_t T;
+  static __device__ __forceinline__ uint32_t load(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t d0 = q[0], d1 = sh ? q[1] : 0u;
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
+  }
+  static __device__ __forceinline__ uint32_t avg(uint32_t a, uint32_t b) {
+    return (a | b) - (((a ^ b) >> 1) & 0x7f7f7f7fu);
+  }
+  static __device__ __forceinline__ void put(uint8_t *o, uint32_t v) { *(uint32_t *)o = v; }
+  static __device__ __forceinline__ void set(uint32_t &v, int j, uint32_t b) { v |= b << (8 * j); }
+};
+
+template <int BS>
+__global__ __launch_bounds__(256) void k_interp_rows(const uint8_t *__restrict__ p0, int s0,
+                                                     const uint8_t *__restrict__ p1, int s1, uint8_t *__restrict__ out,
+                                                     int so, const int16_t *__restrict__ mv0,
+                                                     const int16_t *__restrict__ mv1, int bw, int bh, int wP, int hP,
+                                                     int pad, int chroma, int wt0, int wt1) {
+  typedef InterpRow<BS> R;
+  const int xp = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (xp >= bw || y >= bh * BS) return;
+  const int yp = y / BS, i = y - yp * BS;
+  const int b = yp * bw + xp;
+  const uint32_t w1 = ((const uint32_t *)mv1)[b];
+  int m1x = (int16_t)(w1 & 0xffffu), m1y = (int16_t)(w1 >> 16);
+  int m0x, m0y;
+  if (chroma) {  // :934-938
+    m1x = (int16_t)(m1x >> 1);
+    m1y = (int16_t)(m1y >> 1);
+    const int numer = -wt1, denom = wt0;
+    if (numer == denom) {
+      m0x = m1x;
+      m0y = m1y;
+    } else if (numer == -denom) {
+      m0x = (int16_t)-m1x;
+      m0y = (int16_t)-m1y;
+    } else {
+      m0x = (int16_t)interp_scale_val(m1x, numer, denom);
+      m0y = (int16_t)interp_scale_val(m1y, numer, denom);
+    }
+  } else {
+    const uint32_t w0 = ((const uint32_t *)mv0)[b];
+    m0x = (int16_t)(w0 & 0xffffu);
+    m0y = (int16_t)(w0 >> 16);
+  }
+  const int xs0 = xp * BS + ((m0x + 4) >> 3), xs1 = xp * BS + ((m1x + 4) >> 3);
+  const int ys0 = yp * BS + ((m0y + 4) >> 3), ys1 = yp * BS + ((m1y + 4) >> 3);
+  const bool in0 = xs0 >= -pad && xs0 + BS <= wP && ys0 >= -pad && ys0 + BS <= hP;
+  const bool in1 = xs1 >= -pad && xs1 + BS <= wP && ys1 >= -pad && ys1 + BS <= hP;
+  typename R::T v;
+  if (in0 && in1) {
+    v = R::avg(R::load(p0 + (long long)(ys0 + i) * s0 + xs0), R::load(p1 + (long long)(ys1 + i) * s1 + xs1));
+  } else if (in1) {
+    v = R::load(p1 + (long long)(ys1 + i) * s1 + xs1);
+  } else if (in0) {
+    v = R::load(p0 + (long long)ys0 * s0 + xs0 + (long long)i * s1);  // ref1's stride, :420-422
+  } else {
+    v = typename R::T{};
+    const int y0 = min(hP - 1, max(-pad, i + ys0)), y1 = min(hP - 1, max(-pad, i + ys1));
+#pragma unroll
+    for (int j = 0; j < BS; j++) {
+      const int x0 = min(wP - 1, max(-pad, j + xs0)), x1 = min(wP - 1, max(-pad, j + xs1));
+      R::set(v, j, ((uint32_t)p0[(long long)y0 * s0 + x0] + p1[(long long)y1 * s1 + x1] + 1) >> 1);
+    }
+  }
+  R::put(out + (long long)y * so + xp * BS, v);
+}
+
 extern "C" {
 
 int thor_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
@@ -72,6 +172,17 @@ int thor_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8
                      void *stream) {
   if (bw == 0 || bh == 0) return THOR_OK;
   if (!p0 || !p1 || !out || !mv0 || !mv1 || bw < 0 || bh < 0 || bs < 1 || bs > 64 || pad < 0) return THOR_ERR_ARG;
+  const bool mv_ok = !(((uintptr_t)mv1 | (chroma ? 0 : (uintptr_t)mv0)) & 3);
+  if ((bs == 8 || bs == 4) && mv_ok && !(((uintptr_t)out | (uintptr_t)so) & (bs - 1))) {
+    const dim3 grid((bw + 63) / 64, (bh * bs + 3) / 4);
+    if (bs == 8)
+      k_interp_rows<8><<<grid, 256, 0, (hipStream_t)stream>>>(p0, s0, p1, s1, out, so, mv0, mv1, bw, bh, wP, hP, pad,
+                                                                chroma, wt0, wt1);
+    else
+      k_interp_rows<4><<<grid, 256, 0, (hipStream_t)stream>>>(p0, s0, p1, s1, out, so, mv0, mv1, bw, bh, wP, hP, pad,
+                                                                chroma, wt0, wt1);
+    return hipGetLastError() == hipSuccess ? THOR_OK : THOR_ERR_HIP;
+  }
   const dim3 grid((bw * bs + 63) / 64, (bh * bs + 3) / 4);
   k_interp_comp<<<grid, 256, 0, (hipStream_t)stream>>>(p0, s0, p1, s1, out, so, mv0, mv1, bw, bh, bs, wP, hP, pad,
                                                        chroma, wt0, wt1);
