@@ -262,6 +262,19 @@ int thor_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8
                      const int16_t *mv1, int bw, int bh, int bs, int wP, int hP, int pad, int chroma, int wt0, int wt1,
                      void *stream);
 
+/* interpolate_frame (common/temporal_interp.c:946-970) in one launch: Y with
+ * the reference's 8x8 blocks (bs = BLOCK_STEP/2, pad 4, wP = width + 4), U and
+ * V with 4x4 blocks (pad 2, wP = (width + 4) / 2) -- the thor_interp_comp
+ * semantics above per plane.  planes[0..2] = Y, U, V: (0,0) DEVICE pointers of
+ * pic[0], pic[1] (already swapped by mv_data->reversed) and the output. */
+typedef struct thor_interp_plane {
+  const uint8_t *p0, *p1;
+  uint8_t *out;
+  int32_t s0, s1, so;
+} thor_interp_plane_t;
+int thor_interp_frame(const thor_interp_plane_t *planes, const int16_t *mv0, const int16_t *mv1, int bw, int bh,
+                      int width, int height, int wt0, int wt1, void *stream);
+
 /* ---- device memory helpers (so the C-ABI is usable without torch) ------ */
 void *thor_dev_alloc(size_t bytes);
 int thor_dev_free(void *p);

@@ -125,3 +125,47 @@ def test_gpu_interp_4k_vs_oracle(comp, pitch_pad):
     got = _gpu_interp(L, c)
     want = oracle_interp(c)
     assert np.array_equal(got, want), "%d bytes differ" % int((got != want).sum())
+
+
+class InterpPlane(C.Structure):  # thor_interp_plane_t
+    _fields_ = [("p0", C.c_void_p), ("p1", C.c_void_p), ("out", C.c_void_p), ("s0", C.c_int32), ("s1", C.c_int32),
+                ("so", C.c_int32)]
+
+
+@pytest.mark.gpu
+def test_gpu_interp_frame_one_launch_vs_reference_goldens():
+    """thor_interp_frame (Y, U, V in one launch): Y against the luma golden,
+    U and V (fed the same chroma references) against the chroma golden."""
+    from thor_amd import lib as tl
+
+    L = tl.load()
+    cases = list(_cases())
+    for cy, cc in zip(cases[0::2], cases[1::2]):
+        bufs = []
+
+        def put(a):
+            a = np.ascontiguousarray(a)
+            p = L.thor_dev_alloc(a.nbytes)
+            assert p
+            bufs.append(p)
+            assert L.thor_h2d(p, a.ctypes.data, a.nbytes) == 0
+            return p
+
+        try:
+            planes, outs = (InterpPlane * 3)(), []
+            for k, c in enumerate((cy, cc, cc)):
+                pf = 96 if k == 0 else 48
+                s = c["r0"].shape[1]
+                o = np.zeros_like(c["out"])
+                d0, d1, do = put(c["r0"]), put(c["r1"]), put(o)
+                planes[k] = InterpPlane(d0 + pf * s + pf, d1 + pf * s + pf, do, s, s, o.shape[1])
+                outs.append((do, o))
+            rc = L.thor_interp_frame(C.cast(planes, C.c_void_p), put(cy["mv"][0]), put(cy["mv"][1]), cy["bw"], cy["bh"],
+                                     cy["w"], cy["h"], cy["wt0"], cy["wt1"], None)
+            assert rc == 0
+            for k, ((do, o), c) in enumerate(zip(outs, (cy, cc, cc))):
+                assert L.thor_d2h(o.ctypes.data, do, o.nbytes) == 0
+                assert np.array_equal(o, c["out"]), "%dx%d plane %d" % (c["w"], c["h"], k)
+        finally:
+            for p in bufs:
+                L.thor_dev_free(p)

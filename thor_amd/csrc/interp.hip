@@ -110,13 +110,11 @@ struct InterpRow<4> {
 };
 
 template <int BS>
-__global__ __launch_bounds__(256) void k_interp_rows(const uint8_t *__restrict__ p0, int s0,
-                                                     const uint8_t *__restrict__ p1, int s1, uint8_t *__restrict__ out,
-                                                     int so, const int16_t *__restrict__ mv0,
-                                                     const int16_t *__restrict__ mv1, int bw, int bh, int wP, int hP,
-                                                     int pad, int chroma, int wt0, int wt1) {
+__device__ __forceinline__ void interp_row(const uint8_t *__restrict__ p0, int s0, const uint8_t *__restrict__ p1, int s1,
+                                           uint8_t *__restrict__ out, int so, const int16_t *__restrict__ mv0,
+                                           const int16_t *__restrict__ mv1, int bw, int bh, int wP, int hP, int pad,
+                                           int chroma, int wt0, int wt1, int xp, int y) {
   typedef InterpRow<BS> R;
-  const int xp = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (xp >= bw || y >= bh * BS) return;
   const int yp = y / BS, i = y - yp * BS;
   const int b = yp * bw + xp;
@@ -165,6 +163,33 @@ __global__ __launch_bounds__(256) void k_interp_rows(const uint8_t *__restrict__
   R::put(out + (long long)y * so + xp * BS, v);
 }
 
+template <int BS>
+__global__ __launch_bounds__(256) void k_interp_rows(const uint8_t *__restrict__ p0, int s0,
+                                                     const uint8_t *__restrict__ p1, int s1, uint8_t *__restrict__ out,
+                                                     int so, const int16_t *__restrict__ mv0,
+                                                     const int16_t *__restrict__ mv1, int bw, int bh, int wP, int hP,
+                                                     int pad, int chroma, int wt0, int wt1) {
+  interp_row<BS>(p0, s0, p1, s1, out, so, mv0, mv1, bw, bh, wP, hP, pad, chroma, wt0, wt1,
+                 blockIdx.x * 64 + (threadIdx.x & 63), blockIdx.y * 4 + (threadIdx.x >> 6));
+}
+
+// interpolate_frame (:946-970) in one launch: grid z = plane (Y with 8-px
+// blocks, U and V with 4-px blocks and the derived chroma vectors).
+struct InterpFrame {
+  thor_interp_plane_t pl[3];
+};
+__global__ __launch_bounds__(256) void k_interp_frame(const InterpFrame F, const int16_t *__restrict__ mv0,
+                                                      const int16_t *__restrict__ mv1, int bw, int bh, int w, int h,
+                                                      int wt0, int wt1) {
+  const int xp = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const thor_interp_plane_t &P = F.pl[blockIdx.z];
+  if (blockIdx.z == 0)
+    interp_row<8>(P.p0, P.s0, P.p1, P.s1, P.out, P.so, mv0, mv1, bw, bh, w + 4, h + 4, 4, 0, wt0, wt1, xp, y);
+  else
+    interp_row<4>(P.p0, P.s0, P.p1, P.s1, P.out, P.so, mv0, mv1, bw, bh, (w + 4) / 2, (h + 4) / 2, 2, 1, wt0, wt1, xp,
+                  y);
+}
+
 extern "C" {
 
 int thor_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
@@ -186,6 +211,33 @@ int thor_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8
   const dim3 grid((bw * bs + 63) / 64, (bh * bs + 3) / 4);
   k_interp_comp<<<grid, 256, 0, (hipStream_t)stream>>>(p0, s0, p1, s1, out, so, mv0, mv1, bw, bh, bs, wP, hP, pad,
                                                        chroma, wt0, wt1);
+  return hipGetLastError() == hipSuccess ? THOR_OK : THOR_ERR_HIP;
+}
+
+int thor_interp_frame(const thor_interp_plane_t *planes, const int16_t *mv0, const int16_t *mv1, int bw, int bh,
+                      int width, int height, int wt0, int wt1, void *stream) {
+  if (bw == 0 || bh == 0) return THOR_OK;
+  if (!planes || !mv0 || !mv1 || bw < 0 || bh < 0 || width <= 0 || height <= 0) return THOR_ERR_ARG;
+  InterpFrame F;
+  bool fast = !(((uintptr_t)mv0 | (uintptr_t)mv1) & 3);
+  for (int c = 0; c < 3; c++) {
+    F.pl[c] = planes[c];
+    if (!F.pl[c].p0 || !F.pl[c].p1 || !F.pl[c].out) return THOR_ERR_ARG;
+    if (((uintptr_t)F.pl[c].out | (uintptr_t)F.pl[c].so) & (c ? 3 : 7)) fast = false;
+  }
+  if (!fast) {  // per-plane launches on the general kernel
+    for (int c = 0; c < 3; c++) {
+      const thor_interp_plane_t &P = F.pl[c];
+      const int rc = c == 0 ? thor_interp_comp(P.p0, P.s0, P.p1, P.s1, P.out, P.so, mv0, mv1, bw, bh, 8, width + 4,
+                                               height + 4, 4, 0, wt0, wt1, stream)
+                            : thor_interp_comp(P.p0, P.s0, P.p1, P.s1, P.out, P.so, mv0, mv1, bw, bh, 4,
+                                               (width + 4) / 2, (height + 4) / 2, 2, 1, wt0, wt1, stream);
+      if (rc) return rc;
+    }
+    return THOR_OK;
+  }
+  const dim3 grid((bw + 63) / 64, (bh * 8 + 3) / 4, 3);
+  k_interp_frame<<<grid, 256, 0, (hipStream_t)stream>>>(F, mv0, mv1, bw, bh, width, height, wt0, wt1);
   return hipGetLastError() == hipSuccess ? THOR_OK : THOR_ERR_HIP;
 }
 

@@ -107,6 +107,8 @@ def load(path: str = LIB_PATH):
     L.thor_scale_pyramid.restype = i
     L.thor_interp_comp.argtypes = [P, i, P, i, P, i, P, P] + [i] * 9 + [P]
     L.thor_interp_comp.restype = i
+    L.thor_interp_frame.argtypes = [P, P, P, i, i, i, i, i, i, P]
+    L.thor_interp_frame.restype = i
     # the reference's SIMD kernel surface (include/thor_kernels.h)
     u8p = P
     L.transform_simd.argtypes = [P, P, i, i]
