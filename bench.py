@@ -155,31 +155,33 @@ def encoder_leg(torch, lib, reps: int = 10):
 
 
 def pyramid_leg(torch, lib, reps: int = 50):
-    """Temporal-interpolation luma pyramid (thor_scale_pyramid, the chain of
+    """Temporal-interpolation luma pyramid (thor_scale_pyramid2, the chains of
     scale_frame_down2x2_simd calls of common/temporal_interp.c:1011-1019) on
-    one 4K reference frame: 3 levels + their 32-px padding.  Not part of
+    both 4K reference frames: 3 levels each + their 32-px padding.  Not part of
     `value`.  Algorithmic bytes: level 0 read once (W*H) + every level byte
     written once, padding included."""
     W, H, n = 3840, 2160, 3
     pad = 32
     dev = torch.device("cuda", torch.cuda.current_device())
-    src = torch.randint(0, 256, (H, W), dtype=torch.uint8, device=dev)
-    bufs, ptrs, strides, wr = [], [], [], 0
-    for l in range(1, n + 1):
-        wl, hl = W >> l, H >> l
-        s = (wl + 2 * pad + 15) & ~15
-        b = torch.empty((hl + 2 * pad) * s, dtype=torch.uint8, device=dev)
-        bufs.append(b)
-        ptrs.append(b.data_ptr() + pad * s + pad)
-        strides.append(s)
-        wr += (hl + 2 * pad) * (wl + 2 * pad)
-    parr = (C.c_void_p * 3)(*ptrs)
+    srcs = [torch.randint(0, 256, (H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+    bufs, parrs, wr = [], [], 0
+    strides = [((W >> l) + 2 * pad + 15) & ~15 for l in range(1, n + 1)]
+    for _ in range(2):
+        ptrs = []
+        for l in range(1, n + 1):
+            wl, hl, s = W >> l, H >> l, strides[l - 1]
+            b = torch.empty((hl + 2 * pad) * s, dtype=torch.uint8, device=dev)
+            bufs.append(b)
+            ptrs.append(b.data_ptr() + pad * s + pad)
+            wr += (hl + 2 * pad) * (wl + 2 * pad)
+        parrs.append((C.c_void_p * 3)(*ptrs))
     sarr = (C.c_int * 3)(*strides)
     st = torch.cuda.current_stream().cuda_stream
 
     def run():
-        assert lib.thor_scale_pyramid(src.data_ptr(), W, W, H, C.cast(parr, C.c_void_p),
-                                      C.cast(sarr, C.c_void_p), n, st) == 0
+        assert lib.thor_scale_pyramid2(srcs[0].data_ptr(), srcs[1].data_ptr(), W, W, H,
+                                       C.cast(parrs[0], C.c_void_p), C.cast(parrs[1], C.c_void_p),
+                                       C.cast(sarr, C.c_void_p), n, st) == 0
 
     run()
     torch.cuda.synchronize()
@@ -190,9 +192,10 @@ def pyramid_leg(torch, lib, reps: int = 50):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    alg = W * H + wr
-    return {"workload": "4K luma reference frame -> 3 down-sampled, padded levels (k_down_pyramid + k_pad_pyramid)",
-            "us_per_frame": round(ms * 1e3, 2), "alg_bytes": int(alg), "achieved_gb_s": round(alg / ms / 1e6, 1),
+    alg = 2 * W * H + wr
+    return {"workload": "both 4K luma references of interpolate_frames -> 3 down-sampled, padded levels "
+                        "each (thor_scale_pyramid2: k_down_pyramid + k_pad_pyramid, grid z = reference)",
+            "us_per_pair": round(ms * 1e3, 2), "alg_bytes": int(alg), "achieved_gb_s": round(alg / ms / 1e6, 1),
             "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
 
 

@@ -247,6 +247,13 @@ int thor_pyramid_levels(int width, int height);
 int thor_scale_pyramid(const uint8_t *src, int src_stride, int width, int height, uint8_t *const *levels,
                        const int *level_strides, int nlevels, void *stream);
 
+/* Both references of interpolate_frames (:1011-1019) in the same two launches
+ * (grid z = frame); same frame size and strides for the two, as
+ * interpolate_frames allocates them. */
+int thor_scale_pyramid2(const uint8_t *src0, const uint8_t *src1, int src_stride, int width, int height,
+                        uint8_t *const *levels0, uint8_t *const *levels1, const int *level_strides, int nlevels,
+                        void *stream);
+
 /* Replaces interpolate_comp (common/temporal_interp.c:920-944) on one plane:
  * for each of the bw x bh blocks of bs x bs pixels, mot_comp_avg (:387-441)
  * with the block's vectors (1/8 pel, rounded to integer: ACC_BITS 3) --

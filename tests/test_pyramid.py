@@ -148,3 +148,51 @@ def test_scale_pyramid_rejects_bad_arguments():
     assert L.thor_scale_pyramid(16, 64, 64, 64, C.cast(parr, C.c_void_p), C.cast(sarr, C.c_void_p), 4, None) == -1
     assert L.thor_scale_pyramid(16, 60, 64, 64, C.cast(parr, C.c_void_p), C.cast(sarr, C.c_void_p), 1, None) == -1
     assert L.thor_scale_pyramid(16, 64, 64, 64, C.cast(parr, C.c_void_p), C.cast(sarr, C.c_void_p), 0, None) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_pyramid2_both_references_vs_oracle():
+    """thor_scale_pyramid2: ref0 and ref1 of interpolate_frames in one pair of launches."""
+    from thor_amd import lib as tl
+
+    L = tl.load()
+    w, h, n = 1928, 1088, 3
+    rng = np.random.default_rng(99)
+    imgs = [rng.integers(0, 256, (h, w), dtype=np.uint8) for _ in range(2)]
+    ss = (w + 15) & ~15
+    bufs = []
+    try:
+        srcs, lv, shapes = [], [], []
+        for img in imgs:
+            src = np.zeros((h, ss), np.uint8)
+            src[:, :w] = img
+            d = L.thor_dev_alloc(src.nbytes)
+            assert d
+            bufs.append(d)
+            assert L.thor_h2d(d, src.ctypes.data, src.nbytes) == 0
+            srcs.append(d)
+            ptrs, shp = [], []
+            for l in range(1, n + 1):
+                wl, hl = w >> l, h >> l
+                s = _stride(wl)
+                nb = (hl + 2 * PAD) * s
+                dl = L.thor_dev_alloc(nb)
+                assert dl
+                bufs.append(dl)
+                ptrs.append(dl + PAD * s + PAD)
+                shp.append((hl, wl, s, dl, nb))
+            lv.append((C.c_void_p * 3)(*ptrs))
+            shapes.append(shp)
+        sarr = (C.c_int * 3)(*[_stride(w >> l) for l in range(1, n + 1)])
+        rc = L.thor_scale_pyramid2(srcs[0], srcs[1], ss, w, h, C.cast(lv[0], C.c_void_p), C.cast(lv[1], C.c_void_p),
+                                   C.cast(sarr, C.c_void_p), n, None)
+        assert rc == 0
+        for img, shp in zip(imgs, shapes):
+            want = oracle_pyramid(img, n)
+            for (hl, wl, s, dl, nb), b in zip(shp, want):
+                host = np.empty(nb, np.uint8)
+                assert L.thor_d2h(host.ctypes.data, dl, nb) == 0
+                assert np.array_equal(host.reshape(hl + 2 * PAD, s)[:, :wl + 2 * PAD], b)
+    finally:
+        for p in bufs:
+            L.thor_dev_free(p)

@@ -30,8 +30,14 @@ __device__ __forceinline__ uint32_t pyr_px(uint32_t a, uint32_t b, uint32_t c, u
   return (((a + b + 1) >> 1) + ((c + d + 1) >> 1)) >> 1;
 }
 
-__global__ __launch_bounds__(256) void k_down_pyramid(const uint8_t *__restrict__ src, int ss, int W, int H,
-                                                      const PyrLevels L) {
+// grid z = frame (interpolate_frames down-samples ref0 and ref1, :1011-1019)
+struct PyrJob {
+  const uint8_t *src[2];
+  PyrLevels L[2];
+};
+__global__ __launch_bounds__(256) void k_down_pyramid(const int ss, int W, int H, const PyrJob J) {
+  const uint8_t *__restrict__ src = J.src[blockIdx.z];
+  const PyrLevels &L = J.L[blockIdx.z];
   const int tx = blockIdx.x * 64 + threadIdx.x, ty = blockIdx.y * 4 + threadIdx.y;
   if (4 * tx >= L.w[0] || 4 * ty >= L.h[0]) return;
   const int x0 = 8 * tx, y0 = 8 * ty;
@@ -99,7 +105,8 @@ __global__ __launch_bounds__(256) void k_down_pyramid(const uint8_t *__restrict_
 }
 
 // pad every level (grid y = level)
-__global__ __launch_bounds__(256) void k_pad_pyramid(const PyrLevels L) {
+__global__ __launch_bounds__(256) void k_pad_pyramid(const PyrJob J) {
+  const PyrLevels &L = J.L[blockIdx.z];
   const int l = blockIdx.y;
   const PadPlane p(L.y[l], L.s[l], L.w[l], L.h[l], THOR_PYR_PAD);
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -124,31 +131,51 @@ int thor_pyramid_levels(int width, int height) {
   return ml > 1 ? ml - 1 : 0;
 }
 
-int thor_scale_pyramid(const uint8_t *src, int src_stride, int width, int height, uint8_t *const *levels,
-                       const int *level_strides, int nlevels, void *stream) {
+static int pyramid_launch(const uint8_t *const *srcs, int nframes, int src_stride, int width, int height,
+                          uint8_t *const *const *levels, const int *level_strides, int nlevels, void *stream) {
   if (nlevels == 0) return THOR_OK;
-  if (!src || !levels || !level_strides || nlevels < 0 || nlevels > THOR_PYR_MAX) return THOR_ERR_ARG;
+  if (!levels || !level_strides || nlevels < 0 || nlevels > THOR_PYR_MAX) return THOR_ERR_ARG;
   if (width <= 0 || height <= 0 || (width >> nlevels) < 1 || (height >> nlevels) < 1) return THOR_ERR_ARG;
-  if (((uintptr_t)src & 7) || (src_stride & 7) || src_stride < width) return THOR_ERR_ARG;
-  PyrLevels L{};
-  L.n = nlevels;
+  if ((src_stride & 7) || src_stride < width) return THOR_ERR_ARG;
+  PyrJob J{};
   int chunks = 0;
-  for (int l = 0; l < nlevels; l++) {
-    L.y[l] = levels[l];
-    L.s[l] = level_strides[l];
-    L.w[l] = width >> (l + 1);
-    L.h[l] = height >> (l + 1);
-    // create_yuv_frame layout: 16-byte aligned rows at x = -pad, stride % 16 == 0
-    if (!L.y[l] || ((uintptr_t)L.y[l] & 15) || (L.s[l] & 15) || L.s[l] < L.w[l] + 2 * THOR_PYR_PAD) return THOR_ERR_ARG;
-    const int c = pyr_pad_chunks(L.w[l], L.h[l]);
-    chunks = c > chunks ? c : chunks;
+  for (int f = 0; f < nframes; f++) {
+    if (!srcs[f] || ((uintptr_t)srcs[f] & 7) || !levels[f]) return THOR_ERR_ARG;
+    J.src[f] = srcs[f];
+    PyrLevels &L = J.L[f];
+    L.n = nlevels;
+    for (int l = 0; l < nlevels; l++) {
+      L.y[l] = levels[f][l];
+      L.s[l] = level_strides[l];
+      L.w[l] = width >> (l + 1);
+      L.h[l] = height >> (l + 1);
+      // create_yuv_frame layout: 16-byte aligned rows at x = -pad, stride % 16 == 0
+      if (!L.y[l] || ((uintptr_t)L.y[l] & 15) || (L.s[l] & 15) || L.s[l] < L.w[l] + 2 * THOR_PYR_PAD) return THOR_ERR_ARG;
+      const int c = pyr_pad_chunks(L.w[l], L.h[l]);
+      chunks = c > chunks ? c : chunks;
+    }
   }
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((L.w[0] + 4 * 64 - 1) / (4 * 64), (L.h[0] + 4 * 4 - 1) / (4 * 4));
-  k_down_pyramid<<<grid, dim3(64, 4), 0, st>>>(src, src_stride, width, height, L);
+  const PyrLevels &L = J.L[0];
+  const dim3 grid((L.w[0] + 4 * 64 - 1) / (4 * 64), (L.h[0] + 4 * 4 - 1) / (4 * 4), nframes);
+  k_down_pyramid<<<grid, dim3(64, 4), 0, st>>>(src_stride, width, height, J);
   if (hipGetLastError() != hipSuccess) return THOR_ERR_HIP;
-  k_pad_pyramid<<<dim3((chunks + 255) / 256, nlevels), 256, 0, st>>>(L);
+  k_pad_pyramid<<<dim3((chunks + 255) / 256, nlevels, nframes), 256, 0, st>>>(J);
   return hipGetLastError() == hipSuccess ? THOR_OK : THOR_ERR_HIP;
+}
+
+int thor_scale_pyramid(const uint8_t *src, int src_stride, int width, int height, uint8_t *const *levels,
+                       const int *level_strides, int nlevels, void *stream) {
+  if (nlevels != 0 && !src) return THOR_ERR_ARG;
+  return pyramid_launch(&src, 1, src_stride, width, height, &levels, level_strides, nlevels, stream);
+}
+
+int thor_scale_pyramid2(const uint8_t *src0, const uint8_t *src1, int src_stride, int width, int height,
+                        uint8_t *const *levels0, uint8_t *const *levels1, const int *level_strides, int nlevels,
+                        void *stream) {
+  const uint8_t *srcs[2] = {src0, src1};
+  uint8_t *const *lv[2] = {levels0, levels1};
+  return pyramid_launch(srcs, 2, src_stride, width, height, lv, level_strides, nlevels, stream);
 }
 
 }  // extern "C"

@@ -105,6 +105,8 @@ def load(path: str = LIB_PATH):
     L.thor_pyramid_levels.restype = i
     L.thor_scale_pyramid.argtypes = [P, i, i, i, P, P, i, P]
     L.thor_scale_pyramid.restype = i
+    L.thor_scale_pyramid2.argtypes = [P, P, i, i, i, P, P, P, i, P]
+    L.thor_scale_pyramid2.restype = i
     L.thor_interp_comp.argtypes = [P, i, P, i, P, i, P, P] + [i] * 9 + [P]
     L.thor_interp_comp.restype = i
     L.thor_interp_frame.argtypes = [P, P, P, i, i, i, i, i, i, P]
