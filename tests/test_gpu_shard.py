@@ -49,7 +49,7 @@ def _worker(rank, world, port, name, nframes, q):
             dec.close()
 
 
-@pytest.mark.parametrize("name,nframes,world", [("cif_high", 10, 2), ("hd_low", 6, 2), ("cif_med", 10, 3)])
+@pytest.mark.parametrize("name,nframes,world", [("cif_high", 10, 2), ("hd_low", 6, 2), ("cif_med", 10, 3), ("k4_med", 8, 2)])
 def test_row_sharded_decode_matches_reference(name, nframes, world):
     import random
     import sys

@@ -11,7 +11,7 @@ from thor_amd.trace import load_trace
 
 pytestmark = pytest.mark.gpu
 
-STREAMS = ["cif_low", "cif_med", "cif_high", "cif_hdb", "hd_low", "k4_low"]
+STREAMS = ["cif_low", "cif_med", "cif_high", "cif_hdb", "hd_low", "k4_low", "k4_med", "w8_low"]
 
 
 def _md5(b):
@@ -133,3 +133,20 @@ def test_single_frame_api_without_lists(streams):
             assert got == streams["cif_high"]["stage_md5"][fr.decode_order]["final"], fr.decode_order
     finally:
         d.close()
+
+
+def test_missing_reference_is_an_error():
+    """A P frame whose reference frame is not resident must not decode to stale
+    pixels with rc 0: thor_dec_sync reports THOR_ERR_REF (-4), and the flag is
+    cleared afterwards (the next sync of a good frame succeeds)."""
+    from thor_amd.decoder import GpuDecoder
+
+    seq, frames = load_trace(trace_path("cif_low"))
+    dec = GpuDecoder(seq)
+    try:
+        dec.decode(dec.upload(frames[1]))  # frame 0 (its reference) was never decoded
+        assert dec.lib.thor_dec_sync(dec.h) == -4
+        dec.decode(dec.upload(frames[0]))
+        assert dec.lib.thor_dec_sync(dec.h) == 0
+    finally:
+        dec.close()

@@ -10,7 +10,7 @@ from conftest import trace_path
 from oracle import OracleDecoder
 from thor_amd.trace import load_trace
 
-STREAMS = ["cif_low", "cif_med", "cif_high", "cif_hdb", "hd_low", "k4_low"]
+STREAMS = ["cif_low", "cif_med", "cif_high", "cif_hdb", "hd_low", "k4_low", "k4_med", "w8_low"]
 
 
 @pytest.mark.parametrize("name", STREAMS)

@@ -8,7 +8,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libthor_amd.so")
-SOURCES = ["libthor_amd.hip", "recon.hip", "resid.hip", "txq.hip", "inter.hip", "intra.hip", "loopfilter.hip", "capi.hip", "simd_surface.hip", "common.h"]
+# every translation unit and header under csrc/ (libthor_amd.hip #includes the .hip files)
+SOURCES = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result", "-Wno-bitwise-instead-of-logical"]

@@ -127,7 +127,7 @@ int thor_d2h(void *dst, const void *src, size_t bytes) {
 }
 
 thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
-  if (!seq || seq->width <= 0 || seq->height <= 0 || (seq->width & 15) || (seq->height & 7)) return nullptr;
+  if (!seq || seq->width <= 0 || seq->height <= 0 || (seq->width & 7) || (seq->height & 7)) return nullptr;  // multiples of 8 (enc/strings.c:437)
   if (num_slots <= 1) num_slots = 34;  // 33 references + the frame being decoded
   if (num_slots > THOR_MAX_SLOTS) num_slots = THOR_MAX_SLOTS;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -228,16 +228,32 @@ int thor_dec_set_stop_stage(thor_dec_t *d, int stage) {
   d->stop_stage = stage;
   return THOR_OK;
 }
-int thor_dec_sync(thor_dec_t *d) {
-  if (!d) return THOR_ERR_ARG;
-  HIPCHK(hipStreamSynchronize(d->stream));
-  unsigned to = 0;
-  HIPCHK(hipMemcpy(&to, d->ctl + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (to) {
+// Reads and clears the intra-chain timeout flag (ctl[1], set by k_intra when a
+// wavefront wait gives up): each call reports only the timeouts since the last.
+// Also reads and clears the missing-reference flag (ctl[2], set by k_frame_prep
+// when an inter CU names a frame that is not resident in the ring).
+static int check_timeout(thor_dec *d) {
+  unsigned fl[2] = {0, 0};
+  HIPCHK(hipMemcpy(fl, d->ctl + 1, sizeof(fl), hipMemcpyDeviceToHost));
+  if (fl[0] | fl[1]) {
+    const unsigned zero[2] = {0, 0};
+    HIPCHK(hipMemcpy(d->ctl + 1, zero, sizeof(zero), hipMemcpyHostToDevice));
+  }
+  if (fl[1]) {
+    fprintf(stderr, "thor_amd: a block references a frame that is not resident\n");
+    return THOR_ERR_REF;
+  }
+  if (fl[0]) {
     fprintf(stderr, "thor_amd: intra dependency wait timed out\n");
     return THOR_ERR_HIP;
   }
   return THOR_OK;
+}
+
+int thor_dec_sync(thor_dec_t *d) {
+  if (!d) return THOR_ERR_ARG;
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return check_timeout(d);
 }
 
 static int find_slot_host(const thor_dec *d, int fnum) {
@@ -711,6 +727,10 @@ int thor_dec_read_frame(thor_dec_t *d, int frame_num, uint8_t *y, uint8_t *u, ui
   if (s < 0) return THOR_ERR_REF;
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
+  {
+    const int rc = check_timeout(d);  // a frame whose intra chains timed out is not returned as valid
+    if (rc != THOR_OK) return rc;
+  }
   int W = d->seq.width, H = d->seq.height;
   const uint8_t *base = d->slots + (long long)s * d->slot_bytes;
   if (y) HIPCHK(hipMemcpy2D(y, W, base + d->offy, d->sy, W, H, hipMemcpyDeviceToHost));
@@ -720,8 +740,9 @@ int thor_dec_read_frame(thor_dec_t *d, int frame_num, uint8_t *y, uint8_t *u, ui
 }
 
 int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const uint8_t *u, const uint8_t *v) {
-  if (!d || !y || !u || !v) return THOR_ERR_ARG;
+  if (!d || !y || !u || !v || d->pending) return THOR_ERR_ARG;
   HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));  // in-flight kernels may still read the slot being replaced
   int s = find_slot_host(d, frame_num);
   if (s < 0) s = pick_slot(d, frame_num);
   int W = d->seq.width, H = d->seq.height;

@@ -38,6 +38,10 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   const int sg1 = ref1 >= f.frame_num;
   const int8_t *lut = (const int8_t *)f.slot_lut;
   const int s0 = lut[ref0 & 127], s1 = bi ? lut[ref1 & 127] : 0;
+  // an inter CU naming a reference that is not resident: flag it (ctl[2] ->
+  // THOR_ERR_REF from thor_dec_sync / thor_dec_read_frame) instead of leaving
+  // stale slot pixels behind silently
+  if (lane == 0 && mode != M_INTRA && (s0 < 0 || (bi && s1 < 0))) atomicOr(&f.ctl[2], 1u);
   const unsigned resbits = mode == M_SKIP ? 0u : ((unsigned)(B.coeff_mask & 7) << 18);
   const bool quarters = mode == M_INTER || mode == M_BIPRED;  // four size/2 quarters with mv_arr[i], :381-392
   int div = S >> 3;

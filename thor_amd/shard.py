@@ -57,6 +57,10 @@ class RowShard:
 
         if device_exchange:
             dev = torch.device("cuda", torch.cuda.current_device())
+            # the band copies (decoder stream) and the collective (torch's current
+            # stream) must be ordered: run the decoder on torch's current stream
+            if hasattr(dec, "set_stream"):
+                dec.set_stream(torch.cuda.current_stream(dev).cuda_stream)
             self.send = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
             self.recv = torch.empty(self.world * self.nbytes, dtype=torch.uint8, device=dev)
         else:

@@ -45,6 +45,9 @@ STREAMS = [
     ("cif_hdb", 352, 288, 17, "config_HDB16_low_complexity.txt", ["-interp_ref", "0"], 4),
     ("hd_low", 1920, 1080, 17, "config_LDB_low_complexity.txt", [], 5),
     ("k4_low", 3840, 2160, 8, "config_LDB_low_complexity.txt", [], 6),
+    # round 2: BASELINE config 4 (bi-pred at 4K), a width = 8 mod 16 clip (enc/strings.c:437)
+    ("k4_med", 3840, 2160, 8, "config_LDB_medium_complexity.txt", [], 7),
+    ("w8_low", 360, 288, 6, "config_LDB_low_complexity.txt", [], 8),
 ]
 
 
