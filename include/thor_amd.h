@@ -224,6 +224,29 @@ int thor_enc_tu_batch(const thor_enc_tu_t *tus, int n, const uint8_t *orig, cons
 int thor_enc_cost_batch(const uint32_t *ssd, const int32_t *tu_first, const int32_t *tu_count, const int32_t *nbits,
                         double lambda, uint32_t *cost, int ncu, void *stream);
 
+/* ---- device-resident encoder (the full RD loop) ---- *
+ * Encoder parameters: enc_params (enc/mainenc.h:34-88), the flags of the
+ * reference's configuration files / command line (enc/strings.c:286-338),
+ * same names and types (float where the reference parses ARG_FLOAT).      */
+typedef struct thor_enc_params {
+  int32_t width, height, qp, num_frames, skip;
+  float frame_rate;
+  float lambda_coeffI, lambda_coeffP, lambda_coeffB, lambda_coeffB0, lambda_coeffB1, lambda_coeffB2, lambda_coeffB3;
+  float early_skip_thr;
+  int32_t enable_tb_split, enable_pb_split, max_num_ref, HQperiod, num_reorder_pics, dyadic_coding, interp_ref;
+  int32_t dqpP, dqpB, dqpB0, dqpB1, dqpB2, dqpB3;
+  float mqpP, mqpB, mqpB0, mqpB1, mqpB2, mqpB3;
+  int32_t dqpI, intra_period, intra_rdo, rdoq, max_delta_qp, delta_qp_step, encoder_speed, sync, deblocking, clpf,
+      snrcalc, use_block_contexts, enable_bipred;
+} thor_enc_params_t;
+
+/* The reference defaults (enc/strings.c:286-338). */
+void thor_enc_default_params(thor_enc_params_t *p);
+/* 0 if the parameters are supported by the device encoder, else THOR_ERR_ARG
+ * (check_parameters, enc/strings.c:431-479, plus this build's limits:
+ * rdoq 0, no interp_ref, no speed-0 B frames). */
+int thor_enc_check_params(const thor_enc_params_t *p);
+
 /* ---- temporal interpolation: luma down-sampling pyramid ----------------- */
 
 /* Number of down-sampled levels interpolate_frames builds for a width x height

@@ -554,10 +554,7 @@ static const int tc_tab[56] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0
                                2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14};
 
 /* per-4x4 side info as copy_deblock_data (dec/decode_block.c:122-156) stores it */
-typedef struct {
-  uint8_t mode, cbp_y, cbp_u, cbp_v, size, tb_split, pb_part;
-  int16_t mv0x, mv0y, mv1x, mv1y;
-} dbinfo_t;
+typedef or_cell_t dbinfo_t;
 
 static void fill_dbinfo(dbinfo_t *db, int bstride, const thor_block_t *b) {
   int size = b->size;
@@ -971,4 +968,18 @@ void or_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_
           p[i * so + j] = (uint8_t)v;
         }
     }
+}
+
+/* The frame loop filters over caller-supplied per-4x4 side info (the
+ * encoder-side checker, tools/enc_host): deblock_frame_y / _uv
+ * (common/common_frame.c:46-321, chroma at chroma_qp[qp]) and clpf_frame with
+ * per-SB flags (:485-557). */
+void or_deblock_cells(or_frame_t *f, const or_cell_t *cells, int W, int H, int qp) {
+  deblock_y(f->y, f->stride_y, cells, W, H, qp);
+  int qpc = chroma_qp_tab[qp];
+  deblock_uv(f->u, f->stride_c, cells, W, H, qpc);
+  deblock_uv(f->v, f->stride_c, cells, W, H, qpc);
+}
+void or_clpf_cells(or_frame_t *f, const or_cell_t *cells, int W, int H, const uint8_t *flags) {
+  clpf_frame(f, cells, W, H, flags);
 }

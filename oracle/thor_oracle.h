@@ -15,6 +15,9 @@
 #define THOR_ORACLE_H
 #include <stdint.h>
 #include "../include/thor_amd.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
 
 /* ---- block kernels ------------------------------------------------------ */
 void or_mc_luma(uint8_t *pblock, int pstride, const uint8_t *ref, int rstride, int width, int height, int mvx,
@@ -42,6 +45,13 @@ int or_encode_tu(const uint8_t *orig, int os, const uint8_t *pred, int ps, uint8
                  int type, int fast, int16_t *levels, uint32_t *ssd);
 
 /* ---- frames ------------------------------------------------------------- */
+/* per-4x4 side info as copy_deblock_data stores it (dec/decode_block.c:122-156,
+ * enc/encode_block.c:1947-1981) */
+typedef struct {
+  uint8_t mode, cbp_y, cbp_u, cbp_v, size, tb_split, pb_part;
+  int16_t mv0x, mv0y, mv1x, mv1y;
+} or_cell_t;
+
 typedef struct or_frame {
   uint8_t *y, *u, *v; /* interior (0,0) pointers of padded planes */
   int stride_y, stride_c;
@@ -66,4 +76,11 @@ void or_pad_plane(uint8_t *p, int s, int w, int h, int pad);
 void or_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
                     const int16_t *mv1, int bw, int bh, int bs, int wP, int hP, int pad, int chroma, int wt0, int wt1);
 
+struct or_frame;
+void or_deblock_cells(struct or_frame *f, const or_cell_t *cells, int W, int H, int qp);
+void or_clpf_cells(struct or_frame *f, const or_cell_t *cells, int W, int H, const uint8_t *flags);
+
+#ifdef __cplusplus
+}
+#endif
 #endif

@@ -1,0 +1,719 @@
+// Device-resident Thor encoder, part 1: portability layer, tables, the bit
+// writer, VLC tables, block syntax (write_block) and the neighbour logic (MV
+// predictor, skip / merge candidates, block contexts, availability).
+//
+// SPMD single source.  The encoder runs as ONE wavefront per superblock row
+// (WPP, enc.hip): control flow is wave-uniform, pixel work is spread over the
+// 64 lanes with `for (e = TE_LANE; e < n; e += TE_NL)` loops and wave
+// reductions.  The same source also compiles as plain host C++ with
+// TE_NL = 1 (TE_HOST, tools/enc_host/): that build exists ONLY as a debugging
+// harness for the RD logic against the reference bitstream on a CPU-only box;
+// libthor_amd.so never contains it.
+//
+// Every function restates the reference behaviour it cites (file:line under
+// the reference tree; enc/ and common/ of awakecoding/thor).  Integer and
+// float semantics follow the reference's gcc -std=c99 x86-64 build exactly:
+// arithmetic right shifts, C division truncating toward zero, float params
+// promoted to double, no FMA contraction (-ffp-contract=off).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#if defined(TE_HOST)
+#include <stdlib.h>
+#define TE_FN static inline
+#define TE_NOINL static
+#define TE_LANE 0
+#define TE_NL 1
+#define TE_CONST static const
+#else
+#define TE_FN __device__ __forceinline__
+#define TE_NOINL __device__ __noinline__
+#define TE_LANE ((int)threadIdx.x)
+#define TE_NL 64
+#define TE_CONST __constant__ static const
+#endif
+
+// ---- wave helpers -----------------------------------------------------------
+// te_sync: every lane's earlier global / LDS writes are visible to every lane
+// of the wave afterwards (one wave = one workgroup: the workgroup barrier +
+// fences).
+TE_FN void te_sync() {
+#if !defined(TE_HOST)
+  __syncthreads();
+#endif
+}
+TE_FN uint32_t te_sum(uint32_t v) {
+#if !defined(TE_HOST)
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+#endif
+  return v;
+}
+TE_FN int te_maxi(int v) {
+#if !defined(TE_HOST)
+  for (int o = 32; o > 0; o >>= 1) {
+    const int w = __shfl_xor(v, o);
+    v = v > w ? v : w;
+  }
+#endif
+  return v;
+}
+TE_FN int te_any(int v) {
+#if !defined(TE_HOST)
+  return __any(v) ? 1 : 0;
+#else
+  return v != 0;
+#endif
+}
+
+#define TE_MIN(a, b) ((a) < (b) ? (a) : (b))
+#define TE_MAX(a, b) ((a) > (b) ? (a) : (b))
+TE_FN int te_clip255(int x) { return x < 0 ? 0 : (x > 255 ? 255 : x); }
+TE_FN int te_clip16(int x) { return x < -32768 ? -32768 : (x > 32767 ? 32767 : x); }
+TE_FN int te_wrap16(int x) { return (int)(int16_t)(uint16_t)(x & 0xffff); }
+TE_FN int te_abs(int x) { return x < 0 ? -x : x; }
+TE_FN int te_log2(int x) {  // log2i of a power of two
+  int r = 0;
+  while (x > 1) {
+    x >>= 1;
+    r++;
+  }
+  return r;
+}
+TE_FN int te_log2u(unsigned x) {  // floor(log2) (common/simd.h log2i), x >= 1
+  int r = 0;
+  while (x > 1) {
+    x >>= 1;
+    r++;
+  }
+  return r;
+}
+
+// ---- constants (common/global.h:57-88, common/types.h) ---------------------
+enum { TE_SKIP = 0, TE_INTRA = 1, TE_INTER = 2, TE_BIPRED = 3, TE_MERGE = 4 };
+enum { TE_I = 0, TE_P = 1, TE_B = 2 };
+enum { TE_DC = 0, TE_PLANAR, TE_HOR, TE_VER, TE_UPLEFT, TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT, TE_UPLEFTLEFT,
+       TE_DOWNLEFTLEFT, TE_NUM_INTRA };
+#define TE_MAX_UINT32 2147483648u  // MAX_UINT32 is `1<<31` (global.h:65), i.e. 2^31 as uint32_t
+#define TE_MAX_REF 4               // references an encoder frame can use (max_num_ref <= 4, 2-bit header field)
+#define TE_MVCAND 64               // frame_info_t.mvcand[..][64] (enc/mainenc.h:126)
+
+struct TeMv {
+  int16_t x, y;
+};
+// inter_pred_t (common/types.h:111-118); uint32 ref_idx / bipred_flag kept as
+// int32 (bipred_flag is -1 for intra neighbours: dir = -1, encode_block.c:2028)
+struct TeInterPred {
+  TeMv mv0, mv1;
+  int32_t ref_idx0, ref_idx1, bipred_flag;
+};
+// deblock_data_t per 4x4 cell (common/types.h:127-135), filled by copy_deblock_data
+// (enc/encode_block.c:1947-1981), zeroed per frame (enc/encode_frame.c:74)
+struct TeCell {
+  TeInterPred ip;
+  uint8_t mode, size, tb_split, pb_part;
+  uint8_t cbp_y, cbp_u, cbp_v, rsv;
+};
+struct TeCtx {  // block_context_t (common/types.h:181-188)
+  int split, cbp, index;
+};
+
+// Frame-level inputs of one encoder frame (encoder_info_t / frame_info_t /
+// enc_params, enc/mainenc.h): everything the RD loop reads besides the pixels.
+struct TeFrame {
+  const uint8_t *oy, *ou, *ov;  // original frame (orig), interior (0,0)
+  int osy, osc;
+  uint8_t *ry, *ru, *rv;        // frame being reconstructed (rec), interior (0,0)
+  int rsy, rsc;                 // strides of rec AND of every reference (one ring)
+  const uint8_t *refy[TE_MAX_REF], *refu[TE_MAX_REF], *refv[TE_MAX_REF];  // ref[ref_array[r]] (padded 96/48)
+  int ref_fnum[TE_MAX_REF];
+  TeCell *cells;
+  int W, H;
+  int frame_num, frame_type, qp, num_ref, num_intra_modes, interp_ref;
+  double lambda, sqrt_lambda;   // frame_info->lambda and sqrt(lambda), computed on the host
+  // enc_params (enc/strings.c:286-338)
+  int speed, enable_tb_split, enable_pb_split, enable_bipred, max_delta_qp, delta_qp_step;
+  int intra_rdo, use_block_contexts, rdoq, sync;
+  float early_skip_thr;
+  const int *es_thr;  // early-skip thresholds [2][52][4], te_es_thresholds (host)
+};
+
+// ---- tables -------------------------------------------------------------------
+TE_CONST int te_chroma_qp_t[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+                                   18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33,
+                                   34, 34, 35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45};
+TE_FN int te_chroma_qp(int q) { return te_chroma_qp_t[q < 0 ? 0 : (q > 51 ? 51 : q)]; }
+TE_CONST int te_gquant[6] = {26214, 23302, 20560, 18396, 16384, 14564};  // common/common_block.c:97
+TE_CONST int te_gdequant[6] = {40, 45, 51, 57, 64, 72};                  // :98
+// iq_8x8, enc/encode_block.c:2967-2971
+TE_CONST uint16_t te_iq8[52] = {6,   7,   8,   8,   10,  11,  12,  13,  15,  17,  19,   21,   24,   27,
+                                30,  34,  38,  43,  48,  54,  60,  68,  76,  86,  96,   108,  121,  136,
+                                152, 171, 192, 216, 242, 272, 305, 342, 384, 431, 484,  543,  610,  684,
+                                768, 862, 968, 1086, 1219, 1368, 1536, 1724, 1935, 2172};
+
+// zigzag scans (common/common_block.c:38-73; zigzag16 / 64 / 256 all follow
+// this rule): anti-diagonals, alternating direction; te_zz(q, raster) = scan
+// position.
+TE_FN int te_zz(int q, int r) {
+  const int i = r / q, j = r - (r / q) * q, d = i + j;
+  // positions before diagonal d
+  int before;
+  if (d < q) before = d * (d + 1) / 2;
+  else {
+    const int e = 2 * q - 1 - d;  // diagonals after (and including) d have e, e-1, ... elements
+    before = q * q - e * (e + 1) / 2;
+  }
+  const int lo = d < q ? 0 : d - q + 1;  // smallest row index on diagonal d
+  const int hi = d < q ? d : q - 1;
+  // even d: bottom-left to top-right (rows descending), odd d: rows ascending
+  return (d & 1) ? before + (i - lo) : before + (hi - i);
+}
+
+// ---- bit writer (enc/putbits.c:112-146) -------------------------------------
+// One stream per superblock: MSB-first bits into 32-bit words.  Rewinding
+// (write_stream_pos) sets the position back; later writes overwrite.  Only
+// lane 0 touches the words; every lane tracks the position.
+struct TeBits {
+  uint32_t *w;
+  int pos, cap;  // bits
+};
+TE_FN void te_put(TeBits &b, int n, uint32_t val) {
+  if (n <= 0) return;
+  if (n < 32) val &= (1u << n) - 1;
+  if (TE_LANE == 0 && b.pos + n <= b.cap) {
+    const int wi = b.pos >> 5, off = b.pos & 31;  // bit `off` from the MSB of word wi
+    const int r0 = 32 - off;                        // room in word wi
+    if (n <= r0) {
+      const uint32_t m = (n == 32 ? 0xffffffffu : ((1u << n) - 1)) << (r0 - n);
+      b.w[wi] = (b.w[wi] & ~m) | (val << (r0 - n));
+    } else {
+      const int n1 = n - r0;  // bits spilling into word wi + 1
+      const uint32_t m0 = r0 == 32 ? 0xffffffffu : ((1u << r0) - 1);
+      b.w[wi] = (b.w[wi] & ~m0) | (val >> n1);
+      const uint32_t m1 = ((1u << n1) - 1) << (32 - n1);
+      b.w[wi + 1] = (b.w[wi + 1] & ~m1) | ((val & ((1u << n1) - 1)) << (32 - n1));
+    }
+  }
+  b.pos += n;
+}
+
+// quote_vlc / put_vlc, enc/putvlc.c:34-229 (tables 0-5, 10, 11; the others
+// are unused by the encoder): code length, and the code word in *code.
+TE_FN int te_vlc(unsigned n, unsigned cn, unsigned *code) {
+  unsigned len, c;
+  if (n <= 5) {
+    if ((int)cn < (6 * (1 << n))) {
+      const unsigned t = 1u << n;
+      c = t + (cn & (t - 1));
+      len = 1 + n + (cn >> n);
+    } else {
+      c = cn - (6 * (1 << n)) + (1 << n);
+      len = (6 - n) + 1 + 2 * te_log2u(c);
+    }
+  } else if (n == 10) {
+    c = cn + 1;
+    len = 1 + 2 * te_log2u(c);
+  } else {  // n == 11
+    len = cn < 2 ? cn + 1 : cn / 2 + 3;
+    c = cn < 2 ? 1 : 2 + (cn & 1);
+  }
+  if (code) *code = c;
+  return (int)len;
+}
+TE_FN int te_quote_vlc(unsigned n, unsigned cn) { return te_vlc(n, cn, nullptr); }
+TE_FN int te_put_vlc(TeBits &b, unsigned n, unsigned cn) {
+  unsigned c;
+  const int len = te_vlc(n, cn, &c);
+  // putbits(len, code): len can exceed 32 only for absurd code numbers
+  if (len > 32) {
+    te_put(b, len - 32, 0);
+    te_put(b, 32, c);
+  } else {
+    te_put(b, len, c);
+  }
+  return len;
+}
+
+// quote_mv_bits, enc/encode_block.c:799-814
+TE_FN int te_mv_bits(int dy, int dx) {
+  int bits = te_quote_vlc(10, 2 * te_abs(dx) - (dx < 0 ? 1 : 0));
+  bits += te_quote_vlc(10, 2 * te_abs(dy) - (dy < 0 ? 1 : 0));
+  return bits;
+}
+// write_mv, enc/write_bits.c:50-69
+TE_FN void te_write_mv(TeBits &b, TeMv mv, TeMv mvp) {
+  const int dx = mv.x - mvp.x, dy = mv.y - mvp.y;
+  te_put_vlc(b, 10, 2 * (uint16_t)te_abs(dx) - (dx < 0 ? 1 : 0));
+  te_put_vlc(b, 10, 2 * (uint16_t)te_abs(dy) - (dy < 0 ? 1 : 0));
+}
+
+// ---- availability (common/common_block.c:100-129) ----------------------------
+TE_FN int te_up_avail(int ypos) { return ypos > 0; }
+TE_FN int te_left_avail(int xpos) { return xpos > 0; }
+TE_FN int te_upright_avail(int ypos, int xpos, int size, int width) {
+  int a = (ypos > 0) && (xpos + size < width);
+  if (size == 32 && (ypos % 64) == 32) a = 0;
+  if (size == 16 && ((ypos % 32) == 16 || ((ypos % 64) == 32 && (xpos % 32) == 16))) a = 0;
+  if (size == 8 && ((ypos % 16) == 8 || ((ypos % 32) == 16 && (xpos % 16) == 8) || ((ypos % 64) == 32 && (xpos % 32) == 24)))
+    a = 0;
+  return a;
+}
+TE_FN int te_downleft_avail(int ypos, int xpos, int size, int height) {
+  int a = (xpos > 0) && (ypos + size < height);
+  if (size == 64) a = 0;
+  if (size == 32 && (ypos % 64) == 32) a = 0;
+  if (size == 16 && ((ypos % 64) == 48 || ((ypos % 64) == 16 && (xpos % 32) == 16))) a = 0;
+  if (size == 8 && ((ypos % 64) == 56 || ((ypos % 16) == 8 && (xpos % 16) == 8) || ((ypos % 64) == 24 && (xpos % 32) == 16)))
+    a = 0;
+  return a;
+}
+
+TE_FN TeInterPred te_zero_pred() {
+  TeInterPred z;
+  z.mv0.x = z.mv0.y = z.mv1.x = z.mv1.y = 0;
+  z.ref_idx0 = z.ref_idx1 = z.bipred_flag = 0;
+  return z;
+}
+
+// get_mv_pred, common/inter_prediction.c:182-294: median of three neighbours
+// chosen by the availability pattern.
+TE_FN TeMv te_mv_pred(int ypos, int xpos, int width, int height, int size, const TeCell *db) {
+  const int bsz = size / 4, bs = width / 4, bi = (ypos / 4) * bs + xpos / 4;
+  const int up0 = bi - bs, up1 = bi - bs + (bsz - 1) / 2, up2 = bi - bs + bsz - 1;
+  const int l0 = bi - 1, l1 = bi + bs * ((bsz - 1) / 2) - 1, l2 = bi + bs * (bsz - 1) - 1;
+  const int dl = bi + bs * bsz - 1, ur = bi - bs + bsz, ul = bi - bs - 1;
+  const int U = te_up_avail(ypos), UR = te_upright_avail(ypos, xpos, size, width), L = te_left_avail(xpos),
+            DL = te_downleft_avail(ypos, xpos, size, height);
+  TeMv z;
+  z.x = z.y = 0;
+  TeMv a = z, b = z, c = z;
+  if (U == 0 && UR == 0 && L == 0 && DL == 0) {
+  } else if (U == 1 && UR == 0 && L == 0 && DL == 0) {
+    a = db[up0].ip.mv0; b = db[up1].ip.mv0; c = db[up2].ip.mv0;
+  } else if (U == 1 && UR == 1 && L == 0 && DL == 0) {
+    a = db[up0].ip.mv0; b = db[up2].ip.mv0; c = db[ur].ip.mv0;
+  } else if (U == 0 && UR == 0 && L == 1 && DL == 0) {
+    a = db[l0].ip.mv0; b = db[l1].ip.mv0; c = db[l2].ip.mv0;
+  } else if (U == 1 && UR == 0 && L == 1 && DL == 0) {
+    a = db[ul].ip.mv0; b = db[up2].ip.mv0; c = db[l2].ip.mv0;
+  } else if (U == 1 && UR == 1 && L == 1 && DL == 0) {
+    a = db[up0].ip.mv0; b = db[ur].ip.mv0; c = db[l2].ip.mv0;
+  } else if (U == 0 && UR == 0 && L == 1 && DL == 1) {
+    a = db[l0].ip.mv0; b = db[l2].ip.mv0; c = db[dl].ip.mv0;
+  } else if (U == 1 && UR == 0 && L == 1 && DL == 1) {
+    a = db[up2].ip.mv0; b = db[l0].ip.mv0; c = db[dl].ip.mv0;
+  } else if (U == 1 && UR == 1 && L == 1 && DL == 1) {
+    a = db[up0].ip.mv0; b = db[ur].ip.mv0; c = db[l0].ip.mv0;
+  }
+  TeMv p;
+  if (a.x < b.x) p.x = TE_MIN(b.x, TE_MAX(a.x, c.x));
+  else p.x = TE_MIN(a.x, TE_MAX(b.x, c.x));
+  if (a.y < b.y) p.y = TE_MIN(b.y, TE_MAX(a.y, c.y));
+  else p.y = TE_MIN(a.y, TE_MAX(b.y, c.y));
+  return p;
+}
+
+TE_FN int te_pred_equal(const TeInterPred &t, const TeInterPred &c) {
+  // duplicate test of get_mv_skip / get_mv_merge (inter_prediction.c:434-438, :587-591)
+  return t.mv0.x == c.mv0.x && t.mv0.y == c.mv0.y && t.ref_idx0 == c.ref_idx0 && t.mv1.x == c.mv1.x &&
+         t.mv1.y == c.mv1.y && t.ref_idx1 == c.ref_idx1 && (t.bipred_flag == c.bipred_flag || t.bipred_flag == -1);
+}
+
+// get_mv_skip / get_mv_merge with LIMITED_SKIP (common/global.h:81),
+// common/inter_prediction.c:449-501 / :296-348: left (bottom-most) and
+// up-right (else up, right-most) neighbours, duplicates removed.  The merge
+// list is the same derivation (both functions are identical under
+// LIMITED_SKIP; bipred_copy is unused there).
+TE_FN int te_mv_skip(int ypos, int xpos, int width, int height, int size, const TeCell *db, TeInterPred *out) {
+  const int bsz = size / 4, bs = width / 4, bi = (ypos / 4) * bs + xpos / 4;
+  int up0 = bi - bs, up2 = bi - bs + bsz - 1, l0 = bi - 1, l2 = bi + bs * (bsz - 1) - 1, ur = bi - bs + bsz;
+  const int U = te_up_avail(ypos), L = te_left_avail(xpos), UR = te_upright_avail(ypos, xpos, size, width);
+  if (ypos + size > height) l2 = l0;
+  if (xpos + size > width) up2 = up0;
+  TeInterPred t0 = L ? db[l2].ip : te_zero_pred();
+  TeInterPred t1 = UR ? db[ur].ip : (U ? db[up2].ip : te_zero_pred());
+  out[0] = t0;
+  int n = 1;
+  if (!te_pred_equal(t1, out[0])) out[n++] = t1;
+  return n;
+}
+
+// find_block_contexts, common/common_block.c:158-178
+TE_FN TeCtx te_block_ctx(int ypos, int xpos, int height, int width, int size, const TeCell *db, int enable) {
+  TeCtx c;
+  if (ypos >= 8 && xpos >= 8 && ypos + size < height && xpos + size < width && enable && size <= 64) {
+    const int bs = width / 4, bi = (ypos / 4) * bs + xpos / 4;
+    const TeCell &u = db[bi - bs], &l = db[bi - 1];
+    c.split = (u.size < size) + (l.size < size);
+    c.cbp = (u.cbp_y > 0) + (l.cbp_y > 0);
+    const int cbp2 = (u.cbp_y > 0 || u.cbp_u > 0 || u.cbp_v > 0) + (l.cbp_y > 0 || l.cbp_u > 0 || l.cbp_v > 0);
+    c.index = 3 * c.split + cbp2;
+  } else {
+    c.split = c.cbp = c.index = -1;
+  }
+  return c;
+}
+
+// add_mvcandidate, enc/encode_block.c:60-73: integer-rounded MV, deduplicated
+// by a 64-bit hash mask (hash collisions drop the candidate, as there).
+struct TeMvCand {
+  TeMv mv[TE_MAX_REF][TE_MVCAND];
+  int num[TE_MAX_REF];
+  uint64_t mask[TE_MAX_REF];
+};
+TE_FN void te_add_mvcand(TeMvCand &mc, int r, TeMv mv) {
+  TeMv im;
+  im.x = (int16_t)((mv.x + 2) >> 2);
+  im.y = (int16_t)((mv.y + 2) >> 2);
+  const uint64_t m = (uint64_t)1 << ((((int)im.y << 3) ^ (int)im.x) & 63);
+  if (!(m & mc.mask[r])) {
+    // every lane stores the same value: each lane later reads its own write,
+    // so no cross-lane ordering is needed
+    mc.mv[r][mc.num[r]] = im;
+    mc.num[r] += 1;
+  }
+  mc.mask[r] |= m;
+}
+
+// ---- block parameters (block_param_t, common/types.h:153-170) ---------------
+// Coefficients are stored compactly: per component four q x q tiles
+// (q = min(N, 16)), one per transform block (tb-split quarters in raster
+// order), row-major.  Only that low-frequency corner can be non-zero
+// (common/transform.c:309-327; quantize writes nothing else, enc/encode_block.c:170-174).
+#define TE_COEF_COMP 1024
+struct TeParam {
+  int mode, intra_mode, skip_idx, pb_part;
+  TeMv mv0[4], mv1[4];
+  int ref_idx0, ref_idx1, dir;
+  int cbp_y, cbp_u, cbp_v;
+  int tb_param, tb_split;
+  int16_t *coeff;  // 3 x TE_COEF_COMP (Y, U, V)
+};
+
+struct TeBlockInfo {  // block_info_t, enc/mainenc.h:97-116
+  int size, ypos, xpos, bwidth, bheight;
+  TeParam bp;  // block_info.block_param (the best so far)
+  TeInterPred skip_c[2], merge_c[2];
+  int num_skip, num_merge;
+  TeMv mvp;
+  int max_num_pb_part, max_num_tb_part, delta_qp, final_encode;
+  TeCtx ctx;
+  uint8_t *rec, *rec_best;  // compact Y (size^2) | U | V ((size/2)^2 each)
+};
+
+// ---- block syntax (enc/write_bits.c) --------------------------------------
+// find_code, write_bits.c:71-108
+TE_FN int te_find_code(int run, int level, int maxrun, int chroma, int eob) {
+  const int maxrun2 = TE_MAX(4, maxrun);
+  const int index = run + (level > 1) * (maxrun2 + 1);
+  if (chroma) {
+    if (eob) return 0;
+    if (index <= 4) return index + 1;
+    if (index <= maxrun2) return index + 3;
+    if (index == maxrun2 + 1) return 6;
+    if (index == maxrun2 + 2) return 7;
+    return index + 1;
+  }
+  if (eob) return 2;
+  if (index < 2) return index;
+  if (index <= 4) return index + 1;
+  if (index <= maxrun2) return index + 3;
+  if (index == maxrun2 + 1) return 6;
+  if (index == maxrun2 + 2) return 7;
+  return index + 1;
+}
+
+// write_coeff, write_bits.c:110-253: run-level VLC of one transform block's
+// q x q tile `c` (raster) of an N x N block.  Serial (lane-uniform).
+TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, int16_t *scan /* 256 scratch */) {
+  const int q = TE_MIN(16, size), N = q * q;
+  const int chroma = type & 1, intra = (type >> 1) & 1;
+  int vlc_adaptive = intra && !chroma;
+  for (int r = TE_LANE; r < N; r += TE_NL) scan[te_zz(q, r)] = c[r];
+  te_sync();
+  int pos = N - 1;
+  while (scan[pos] == 0 && pos > 0) pos--;
+  const int last_pos = pos;  // cbp != 0 guarantees a non-zero level (fatalerror otherwise, :142-143)
+  pos = 0;
+  if (chroma) {
+    if (last_pos == 0 && te_abs(scan[0]) == 1) {
+      te_put(b, 1, 1);
+      te_put(b, 1, scan[0] < 0 ? 1 : 0);
+      pos = N;
+    } else {
+      te_put(b, 1, 0);
+    }
+  }
+  int level_mode = 1, level = 1;
+  while (pos <= last_pos) {
+    if (level_mode) {
+      while (pos <= last_pos && level > 0) {
+        const int cc = scan[pos];
+        level = te_abs(cc);
+        te_put_vlc(b, vlc_adaptive, level);
+        if (level > 0) te_put(b, 1, cc < 0 ? 1 : 0);
+        if (chroma == 0) vlc_adaptive = level > 3;
+        pos++;
+      }
+    }
+    const int maxrun = N - pos - 1;
+    int run = 0, cc = 0;
+    while (cc == 0 && pos <= last_pos) {
+      cc = scan[pos];
+      if (cc == 0) {
+        run++;
+      } else {
+        level = te_abs(cc);
+        const int sign = cc < 0 ? 1 : 0;
+        const int cn = te_find_code(run, level, maxrun, chroma, 0);
+        if (chroma && size <= 8) {
+          te_put_vlc(b, 10, cn);
+        } else {
+          if (cn == 0) te_put(b, 2, 2);
+          else te_put_vlc(b, 2, cn + 1);
+        }
+        if (level > 1) te_put_vlc(b, 0, 2 * (level - 2) + sign);
+        else te_put(b, 1, sign);
+        run = 0;
+      }
+      pos++;
+      level_mode = level > 1;
+    }
+  }
+  if (pos < N) {
+    if (level_mode) {  // terminated in level mode: one extra zero before EOB (:223-236)
+      const int cc = scan[pos];
+      level = te_abs(cc);
+      te_put_vlc(b, vlc_adaptive, level);
+      if (level > 0) te_put(b, 1, cc < 0 ? 1 : 0);
+      pos++;
+    }
+  }
+  if (pos < N) {  // EOB (:238-252)
+    const int cn = te_find_code(0, 0, 0, chroma, 1);
+    if (chroma && size <= 8) {
+      te_put_vlc(b, 0, cn);
+    } else {
+      if (cn == 0) te_put(b, 2, 2);
+      else te_put_vlc(b, 2, cn + 1);
+    }
+  }
+  te_sync();  // `scan` is reused by the next call
+}
+
+// write_delta_qp, write_bits.c:255-265
+TE_FN void te_write_delta_qp(TeBits &b, int dqp) {
+  te_put_vlc(b, 0, te_abs(dqp));
+  if (dqp != 0) te_put(b, 1, dqp < 0 ? 1 : 0);
+}
+
+// write_super_mode, write_bits.c:268-362
+TE_FN void te_write_super_mode(TeBits &b, const TeFrame &F, const TeBlockInfo &bi, int mode, int ref_idx0,
+                               int split_flag) {
+  const int size = bi.size;
+  if (F.frame_type != TE_I) {
+    if (split_flag == 1) {
+      if (size > 64) {
+        te_put(b, 1, 0);
+      } else {
+        int code = 1;
+        if (bi.ctx.index == 2 || bi.ctx.index > 3) code = (code + 3) % 4;
+        te_put(b, code + 1, 1);
+      }
+      return;
+    }
+    int code = 0;
+    const int bipred_possible = F.num_ref > 1 && F.enable_bipred;
+    const int split_possible = size > 8;
+    const int maxbit = 2 + F.num_ref + split_possible + bipred_possible;
+    if (F.interp_ref) {
+      if (mode == TE_SKIP) code = 0;
+      else if (mode == TE_MERGE) code = 2;
+      else if (mode == TE_BIPRED) code = 3;
+      else if (mode == TE_INTRA) code = 4;
+      else if (mode == TE_INTER && ref_idx0 > 0) code = 4 + ref_idx0;
+      else code = 4 + F.num_ref;
+      if (!bipred_possible && code > 3) code = code - 1;
+      if (!split_possible && code > 1) code = code - 1;
+      if ((bi.ctx.index == 2 || bi.ctx.index > 3) && size > 8) {
+        if (code < 3) code = (code + 2) % 3;
+      }
+    } else {
+      if (mode == TE_SKIP) code = 0;
+      else if (mode == TE_INTER && ref_idx0 == 0) code = 2;
+      else if (mode == TE_MERGE) code = 3;
+      else if (mode == TE_BIPRED) code = 4;
+      else if (mode == TE_INTRA) code = 5;
+      else if (mode == TE_INTER && ref_idx0 > 0) code = 5 + ref_idx0;
+      if (!bipred_possible && code > 4) code = code - 1;
+      if (!split_possible && code > 1) code = code - 1;
+      if ((bi.ctx.index == 2 || bi.ctx.index > 3) && size > 8) {
+        if (code < 4) code = (code + 3) % 4;
+      }
+    }
+    if (code == maxbit) te_put(b, maxbit, 0);
+    else te_put(b, code + 1, 1);
+  } else {
+    if (size > 8 || split_flag == 1) te_put(b, 1, split_flag);
+  }
+}
+
+TE_FN const int16_t *te_tile(const TeParam &p, int comp, int idx) { return p.coeff + comp * TE_COEF_COMP + idx * 256; }
+
+// write_block, write_bits.c:364-650.  Returns the number of bits written.
+TE_NOINL int te_write_block(TeBits &b, const TeFrame &F, const TeBlockInfo &bi, const TeParam &p, int16_t *scan) {
+  const int start = b.pos;
+  const int size = bi.size, mode = p.mode, tb_split = p.tb_split;
+  const int coeff_type = (mode == TE_INTRA) << 1;
+  const int cbp_table[8] = {1, 0, 5, 2, 6, 3, 7, 4};
+  te_write_super_mode(b, F, bi, mode, p.ref_idx0, 0);
+  if (size == 64 && mode != TE_SKIP && F.max_delta_qp) te_write_delta_qp(b, bi.delta_qp);
+  if (mode == TE_INTRA) {
+    const int im = p.intra_mode;
+    if (F.num_intra_modes <= 4) {
+      te_put(b, 2, im);
+    } else if (F.num_intra_modes <= 8) {
+      const int map[10] = {2, 8, 1, 0, 5, 9, 7, 6, 4, 3};
+      const int len[8] = {2, 2, 2, 4, 4, 4, 5, 5}, cw[8] = {0, 1, 2, 12, 13, 14, 30, 31};
+      const int code = map[im];
+      te_put(b, len[code], cw[code]);
+    } else {
+      const int map[10] = {2, 3, 1, 0, 6, 9, 8, 7, 5, 4};
+      const int len[10] = {2, 2, 3, 3, 4, 4, 5, 5, 5, 5}, cw[10] = {2, 3, 2, 3, 2, 3, 0, 1, 2, 3};
+      const int code = map[im];
+      te_put(b, len[code], cw[code]);
+    }
+  } else if (mode == TE_INTER) {
+    if (bi.max_num_pb_part > 1) {
+      if (p.pb_part == 0) te_put(b, 1, 1);
+      else if (p.pb_part == 1) te_put(b, 2, 1);
+      else if (p.pb_part == 2) te_put(b, 3, 1);
+      else te_put(b, 3, 0);
+    }
+    TeMv mvp2 = bi.mvp;
+    if (p.pb_part == 0) {
+      te_write_mv(b, p.mv0[0], mvp2);
+    } else if (p.pb_part == 1) {
+      te_write_mv(b, p.mv0[0], mvp2);
+      mvp2 = p.mv0[0];
+      te_write_mv(b, p.mv0[2], mvp2);
+    } else if (p.pb_part == 2) {
+      te_write_mv(b, p.mv0[0], mvp2);
+      mvp2 = p.mv0[0];
+      te_write_mv(b, p.mv0[1], mvp2);
+    } else {
+      te_write_mv(b, p.mv0[0], mvp2);
+      mvp2 = p.mv0[0];
+      te_write_mv(b, p.mv0[1], mvp2);
+      te_write_mv(b, p.mv0[2], mvp2);
+      te_write_mv(b, p.mv0[3], mvp2);
+    }
+  } else if (mode == TE_BIPRED) {  // BIPRED_PART 0 (common/global.h:76)
+    TeMv mvp2 = bi.mvp;
+    if (p.pb_part == 0) te_write_mv(b, p.mv0[0], mvp2);
+    if (F.frame_type == TE_B) mvp2 = p.mv0[0];
+    if (p.pb_part == 0) {
+      te_write_mv(b, p.mv1[0], mvp2);
+    } else if (p.pb_part == 1) {
+      te_write_mv(b, p.mv1[0], mvp2);
+      mvp2 = p.mv1[0];
+      te_write_mv(b, p.mv1[2], mvp2);
+    } else if (p.pb_part == 2) {
+      te_write_mv(b, p.mv1[0], mvp2);
+      mvp2 = p.mv1[0];
+      te_write_mv(b, p.mv1[1], mvp2);
+    } else {
+      te_write_mv(b, p.mv1[0], mvp2);
+      mvp2 = p.mv1[0];
+      te_write_mv(b, p.mv1[1], mvp2);
+      te_write_mv(b, p.mv1[2], mvp2);
+      te_write_mv(b, p.mv1[3], mvp2);
+    }
+    if (F.frame_type == TE_P) {
+      if (F.num_ref == 2) {
+        const int code = 2 * p.ref_idx0 + p.ref_idx1;
+        if (code == 3) te_put(b, 3, 0);
+        else te_put(b, code + 1, 1);
+      } else {
+        te_put_vlc(b, 10, 4 * p.ref_idx0 + p.ref_idx1);
+      }
+    }
+  } else if (mode == TE_SKIP) {
+    if (bi.num_skip == 4) {
+      te_put(b, 2, p.skip_idx);
+    } else if (bi.num_skip == 3) {
+      if (p.skip_idx == 0) te_put(b, 1, 1);
+      else if (p.skip_idx == 1) te_put(b, 2, 0);
+      else te_put(b, 2, 1);
+    } else if (bi.num_skip == 2) {
+      te_put(b, 1, p.skip_idx);
+    }
+  } else if (mode == TE_MERGE) {
+    if (bi.num_merge == 4) {
+      te_put(b, 2, p.skip_idx);
+    } else if (bi.num_merge == 3) {
+      if (p.skip_idx == 0) te_put(b, 1, 1);
+      else if (p.skip_idx == 1) te_put(b, 2, 0);
+      else te_put(b, 2, 1);
+    } else if (bi.num_merge == 2) {
+      te_put(b, 1, p.skip_idx);
+    }
+  }
+  if (mode != TE_SKIP) {
+    int max_tb = 1, code;
+    if (mode == TE_MERGE || mode == TE_BIPRED) max_tb = 1;
+    else if (mode == TE_INTER) max_tb = bi.max_num_tb_part > 1 ? 2 : 1;
+    else if (mode == TE_INTRA) max_tb = bi.max_num_tb_part;
+    if (max_tb > 1) {
+      if (tb_split) {
+        code = 2;
+      } else {
+        const int cbp = p.cbp_y + (p.cbp_u << 1) + (p.cbp_v << 2);
+        code = cbp_table[cbp];
+        if (bi.ctx.cbp == 0 && code < 2) code = 1 - code;
+        if (code > 1) code++;
+      }
+    } else {
+      const int cbp = p.cbp_y + (p.cbp_u << 1) + (p.cbp_v << 2);
+      code = cbp_table[cbp];
+      if (mode == TE_MERGE) {
+        if (code == 1) code = 7;
+        else if (code > 1) code = code - 1;
+      } else {
+        if (bi.ctx.cbp == 0 && code < 2) code = 1 - code;
+      }
+    }
+    te_put_vlc(b, 0, code);
+    if (tb_split == 0) {
+      if (p.cbp_y) te_write_coeff(b, te_tile(p, 0, 0), size, coeff_type | 0, scan);
+      if (p.cbp_u) te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1, scan);
+      if (p.cbp_v) te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1, scan);
+    } else if (size > 8) {
+      for (int index = 0; index < 4; index++) {
+        const int cy = (p.cbp_y >> (3 - index)) & 1, cu = (p.cbp_u >> (3 - index)) & 1,
+                  cv = (p.cbp_v >> (3 - index)) & 1;
+        code = cbp_table[cy + (cu << 1) + (cv << 2)];
+        if (bi.ctx.cbp == 0 && code < 2) code = 1 - code;
+        te_put_vlc(b, 0, code);
+        if (cy) te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0, scan);
+        if (cu) te_write_coeff(b, te_tile(p, 1, index), size / 4, coeff_type | 1, scan);
+        if (cv) te_write_coeff(b, te_tile(p, 2, index), size / 4, coeff_type | 1, scan);
+      }
+    } else {
+      for (int index = 0; index < 4; index++) {
+        const int cy = (p.cbp_y >> (3 - index)) & 1;
+        te_put(b, 1, cy);
+        if (cy) te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0, scan);
+      }
+      // chroma of an 8x8 CU is not split: cbp_u / cbp_v are the block values here
+      const int cbp = p.cbp_u + 2 * p.cbp_v;
+      if (cbp == 0) te_put(b, 1, 1);
+      else if (cbp == 1) te_put(b, 2, 1);
+      else if (cbp == 2) te_put(b, 3, 1);
+      else te_put(b, 3, 0);
+      if (p.cbp_u) te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1, scan);
+      if (p.cbp_v) te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1, scan);
+    }
+  }
+  return b.pos - start;
+}

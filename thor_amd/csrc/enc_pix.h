@@ -1,0 +1,643 @@
+// Device-resident Thor encoder, part 2: SPMD pixel kernels (motion
+// compensation, SAD / SSD and the fast sub-pel searches, intra prediction,
+// residual, forward / inverse transform, quantisation).  Lane-parallel loops
+// over the block, wave reductions for the sums; every producer ends with
+// te_sync() so any lane may read its output.  See enc_core.h for the model.
+#pragma once
+#include "enc_core.h"
+
+// HEVC integer DCT basis (g*mat_hevc, common/transform.c:41-245): row k of the
+// N-point matrix is row k*32/N of the 32-point matrix.
+struct TeDct {
+  int8_t m[32][32];
+  constexpr TeDct() : m() {
+    const int c[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                       61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+    for (int k = 0; k < 32; k++)
+      for (int n = 0; n < 32; n++) {
+        int v = 64;
+        if (k == 0) v = 64;
+        else {
+          const int t = (k * (2 * n + 1)) % 128;
+          v = t <= 32 ? c[t] : (t <= 64 ? -c[64 - t] : (t <= 96 ? -c[t - 64] : c[128 - t]));
+        }
+        m[k][n] = (int8_t)v;
+      }
+  }
+};
+TE_CONST TeDct te_dct = TeDct();
+TE_FN int te_dctN(int N, int k, int n) { return te_dct.m[k * (32 / N)][n]; }
+
+// 6-tap luma (uni-pred / enable_bipred tables) and 4-tap chroma filters,
+// common/inter_prediction.c:47-70
+TE_CONST int8_t te_luma_uni[4][6] = {{0, 0, 64, 0, 0, 0}, {1, -7, 55, 19, -5, 1}, {1, -7, 38, 38, -7, 1}, {1, -5, 19, 55, -7, 1}};
+TE_CONST int8_t te_luma_bi[4][6] = {{0, 0, 64, 0, 0, 0}, {2, -10, 59, 17, -5, 1}, {1, -8, 39, 39, -8, 1}, {1, -5, 17, 59, -10, 2}};
+TE_CONST int8_t te_chroma_f[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-4, 44, 28, -4},
+                                     {-4, 36, 36, -4}, {-4, 28, 44, -4}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+
+// get_inter_prediction_luma, common/inter_prediction.c:120-180 (its SIMD
+// dispatch, common/common_kernels.c:165-784, computes the same values):
+// `ref` points at the block's co-located position in the padded reference.
+TE_FN void te_mc_luma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, int h, TeMv mv, int sign, int bipred) {
+  const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
+  const int fy = my & 3, fx = mx & 3;
+  const uint8_t *r = ref + (my >> 2) * rs + (mx >> 2);
+  const int n = w * h;
+  if (!fx && !fy) {
+    for (int e = TE_LANE; e < n; e += TE_NL) {
+      const int i = e / w, j = e - (e / w) * w;
+      dst[i * ds + j] = r[i * rs + j];
+    }
+  } else if (fx == 2 && fy == 2) {  // (2,2): 4x4 low-pass centre, :145-157
+    for (int e = TE_LANE; e < n; e += TE_NL) {
+      const int i = e / w, j = e - (e / w) * w;
+      const uint8_t *p = r + i * rs + j;
+      int s = p[-rs] + p[-rs + 1] + p[-1] + 2 * p[0] + 2 * p[1] + p[2] + p[rs - 1] + 2 * p[rs] + 2 * p[rs + 1] + p[rs + 2] +
+              p[2 * rs] + p[2 * rs + 1];
+      dst[i * ds + j] = (uint8_t)te_clip255((s + 8) >> 4);
+    }
+  } else {  // separable 6-tap, exact 32-bit sums, clip255((s + 2048) >> 12)
+    const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
+    const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
+    for (int e = TE_LANE; e < n; e += TE_NL) {
+      const int i = e / w, j = e - (e / w) * w;
+      const uint8_t *p = r + (i - 2) * rs + j - 2;
+      int s = 0;
+      for (int m = 0; m < 6; m++) {
+        int t = 0;
+        for (int k = 0; k < 6; k++) t += fv[k] * p[k * rs + m];
+        s += fh[m] * t;
+      }
+      dst[i * ds + j] = (uint8_t)te_clip255((s + 2048) >> 12);
+    }
+  }
+  te_sync();
+}
+
+// get_inter_prediction_chroma, common/inter_prediction.c:72-118: the luma MV
+// read as 1/8-pel on the chroma plane.
+TE_FN void te_mc_chroma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, int h, TeMv mv, int sign) {
+  const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
+  const int fy = my & 7, fx = mx & 7;
+  const uint8_t *r = ref + (my >> 3) * rs + (mx >> 3);
+  const int n = w * h;
+  if (!fx && !fy) {
+    for (int e = TE_LANE; e < n; e += TE_NL) {
+      const int i = e / w, j = e - (e / w) * w;
+      dst[i * ds + j] = r[i * rs + j];
+    }
+  } else {
+    const int8_t *fh = te_chroma_f[fx], *fv = te_chroma_f[fy];
+    for (int e = TE_LANE; e < n; e += TE_NL) {
+      const int i = e / w, j = e - (e / w) * w;
+      const uint8_t *p = r + (i - 1) * rs + j - 1;
+      int s = 0;
+      for (int m = 0; m < 4; m++) {
+        int t = 0;
+        for (int k = 0; k < 4; k++) t += fh[k] * p[m * rs + k];
+        s += fv[m] * t;
+      }
+      dst[i * ds + j] = (uint8_t)te_clip255((s + 2048) >> 12);
+    }
+  }
+  te_sync();
+}
+
+// sad_calc (enc/encode_block.c:740-755) / ssd_calc (:782-797): exact sums
+TE_FN uint32_t te_sad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
+  uint32_t s = 0;
+  for (int e = TE_LANE; e < w * h; e += TE_NL) {
+    const int i = e / w, j = e - (e / w) * w;
+    s += (uint32_t)te_abs((int)a[i * as + j] - (int)b[i * bs + j]);
+  }
+  return te_sum(s);
+}
+TE_FN uint32_t te_ssd(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
+  uint32_t s = 0;
+  for (int e = TE_LANE; e < w * h; e += TE_NL) {
+    const int i = e / w, j = e - (e / w) * w;
+    const int d = (int)a[i * as + j] - (int)b[i * bs + j];
+    s += (uint32_t)(d * d);
+  }
+  return te_sum(s);
+}
+
+// widesad_calc, enc/encode_block.c:757-780 (its SIMD form widesad_calc_simd,
+// enc/enc_kernels.c:71-98, keeps the first minimum too): SAD at horizontal
+// offsets -3, -1, 0, 1, 3; returns the best, *x = its offset.
+TE_FN uint32_t te_widesad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h, int *x) {
+  const int off[5] = {-3, -1, 0, 1, 3};
+  uint32_t s[5] = {0, 0, 0, 0, 0};
+  for (int e = TE_LANE; e < w * h; e += TE_NL) {
+    const int i = e / w, j = e - (e / w) * w;
+    const int av = a[i * as + j];
+    for (int k = 0; k < 5; k++) s[k] += (uint32_t)te_abs(av - (int)b[i * bs + j + off[k]]);
+  }
+  uint32_t best = 0;
+  int bx = 0;
+  for (int k = 0; k < 5; k++) {
+    const uint32_t v = te_sum(s[k]);
+    if (k == 0 || v < best) {
+      best = v;
+      bx = off[k];
+    }
+  }
+  *x = bx;
+  return best;
+}
+
+// sad_calc_fasthalf, enc/encode_block.c:497-605 (== sad_calc_fasthalf_simd):
+// eight approximate half-pel positions from rounding averages around `b`.
+TE_FN uint32_t te_fasthalf(const uint8_t *a, int as, const uint8_t *b, int bs, int width, int height, int *x, int *y) {
+  uint32_t tl = 0, tr = 0, br = 0, bl = 0, top = 0, right = 0, down = 0, left = 0;
+  for (int e = TE_LANE; e < width * height; e += TE_NL) {
+    const int i = e / width, j = e - (e / width) * width;
+    const uint8_t *q = b + i * bs;
+    const int A = a[i * as + j];
+    int t1, t2, t3, t4, t5, t6, t7, t8, ptl, ptr, pbr, pbl;
+    t1 = (q[-bs + j - 1] + q[-bs + j] + 1) >> 1;
+    t2 = (q[j - 1] + q[j] + 1) >> 1;
+    t1 = (t1 + t2) >> 1;
+    t3 = (q[-2 * bs + j - 1] + q[bs + j - 1] + 1) >> 1;
+    t4 = (q[-2 * bs + j] + q[bs + j] + 1) >> 1;
+    t3 = (t3 + t4) >> 1;
+    t5 = (q[-bs + j - 2] + q[-bs + j + 1] + 1) >> 1;
+    t6 = (q[j - 2] + q[j + 1] + 1) >> 1;
+    t5 = (t5 + t6) >> 1;
+    t5 = (t3 + t5) >> 1;
+    ptl = (t5 + t1) >> 1;
+    left += (uint32_t)te_abs(A - t2);
+
+    t1 = (q[-bs + j] + q[-bs + j + 1] + 1) >> 1;
+    t8 = (q[j] + q[j + 1] + 1) >> 1;
+    t1 = (t1 + t8) >> 1;
+    t5 = (q[-2 * bs + j + 1] + q[bs + j + 1] + 1) >> 1;
+    t3 = (t4 + t5) >> 1;
+    t4 = (q[-bs + j - 1] + q[-bs + j + 2] + 1) >> 1;
+    t7 = (q[j - 1] + q[j + 2] + 1) >> 1;
+    t5 = (t7 + t4) >> 1;
+    t5 = (t3 + t5) >> 1;
+    ptr = (t5 + t1) >> 1;
+    right += (uint32_t)te_abs(A - t8);
+
+    t1 = (q[bs + j - 1] + q[bs + j] + 1) >> 1;
+    t3 = (t1 + t2) >> 1;
+    t2 = (q[-bs + j - 1] + q[2 * bs + j - 1] + 1) >> 1;
+    t4 = (q[-bs + j] + q[2 * bs + j] + 1) >> 1;
+    t5 = (t4 + t2) >> 1;
+    t1 = (q[bs + j - 2] + q[bs + j + 1] + 1) >> 1;
+    t2 = (t6 + t1) >> 1;
+    t2 = (t5 + t2) >> 1;
+    pbl = (t2 + t3) >> 1;
+
+    t2 = (q[bs + j] + q[bs + j + 1] + 1) >> 1;
+    t3 = (t8 + t2) >> 1;
+    t5 = (q[-bs + j + 1] + q[2 * bs + j + 1] + 1) >> 1;
+    t6 = (t4 + t5) >> 1;
+    t8 = (q[bs + j - 1] + q[bs + j + 2] + 1) >> 1;
+    t1 = (t7 + t8) >> 1;
+    t2 = (t6 + t1) >> 1;
+    pbr = (t2 + t3) >> 1;
+
+    down += (uint32_t)te_abs(A - ((q[j] + q[j + bs] + 1) >> 1));
+    top += (uint32_t)te_abs(A - ((q[j] + q[j - bs] + 1) >> 1));
+    tl += (uint32_t)te_abs(A - ptl);
+    tr += (uint32_t)te_abs(A - ptr);
+    br += (uint32_t)te_abs(A - pbr);
+    bl += (uint32_t)te_abs(A - pbl);
+  }
+  tl = te_sum(tl); tr = te_sum(tr); br = te_sum(br); bl = te_sum(bl);
+  top = te_sum(top); right = te_sum(right); down = te_sum(down); left = te_sum(left);
+  int bestx = 0, besty = -2;
+  if (down < top) { besty = 2; top = down; }
+  if (right < top) { bestx = 2; besty = 0; top = right; }
+  if (left < top) { bestx = -2; besty = 0; top = left; }
+  if (tl < top) { bestx = -2; besty = -2; top = tl; }
+  if (tr < top) { bestx = 2; besty = -2; top = tr; }
+  if (br < top) { bestx = 2; besty = 2; top = br; }
+  if (bl < top) { bestx = -2; besty = 2; top = bl; }
+  *x = bestx;
+  *y = besty;
+  return top;
+}
+
+// sad_calc_fastquarter, enc/encode_block.c:609-738 (== the SIMD form): eight
+// approximate quarter-pel positions around the half-pel position (*x, *y) in,
+// the best offset out.
+TE_FN uint32_t te_fastquarter(const uint8_t *o, int os, const uint8_t *r, int rs, int width, int height, int *x, int *y) {
+  uint32_t tl = 0, tr = 0, br = 0, bl = 0, top = 0, right = 0, down = 0, left = 0;
+  const int X = *x, Y = *y;
+  for (int e = TE_LANE; e < width * height; e += TE_NL) {
+    const int i = e / width, j = e - (e / width) * width;
+    const uint8_t *q = r + i * rs;
+    const int O = o[i * os + j];
+    if (X & Y) {
+      const int a = q[j], d = q[j + 1], ee = q[j + rs + 1], f = q[j + rs];
+      const int ad = (a + d + 1) >> 1, de = (d + ee + 1) >> 1, af = (a + f + 1) >> 1, fe = (f + ee + 1) >> 1;
+      tl += te_abs(O - ((ad + af) >> 1));
+      top += te_abs(O - ((de + a) >> 1));
+      tr += te_abs(O - ((ad + de) >> 1));
+      left += te_abs(O - ((ad + f) >> 1));
+      right += te_abs(O - ((ad + ee) >> 1));
+      bl += te_abs(O - ((af + fe) >> 1));
+      down += te_abs(O - ((de + f) >> 1));
+      br += te_abs(O - ((de + fe) >> 1));
+    } else if (X) {
+      const int a = q[j], b = q[j - rs], c = q[j - rs + 1], d = q[j + 1], ee = q[j + rs + 1], f = q[j + rs];
+      const int ad = (a + d + 1) >> 1, de = (d + ee + 1) >> 1, dc = (d + c + 1) >> 1, af = (a + f + 1) >> 1,
+                ab = (a + b + 1) >> 1;
+      tl += te_abs(O - ((ad + ab) >> 1));
+      top += te_abs(O - ((dc + a) >> 1));
+      tr += te_abs(O - ((ad + dc) >> 1));
+      left += te_abs(O - ((ad + a) >> 1));
+      right += te_abs(O - ((ad + d) >> 1));
+      bl += te_abs(O - ((ad + af) >> 1));
+      down += te_abs(O - ((af + d) >> 1));
+      br += te_abs(O - ((ad + de) >> 1));
+    } else if (Y) {
+      const int a = q[j], d = q[j + 1], ee = q[j + rs + 1], f = q[j + rs], g = q[j + rs - 1], h = q[j - 1];
+      const int ad = (a + d + 1) >> 1, af = (a + f + 1) >> 1, fe = (f + ee + 1) >> 1, ah = (a + h + 1) >> 1,
+                gf = (g + f + 1) >> 1;
+      tl += te_abs(O - ((ah + af) >> 1));
+      top += te_abs(O - ((af + a) >> 1));
+      tr += te_abs(O - ((ad + af) >> 1));
+      left += te_abs(O - ((gf + a) >> 1));
+      right += te_abs(O - ((ad + f) >> 1));
+      bl += te_abs(O - ((af + gf) >> 1));
+      down += te_abs(O - ((af + f) >> 1));
+      br += te_abs(O - ((af + fe) >> 1));
+    } else {
+      const int a = q[j], b = q[j - rs], d = q[j + 1], f = q[j + rs], h = q[j - 1];
+      const int ad = (a + d + 1) >> 1, af = (a + f + 1) >> 1, ah = (a + h + 1) >> 1, ab = (a + b + 1) >> 1;
+      tl += te_abs(O - ((ah + ab) >> 1));
+      top += te_abs(O - ((ab + a) >> 1));
+      tr += te_abs(O - ((ad + ab) >> 1));
+      left += te_abs(O - ((ah + a) >> 1));
+      right += te_abs(O - ((ad + a) >> 1));
+      bl += te_abs(O - ((ah + af) >> 1));
+      down += te_abs(O - ((af + a) >> 1));
+      br += te_abs(O - ((af + ad) >> 1));
+    }
+  }
+  tl = te_sum(tl); tr = te_sum(tr); br = te_sum(br); bl = te_sum(bl);
+  top = te_sum(top); right = te_sum(right); down = te_sum(down); left = te_sum(left);
+  int bestx = 0, besty = -1;
+  if (tl < top) { bestx = -1; top = tl; }
+  if (tr < top) { bestx = 1; top = tr; }
+  if (left < top) { bestx = -1; besty = 0; top = left; }
+  if (right < top) { bestx = 1; besty = 0; top = right; }
+  if (bl < top) { bestx = -1; besty = 1; top = bl; }
+  if (down < top) { bestx = 0; besty = 1; top = down; }
+  if (br < top) { bestx = 1; besty = 1; top = br; }
+  *x = bestx;
+  *y = besty;
+  return top;
+}
+
+// ---- intra prediction (common/intra_prediction.c) ---------------------------
+// Neighbour arrays: left[0..2n), top[0..2n), *tl.  Built by make_top_and_left
+// (:57-143): `rf` = frame pixel at the CU origin (stride fs), `rb` = compact
+// reconstructed block at the sub-TU origin (stride rbs) for tb-split TUs.
+struct TeNbr {
+  uint8_t left[2 * 64 + 2], top[2 * 64 + 2];
+  uint8_t lF[2 * 64 + 2], tF[2 * 64 + 2];  // 1-2-1 filtered copies
+  int T[64], L[64];                        // planar edge sums
+  int tl, tlF, TL;
+};
+TE_FN void te_make_top_and_left(TeNbr &nb, const uint8_t *rf, int fs, const uint8_t *rb, int rbs, int i, int j, int ypos,
+                                int xpos, int size, int cb_ur, int cb_dl, int tb_split) {
+  int dl, ur;
+  if (!tb_split) {
+    dl = cb_dl;
+    ur = cb_ur;
+  } else {
+    dl = (j == 0 && (i == 0 || cb_dl)) ? 1 : 0;
+    ur = (j == 0 || (i == 0 && cb_ur)) ? 1 : 0;
+  }
+  const int leftlen = dl ? size + 1 : size, toplen = ur ? size + 1 : size;
+  // top row source
+  const int top128 = tb_split ? (ypos + i == 0) : (ypos == 0);
+  const uint8_t *tsrc = (!tb_split || i == 0) ? rf - fs + (tb_split ? j : 0) : rb - rbs;
+  const int left128 = tb_split ? (xpos + j == 0) : (xpos == 0);
+  const uint8_t *lsrc;  // left column pointer, stride ls
+  int ls;
+  if (!tb_split || j == 0) {
+    lsrc = rf + (tb_split ? i * fs : 0) - 1;
+    ls = fs;
+  } else {
+    lsrc = rb - 1;
+    ls = rbs;
+  }
+  for (int k = TE_LANE; k < 2 * size; k += TE_NL) {
+    nb.top[k] = top128 ? 128 : tsrc[k < toplen ? k : toplen - 1];
+    nb.left[k] = left128 ? 128 : lsrc[(k < leftlen ? k : leftlen - 1) * ls];
+  }
+  // top-left
+  int tl;
+  if (top128) tl = 128;
+  else if (!tb_split || i == 0) tl = xpos > 0 ? rf[-fs + (tb_split ? j : 0) - 1] : tsrc[0];
+  else tl = xpos > 0 ? (j > 0 ? rb[-rbs - 1] : rf[(i - 1) * fs - 1]) : tsrc[0];
+  if (top128) tl = left128 ? 128 : lsrc[0];  // `if (ypos[+i]==0) *top_left = left[0]`
+  nb.tl = tl;
+  te_sync();
+}
+
+// filter_121 (:39-48) of in[0..len) into out
+TE_FN void te_f121(const uint8_t *in, uint8_t *out, int len) {
+  for (int j = TE_LANE; j < len; j += TE_NL) {
+    int v;
+    if (j == 0) v = (3 * in[0] + in[1] + 2) >> 2;
+    else if (j == len - 1) v = (in[len - 2] + 3 * in[len - 1] + 2) >> 2;
+    else v = (in[j - 1] + 2 * in[j] + in[j + 1] + 2) >> 2;
+    out[j] = (uint8_t)v;
+  }
+}
+
+// get_intra_prediction (:363-388) and the mode functions (:145-361) into a
+// compact n x n block.  search_dc: search_intra_prediction_params' DC
+// (enc/encode_block.c:1250, always (left, top)) instead of the position-aware one.
+TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int mode, int search_dc) {
+  const int nn = n * n;
+  switch (mode) {
+    case TE_PLANAR: {  // :182-214, C division truncating toward zero
+      for (int k = TE_LANE; k < 2 * n; k += TE_NL) {
+        const int s = k >= n, jj = k - s * n;
+        const uint8_t *a = s ? nb.left : nb.top;
+        int v;
+        if (jj == 0) v = 3 * a[0] + 2 * a[0] + 2 * a[1] + a[2];
+        else if (jj == 1) v = a[0] + 2 * a[0] + 2 * a[1] + 2 * a[2] + a[3];
+        else if (jj == n - 2) v = a[n - 4] + 2 * a[n - 3] + 2 * a[n - 2] + 2 * a[n - 1] + a[n - 1];
+        else if (jj == n - 1) v = a[n - 3] + 2 * a[n - 2] + 2 * a[n - 1] + 3 * a[n - 1];
+        else v = a[jj - 2] + 2 * a[jj - 1] + 2 * a[jj] + 2 * a[jj + 1] + a[jj + 2];
+        (s ? nb.L : nb.T)[jj] = v;
+      }
+      te_sync();
+      const int TL = nb.left[1] + 2 * nb.left[0] + 2 * nb.tl + 2 * nb.top[0] + nb.top[1];
+      for (int e = TE_LANE; e < nn; e += TE_NL) {
+        const int i = e / n, j = e - (e / n) * n;
+        pb[e] = (uint8_t)te_clip255((nb.L[i] + nb.T[j] - TL + 4) / 8);
+      }
+      break;
+    }
+    case TE_HOR:
+      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.left[e / n];
+      break;
+    case TE_VER:
+      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.top[e - (e / n) * n];
+      break;
+    case TE_UPLEFT:
+    case TE_UPUPLEFT:
+    case TE_UPLEFTLEFT: {
+      te_f121(nb.left, nb.lF, n);
+      te_f121(nb.top, nb.tF, n);
+      const int tlF = (2 * nb.tl + nb.left[0] + nb.top[0] + 2) >> 2;
+      te_sync();
+      for (int e = TE_LANE; e < nn; e += TE_NL) {
+        const int i = e / n, j = e - (e / n) * n;
+        int v;
+        if (mode == TE_UPLEFT) {  // :216-240
+          const int d = i - j;
+          v = d > 0 ? nb.lF[d - 1] : (d == 0 ? tlF : nb.tF[-d - 1]);
+        } else if (mode == TE_UPUPLEFT) {  // :279-307
+          const int d = i - 2 * j;
+          if (d > 1) v = nb.lF[d - 2];
+          else if (d == 1) v = tlF;
+          else if (d == 0) v = (tlF + nb.tF[0]) >> 1;
+          else if (d & 1) v = nb.tF[(-d) / 2];
+          else v = (nb.tF[(-d) / 2] + nb.tF[(-d) / 2 - 1]) >> 1;
+        } else {  // :309-337
+          const int d = 2 * i - j;
+          if (d < -1) v = nb.tF[-d - 2];
+          else if (d == -1) v = tlF;
+          else if (d == 0) v = (tlF + nb.lF[0]) >> 1;
+          else if (d & 1) v = nb.lF[d / 2];
+          else v = (nb.lF[d / 2] + nb.lF[d / 2 - 1]) >> 1;
+        }
+        pb[e] = (uint8_t)v;
+      }
+      break;
+    }
+    case TE_UPRIGHT:
+    case TE_UPUPRIGHT: {
+      te_f121(nb.top, nb.tF, 2 * n);
+      te_sync();
+      for (int e = TE_LANE; e < nn; e += TE_NL) {
+        const int i = e / n, j = e - (e / n) * n;
+        if (mode == TE_UPRIGHT) {  // :242-256
+          pb[e] = nb.tF[i + j + 1];
+        } else {  // :258-277
+          const int d = i + 2 * j;
+          pb[e] = (d & 1) ? nb.tF[(d + 1) / 2] : (uint8_t)((nb.tF[d / 2] + nb.tF[d / 2 + 1]) >> 1);
+        }
+      }
+      break;
+    }
+    case TE_DOWNLEFTLEFT: {  // :339-361
+      te_f121(nb.left, nb.lF, 2 * n);
+      te_sync();
+      for (int e = TE_LANE; e < nn; e += TE_NL) {
+        const int i = e / n, j = e - (e / n) * n;
+        const int d = 2 * i + j;
+        pb[e] = (d & 1) ? nb.lF[(d + 1) / 2] : (uint8_t)((nb.lF[d / 2] + nb.lF[d / 2 + 1]) >> 1);
+      }
+      break;
+    }
+    default: {  // DC, :145-160 (and out-of-range modes, :386-387)
+      const uint8_t *a = (search_dc || xpos != 0) ? nb.left : nb.top;
+      const uint8_t *b = (search_dc || ypos != 0) ? nb.top : nb.left;
+      uint32_t s = 0;
+      for (int k = TE_LANE; k < n; k += TE_NL) s += a[k] + b[k];
+      s = te_sum(s);
+      const int dc = ((int)s + n) / (2 * n);
+      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = (uint8_t)dc;
+      break;
+    }
+  }
+  te_sync();
+}
+
+// ---- transform chain -----------------------------------------------------------
+// Scratch of one transform block (compact, q = min(N, 16)).
+struct TeTx {
+  int16_t R[64 * 64];  // residual (N x N), reconstructed residual
+  int16_t A[32 * 32];  // pre-summed input of the 32 / 64 paths
+  int16_t T[32 * 32];  // pass-1 output
+  int C[256];          // q x q coefficients / levels (raster)
+  int S[256];          // levels in scan order
+  int O[256];          // coefficients in scan order (RDOQ light)
+  int16_t scan[256];   // write_coeff scratch
+};
+
+// One output of the reference SIMD 8-point forward pass (transform8,
+// common/common_kernels.c:1887-1967): 16-bit wrapping butterflies.
+TE_FN int te_fwd8(const int16_t *s, int k, int shift) {
+  int E[4], O[4];
+  for (int m = 0; m < 4; m++) {
+    E[m] = te_wrap16(s[m] + s[7 - m]);
+    O[m] = te_wrap16(s[m] - s[7 - m]);
+  }
+  const int EO0 = te_wrap16(E[0] - E[3]), EO1 = te_wrap16(E[1] - E[2]);
+  int v;
+  switch (k) {
+    case 0: v = 64 * E[0] + 64 * E[1] + 64 * E[2] + 64 * E[3]; break;
+    case 4: v = 64 * E[0] - 64 * E[1] - 64 * E[2] + 64 * E[3]; break;
+    case 2: v = 83 * EO0 + 36 * EO1; break;
+    case 6: v = 36 * EO0 - 83 * EO1; break;
+    case 1: v = 89 * O[0] + 75 * O[1] + 50 * O[2] + 18 * O[3]; break;
+    case 3: v = 75 * O[0] - 18 * O[1] - 89 * O[2] - 50 * O[3]; break;
+    case 5: v = 50 * O[0] - 89 * O[1] + 18 * O[2] + 75 * O[3]; break;
+    default: v = 18 * O[0] - 50 * O[1] + 75 * O[2] - 89 * O[3]; break;
+  }
+  return te_wrap16((v + (1 << (shift - 1))) >> shift);
+}
+
+// transform, common/transform.c:249-330 (SIMD transform_simd for the 8x8
+// butterfly wrap): X.R (size x size, stride size) -> X.C (q x q raster).
+TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
+  const int lg = te_log2(size);
+  int N = size, sh1 = lg, sh2 = lg + 5;
+  const int16_t *in = X.R;
+  if (size == 8) {
+    for (int e = TE_LANE; e < 64; e += TE_NL) {
+      const int row = e >> 3, k = e & 7;
+      X.T[k * 8 + row] = (int16_t)te_fwd8(&X.R[row * 8], k, sh1);
+    }
+    te_sync();
+    for (int e = TE_LANE; e < 64; e += TE_NL) {
+      const int row = e >> 3, k = e & 7;
+      X.C[k * 8 + row] = te_fwd8(&X.T[row * 8], k, sh2);
+    }
+    te_sync();
+    return;
+  }
+  if (size > 16 && fast) {  // 2x2 / 4x4 pre-sum into a 16-point transform, :273-293
+    N = 16;
+    sh1 += 1 + (size == 64);
+    sh2 = 9;
+    const int f = size / 16;
+    for (int e = TE_LANE; e < 256; e += TE_NL) {
+      const int i = e >> 4, j = e & 15;
+      int s = 0;
+      for (int a = 0; a < f; a++)
+        for (int b = 0; b < f; b++) s += X.R[(i * f + a) * size + j * f + b];
+      X.A[e] = (int16_t)te_wrap16(s);
+    }
+    in = X.A;
+  } else if (size == 64) {  // 2x2 pre-sum into a 32-point transform, :294-307
+    N = 32;
+    sh1 = 7;
+    sh2 = 10;
+    for (int e = TE_LANE; e < 1024; e += TE_NL) {
+      const int i = e >> 5, j = e & 31;
+      const int16_t *r = &X.R[(2 * i) * 64 + 2 * j];
+      X.A[e] = (int16_t)te_wrap16(r[0] + r[1] + r[64] + r[65]);
+    }
+    in = X.A;
+  }
+  te_sync();
+  const int q = TE_MIN(size, 16);
+  const int add1 = 1 << (sh1 - 1), add2 = 1 << (sh2 - 1);
+  for (int e = TE_LANE; e < q * N; e += TE_NL) {  // :309-316, int16 store
+    const int i = e / N, j = e - (e / N) * N;
+    const int16_t *x = &in[j * N];
+    int s = 0;
+    for (int k = 0; k < N; k++) s += te_dctN(N, i, k) * (int)x[k];
+    X.T[i * N + j] = (int16_t)te_wrap16((s + add1) >> sh1);
+  }
+  te_sync();
+  for (int e = TE_LANE; e < q * q; e += TE_NL) {  // :319-327
+    const int i = e / q, j = e - (e / q) * q;
+    const int16_t *t = &X.T[j * N];
+    int s = 0;
+    for (int k = 0; k < N; k++) s += te_dctN(N, i, k) * (int)t[k];
+    X.C[i * q + j] = te_wrap16((s + add2) >> sh2);
+  }
+  te_sync();
+}
+
+// quantize, enc/encode_block.c:75-172 (rdoq = 0): X.C -> levels (q x q
+// raster) in X.C.  Returns cbp.
+TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
+  const int intra = (type >> 1) & 1, chroma = type & 1;
+  const int lg = te_log2(size), q = TE_MIN(size, 16), nq = q * q;
+  const int scale = te_gquant[qp % 6], shift2 = 21 - lg + qp / 6;
+  const int offset = (intra ? 38 : -26) * (1 << (shift2 - 8));
+  int lp = -1;
+  for (int r = TE_LANE; r < nq; r += TE_NL) {
+    const int pos = te_zz(q, r), c = X.C[r];
+    if ((te_abs(te_abs(c) * scale + offset) >> shift2) != 0) lp = TE_MAX(lp, pos);
+  }
+  const int last_pos = te_maxi(lp);  // -1: no level (the reference loop ends at pos = -1)
+  const int off0 = (intra ? 102 : 51) * (1 << (shift2 - 8)), off1 = (intra ? 115 : 90) * (1 << (shift2 - 8));
+  int any = 0;
+  for (int r = TE_LANE; r < nq; r += TE_NL) {
+    const int pos = te_zz(q, r);
+    int lev = 0;
+    if (pos <= last_pos) {
+      const int c = X.C[r];
+      const int ac = scale * te_abs(c);
+      const int l0 = ac >> shift2;
+      const int l = (ac + ((l0 == 0 || chroma) ? off0 : off1)) >> shift2;
+      lev = c < 0 ? -l : l;
+      any |= l != 0;
+    }
+    X.S[pos] = lev;
+    X.O[pos] = X.C[r];
+  }
+  const int cbp = te_any(any);
+  te_sync();
+  if (cbp && TE_LANE == 0) {  // "RDOQ light" (:134-168): serial over the scan
+    const int n = chroma ? last_pos + 1 : nq;
+    const int thr = (73 * te_gdequant[qp % 6] << (qp / 6)) >> (4 + lg);
+    for (int pos = 2; pos < n; pos++) {
+      int flag = 1;
+      if (pos > 2 && te_abs(X.S[pos - 3]) > 1) flag = 0;
+      if (pos > 3 && te_abs(X.S[pos - 4]) > 1 && te_abs(X.S[pos - 3]) > 0) flag = 0;
+      if (pos == 2 && (chroma == 0 || last_pos >= 6)) flag = 0;
+      if (flag && X.S[pos - 2] == 0 && X.S[pos - 1] == 0 && te_abs(X.S[pos]) > 1) {
+        const int c1 = X.O[pos], c2 = X.O[pos - 1], c3 = X.O[pos - 2];
+        const int K1 = te_abs(c1), K2 = te_abs(c2), K3 = te_abs(c3), K4 = TE_MAX(K2, K3);
+        if (K1 + K4 < thr) X.S[pos] = c1 < 0 ? -1 : 1;
+        else if (K2 > K3) X.S[pos - 1] = c2 < 0 ? -1 : 1;
+        else X.S[pos - 2] = c3 < 0 ? -1 : 1;
+      }
+    }
+  }
+  te_sync();
+  for (int r = TE_LANE; r < nq; r += TE_NL) X.C[r] = X.S[te_zz(q, r)];  // back to raster (:170-174)
+  te_sync();
+  return cbp;
+}
+
+// dequantize (common/common_block.c:132-146), int16 truncating store, in place
+TE_FN void te_dequant(TeTx &X, int qp, int size) {
+  const int q = TE_MIN(size, 16);
+  const int rshift = te_log2(size) - 1, add = 1 << (rshift - 1);
+  const int lshift = qp / 6, scale = te_gdequant[qp % 6];
+  for (int e = TE_LANE; e < q * q; e += TE_NL) X.C[e] = te_wrap16(((X.C[e] * scale) * (1 << lshift) + add) >> rshift);
+  te_sync();
+}
+
+// inverse_transform (common/transform.c:432-518): X.C (q x q) -> X.R
+// (n x n, n = min(size, 32); 64 = the 32-point output, replicated 2x2 by the reader).
+TE_FN void te_inv_tx(TeTx &X, int size) {
+  const int n = size == 64 ? 32 : size, q = TE_MIN(n, 16);
+  for (int e = TE_LANE; e < q * n; e += TE_NL) {
+    const int k = e / n, yp = e - (e / n) * n;  // coefficient column k
+    int s = 0;
+    for (int m = 0; m < q; m++) s += te_dctN(n, m, yp) * X.C[m * q + k];
+    X.T[k * n + yp] = (int16_t)te_clip16((s + 64) >> 7);
+  }
+  te_sync();
+  for (int e = TE_LANE; e < n * n; e += TE_NL) {
+    const int yp = e / n, xp = e - (e / n) * n;
+    int s = 0;
+    for (int k = 0; k < q; k++) s += te_dctN(n, k, xp) * (int)X.T[k * n + yp];
+    X.R[yp * n + xp] = (int16_t)te_clip16((s + 2048) >> 12);
+  }
+  te_sync();
+}
+// residual value at (y, x) of an inverse-transformed N x N block in X.R
+TE_FN int te_res_at(const TeTx &X, int size, int y, int x) {
+  return size == 64 ? X.R[(y >> 1) * 32 + (x >> 1)] : X.R[y * size + x];
+}

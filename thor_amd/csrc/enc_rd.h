@@ -1,0 +1,1109 @@
+// Device-resident Thor encoder, part 3: the RD loop of one superblock --
+// encode_block, cost_calc, motion estimation, intra mode search, early skip,
+// mode_decision_rdo and the quadtree process_block (enc/encode_block.c), and
+// the per-SB entry encode_frame runs (enc/encode_frame.c:112-147).
+#pragma once
+#include "enc_pix.h"
+
+// Per-wave working memory (global memory on the device; one per SB-row worker).
+#define TE_BLK (64 * 64 * 3 / 2)
+struct TeLevel {             // one quadtree level (64, 32, 16, 8)
+  uint8_t rbuf[2][TE_BLK];   // rec_block / rec_block_best (roles swap, see te_copy_best)
+  int16_t cbuf[3][3 * TE_COEF_COMP];  // coefficient sets: best, tmp, spare
+};
+struct TeScratch {
+  TeLevel lv[4];
+  uint8_t pb[TE_BLK], pb0[TE_BLK], pb1[TE_BLK];  // predictions (Y | U | V, compact)
+  uint8_t org8[64 * 64];                         // bi-pred search target (search_bipred_prediction_params)
+  uint8_t rf[64 * 64];                           // exact sub-pel ME prediction
+  TeTx tx;
+  TeNbr nb;
+};
+// State of the superblock being encoded (frame_info mvcand / best_ref are
+// reset per SB, enc/encode_frame.c:117-121) and its bit stream.
+struct TeSB {
+  TeBits bits;
+  TeMvCand mc;
+  int best_ref;
+};
+
+TE_FN uint8_t *te_pu(uint8_t *b, int size) { return b + size * size; }
+TE_FN uint8_t *te_pv(uint8_t *b, int size) { return b + size * size + (size / 2) * (size / 2); }
+
+TE_FN void te_copy_bytes(uint8_t *d, const uint8_t *s, int n) {
+  for (int e = TE_LANE; e < n; e += TE_NL) d[e] = s[e];
+  te_sync();
+}
+
+// clip_mv, enc/encode_block.c:816-828 (C division by 4; the right-edge test
+// omits `size`, the clamp includes it, as there)
+TE_FN TeMv te_clip_mv(TeMv m, int ypos, int xpos, int fw, int fh, int size, int sign) {
+  const int ext = 96 - 16;
+  int mvy = sign ? -m.y : m.y, mvx = sign ? -m.x : m.x;
+  if (ypos + mvy / 4 < -ext) mvy = 4 * (-ext - ypos);
+  if (ypos + mvy / 4 + size > fh + ext) mvy = 4 * (fh + ext - ypos - size);
+  if (xpos + mvx / 4 < -ext) mvx = 4 * (-ext - xpos);
+  if (xpos + mvx / 4 > fw + ext) mvx = 4 * (fw + ext - xpos - size);
+  TeMv r;
+  r.y = (int16_t)(sign ? -mvy : mvy);
+  r.x = (int16_t)(sign ? -mvx : mvx);
+  return r;
+}
+
+// get_inter_prediction_yuv, enc/encode_block.c:1534-1567: `split` predicts the
+// four size/2 quarters with mv[0..3].  Writes a compact Y|U|V block (stride size).
+TE_FN void te_pred_yuv(const TeFrame &F, int r, uint8_t *pb, const TeBlockInfo &bi, const TeMv *mv, int sign, int bipred,
+                       int split) {
+  const int div = split + 1, bw = bi.bwidth / div, bh = bi.bheight / div, size = bi.size;
+  const int ypos = bi.ypos, xpos = bi.xpos;
+  for (int index = 0; index < div * div; index++) {
+    const int idx = index & 1, idy = (index >> 1) & 1;
+    const TeMv m = te_clip_mv(mv[index], ypos, xpos, F.W, F.H, size, sign);
+    te_mc_luma(pb + idy * bh * size + idx * bw, size, F.refy[r] + (ypos + idy * bh) * F.rsy + xpos + idx * bw, F.rsy, bw, bh,
+               m, sign, bipred);
+    const int oc = idy * (bh / 2) * (size / 2) + idx * (bw / 2);
+    const int orc = (ypos / 2 + idy * (bh / 2)) * F.rsc + xpos / 2 + idx * (bw / 2);
+    te_mc_chroma(te_pu(pb, size) + oc, size / 2, F.refu[r] + orc, F.rsc, bw / 2, bh / 2, m, sign);
+    te_mc_chroma(te_pv(pb, size) + oc, size / 2, F.refv[r] + orc, F.rsc, bw / 2, bh / 2, m, sign);
+  }
+}
+// average_blocks_all, enc/encode_block.c:1569-1588: truncating (p0 + p1) >> 1
+// over bwidth x bheight (chroma halves)
+TE_FN void te_avg_yuv(uint8_t *d, const uint8_t *a, const uint8_t *b, const TeBlockInfo &bi) {
+  const int size = bi.size, bw = bi.bwidth, bh = bi.bheight;
+  for (int e = TE_LANE; e < bw * bh; e += TE_NL) {
+    const int i = e / bw, j = e - (e / bw) * bw;
+    d[i * size + j] = (uint8_t)(((int)a[i * size + j] + (int)b[i * size + j]) >> 1);
+  }
+  const int cw = bw / 2, ch = bh / 2, cs = size / 2, co = size * size, cq = cs * cs;
+  for (int e = TE_LANE; e < cw * ch; e += TE_NL) {
+    const int i = e / cw, j = e - (e / cw) * cw;
+    d[co + i * cs + j] = (uint8_t)(((int)a[co + i * cs + j] + (int)b[co + i * cs + j]) >> 1);
+    d[co + cq + i * cs + j] = (uint8_t)(((int)a[co + cq + i * cs + j] + (int)b[co + cq + i * cs + j]) >> 1);
+  }
+  te_sync();
+}
+
+TE_FN int te_sign_of(const TeFrame &F, int ref_idx, int bi) {
+  // uni-pred: ref->frame_num > rec->frame_num; bi-pred legs: >= (encode_block.c:1694, :1707)
+  return bi ? F.ref_fnum[ref_idx] >= F.frame_num : F.ref_fnum[ref_idx] > F.frame_num;
+}
+
+// ---- transform-block chains -------------------------------------------------
+// encode_and_reconstruct_block_inter, enc/encode_block.c:1469-1532, one
+// component: orig (frame, stride os) - pred -> levels (tiles of `coef`) ->
+// rec (compact, stride size).  Returns cbp (4-bit mask when tb-split).
+TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *org, int os, int size, int qp,
+                               const uint8_t *pb, int16_t *coef, uint8_t *rec, int type, int tb_split) {
+  TeTx &X = S.tx;
+  int cbp = 0;
+  if (tb_split) {
+    const int s2 = size / 2, fast = size == 64 || F.speed > 1;
+    // rblock: the reconstructed residual of every quarter, kept in rec as a
+    // running copy of pred + residual (reconstruct_block after the loop, :1510)
+    for (int t = 0; t < 4; t++) {
+      const int i = (t >> 1) * s2, j = (t & 1) * s2;
+      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
+        const int y = e / s2, x = e - (e / s2) * s2;
+        X.R[e] = (int16_t)((int)org[(i + y) * os + j + x] - (int)pb[(i + y) * size + j + x]);
+      }
+      te_sync();
+      te_fwd_tx(X, s2, fast);
+      const int bit = te_quant(X, qp, s2, type);
+      const int q = TE_MIN(s2, 16);
+      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * 256 + e] = (int16_t)X.C[e];
+      if (bit) {
+        te_dequant(X, qp, s2);
+        te_inv_tx(X, s2);
+      }
+      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
+        const int y = e / s2, x = e - (e / s2) * s2;
+        const int p = pb[(i + y) * size + j + x];
+        rec[(i + y) * size + j + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, s2, y, x) + p) : p);
+      }
+      te_sync();
+      cbp = (cbp << 1) + bit;
+    }
+    return cbp;
+  }
+  const int fast = (size == 64 && F.speed > 0) || F.speed > 1;
+  for (int e = TE_LANE; e < size * size; e += TE_NL) {
+    const int y = e / size, x = e - (e / size) * size;
+    X.R[e] = (int16_t)((int)org[y * os + x] - (int)pb[e]);
+  }
+  te_sync();
+  te_fwd_tx(X, size, fast);
+  cbp = te_quant(X, qp, size, type);
+  const int q = TE_MIN(size, 16);
+  for (int e = TE_LANE; e < q * q; e += TE_NL) coef[e] = (int16_t)X.C[e];
+  if (cbp) {
+    te_dequant(X, qp, size);
+    te_inv_tx(X, size);
+  }
+  for (int e = TE_LANE; e < size * size; e += TE_NL) {
+    const int y = e / size, x = e - (e / size) * size;
+    rec[e] = (uint8_t)(cbp ? te_clip255(te_res_at(X, size, y, x) + pb[e]) : pb[e]);
+  }
+  te_sync();
+  return cbp;
+}
+
+// encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
+// component.  rf / fs: the frame being reconstructed at the CU origin.
+TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch &S, const uint8_t *org, int os, const uint8_t *rf, int fs,
+                               int ypos, int xpos, int size, int qp, uint8_t *pb, int16_t *coef, uint8_t *rec, int type,
+                               int tb_split, int mode, int ur, int dl) {
+  TeTx &X = S.tx;
+  const int fast = F.speed > 1;
+  if (tb_split) {
+    const int s2 = size / 2, q = TE_MIN(s2, 16);
+    int cbp = 0;
+    for (int t = 0; t < 4; t++) {
+      const int i = (t >> 1) * s2, j = (t & 1) * s2;
+      te_make_top_and_left(S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
+      te_intra_pred(S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
+      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
+        const int y = e / s2, x = e - (e / s2) * s2;
+        X.R[e] = (int16_t)((int)org[(i + y) * os + j + x] - (int)pb[e]);
+      }
+      te_sync();
+      te_fwd_tx(X, s2, fast);
+      const int bit = te_quant(X, qp, s2, type);
+      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * 256 + e] = (int16_t)X.C[e];
+      if (bit) {
+        te_dequant(X, qp, s2);
+        te_inv_tx(X, s2);
+      }
+      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
+        const int y = e / s2, x = e - (e / s2) * s2;
+        rec[(i + y) * size + j + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, s2, y, x) + pb[e]) : pb[e]);
+      }
+      te_sync();
+      cbp = (cbp << 1) + bit;
+    }
+    return cbp;
+  }
+  te_make_top_and_left(S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
+  te_intra_pred(S.nb, ypos, xpos, size, pb, mode, 0);
+  for (int e = TE_LANE; e < size * size; e += TE_NL) {
+    const int y = e / size, x = e - (e / size) * size;
+    X.R[e] = (int16_t)((int)org[y * os + x] - (int)pb[e]);
+  }
+  te_sync();
+  te_fwd_tx(X, size, fast);
+  const int cbp = te_quant(X, qp, size, type);
+  const int q = TE_MIN(size, 16);
+  for (int e = TE_LANE; e < q * q; e += TE_NL) coef[e] = (int16_t)X.C[e];
+  if (cbp) {
+    te_dequant(X, qp, size);
+    te_inv_tx(X, size);
+  }
+  for (int e = TE_LANE; e < size * size; e += TE_NL) {
+    const int y = e / size, x = e - (e / size) * size;
+    rec[e] = (uint8_t)(cbp ? te_clip255(te_res_at(X, size, y, x) + pb[e]) : pb[e]);
+  }
+  te_sync();
+  return cbp;
+}
+
+// encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
+// bi.rec, write the block's syntax.  Returns the bit count.
+TE_NOINL int te_encode_block(const TeFrame &F, TeScratch &S, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, yC = ypos / 2, xC = xpos / 2, sC = size / 2;
+  const int mode = p.mode;
+  const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
+  const int re_use = (bi.final_encode & 1) && !F.enable_tb_split;
+  if (re_use) {
+    te_copy_bytes(bi.rec, bi.rec_best, size * size + 2 * sC * sC);
+    return te_write_block(b, F, bi, p, S.tx.scan);
+  }
+  uint8_t *recY = bi.rec, *recU = te_pu(bi.rec, size), *recV = te_pv(bi.rec, size);
+  const int tb_split = TE_MAX(0, p.tb_param), zero_block = p.tb_param == -1;
+  p.tb_split = tb_split;
+  const uint8_t *oY = F.oy + ypos * F.osy + xpos, *oU = F.ou + yC * F.osc + xC, *oV = F.ov + yC * F.osc + xC;
+  int cy = 0, cu = 0, cv = 0;
+  const int itype = (F.frame_type == TE_I) << 1;  // quantisation type follows the frame type (:1764)
+  if (mode == TE_INTRA) {
+    const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
+    cy = te_enc_intra_comp(F, S, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb,
+                           p.coeff, recY, itype | 0, tb_split, p.intra_mode, ur, dl);
+    cu = te_enc_intra_comp(F, S, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
+                           p.coeff + TE_COEF_COMP, recU, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl);
+    cv = te_enc_intra_comp(F, S, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
+                           p.coeff + 2 * TE_COEF_COMP, recV, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl);
+  } else {
+    const int bip = F.enable_bipred;
+    if (mode == TE_SKIP) {
+      if (p.dir == 2) {
+        te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, 0);
+        te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, 0);
+        te_avg_yuv(bi.rec, S.pb0, S.pb1, bi);
+      } else {
+        te_pred_yuv(F, p.ref_idx0, bi.rec, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, 0);
+      }
+    } else if (mode == TE_MERGE) {
+      if (p.dir == 2) {
+        te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, 0);
+        te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, 0);
+        te_avg_yuv(S.pb, S.pb0, S.pb1, bi);
+      } else {
+        te_pred_yuv(F, p.ref_idx0, S.pb, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, 0);
+      }
+    } else if (mode == TE_INTER) {
+      te_pred_yuv(F, p.ref_idx0, S.pb, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, F.enable_pb_split);
+    } else if (mode == TE_BIPRED) {
+      te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, F.enable_pb_split);
+      te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, F.enable_pb_split);
+      te_avg_yuv(S.pb, S.pb0, S.pb1, bi);
+    }
+    if (mode != TE_SKIP) {
+      if (zero_block) {
+        te_copy_bytes(bi.rec, S.pb, size * size + 2 * sC * sC);
+      } else {
+        cy = te_enc_inter_comp(F, S, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split);
+        cu = te_enc_inter_comp(F, S, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + TE_COEF_COMP, recU, itype | 1,
+                               tb_split && size > 8);
+        cv = te_enc_inter_comp(F, S, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * TE_COEF_COMP, recV,
+                               itype | 1, tb_split && size > 8);
+      }
+    }
+  }
+  p.cbp_y = cy;
+  p.cbp_u = cu;
+  p.cbp_v = cv;
+  const int nbits = te_write_block(b, F, bi, p, S.tx.scan);
+  if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
+  return nbits;
+}
+
+// cost_calc, enc/encode_block.c:1218-1228
+TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *rec, int w, int h, int nbits) {
+  const int size = bi.size, sC = size / 2;
+  const int ypos = bi.ypos, xpos = bi.xpos;
+  const uint32_t sy = te_ssd(F.oy + ypos * F.osy + xpos, F.osy, rec, size, w, h);
+  const uint32_t su = te_ssd(F.ou + (ypos / 2) * F.osc + xpos / 2, F.osc, te_pu((uint8_t *)rec, size), sC, w / 2, h / 2);
+  const uint32_t sv = te_ssd(F.ov + (ypos / 2) * F.osc + xpos / 2, F.osc, te_pv((uint8_t *)rec, size), sC, w / 2, h / 2);
+  const double prod = F.lambda * (double)nbits;
+  uint32_t cost = sy + su + sv + (uint32_t)(int32_t)(prod + 0.5);
+  if (cost > (1u << 30)) cost = 1u << 30;
+  return cost;
+}
+
+// search_intra_prediction_params, enc/encode_block.c:1230-1329: SAD over the
+// first `num_modes` modes in the order DC, HOR, VER, PLANAR, [UPLEFT ...].
+TE_NOINL int te_search_intra(const TeFrame &F, TeScratch &S, const TeBlockInfo &bi, int num_modes, int *mode_out) {
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
+  const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
+  te_make_top_and_left(S.nb, F.ry + ypos * F.rsy + xpos, F.rsy, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
+  const int order[10] = {TE_DC, TE_HOR, TE_VER, TE_PLANAR, TE_UPLEFT, TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT,
+                         TE_UPLEFTLEFT, TE_DOWNLEFTLEFT};
+  int min_sad = 1 << 30, best = TE_DC;
+  const int n = num_modes == 4 ? 4 : 10;
+  const uint8_t *o = F.oy + ypos * F.osy + xpos;
+  for (int k = 0; k < n; k++) {
+    te_intra_pred(S.nb, ypos, xpos, size, S.pb, order[k], 1);
+    const int sad = (int)te_sad(o, F.osy, S.pb, size, size, size);
+    if (sad < min_sad) {
+      best = order[k];
+      min_sad = sad;
+    }
+  }
+  *mode_out = best;
+  return min_sad;
+}
+
+TE_FN uint32_t te_lambda_bits(double lam, int bits) { return (uint32_t)(lam * (double)bits + 0.5); }
+
+// motion_estimate, enc/encode_block.c:830-1016 (params->sync = 0).  `org` /
+// `os`: the block (or partition) of the original; `ref`: the reference at the
+// block (partition) origin; size: the CU size (clip_mv, the size-16 rules).
+TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch &S, TeSB &sb, int r, const uint8_t *org, int os,
+                                     const uint8_t *ref, int size, int width, int height, TeMv *mv, TeMv mvc, TeMv mvp,
+                                     int sign, int xpos, int ypos, int enable_bipred) {
+  const int rs = F.rsy, s = sign ? -1 : 1;
+  const double lam = F.sqrt_lambda;
+  uint32_t min_sad = TE_MAX_UINT32;
+  TeMv mv_opt, mv_ref, c;
+  mv_opt.x = mv_opt.y = 0;
+  mv_ref.y = (int16_t)((((int)mvc.y + 2) >> 2) << 2);
+  mv_ref.x = (int16_t)((((int)mvc.x + 2) >> 2) << 2);
+  if ((size == 16 && enable_bipred) || F.speed == 0) {  // telescope search
+    int step = 32;
+    while (step >= 4) {
+      const int range = 2 * step;
+      for (int k = -range; k <= range; k += step)
+        for (int l = -range; l <= range; l += step) {
+          if (step < 32 && !k && !l) continue;
+          c.y = (int16_t)(mv_ref.y + k);
+          c.x = (int16_t)(mv_ref.x + l);
+          c = te_clip_mv(c, ypos, xpos, F.W, F.H, size, sign);
+          uint32_t sad;
+          const uint8_t *rp = ref + s * (c.x >> 2) + s * (c.y >> 2) * rs;
+          if (step == 32 && size == 16 && F.speed < 2 && F.speed > 0) {
+            int x = 0;
+            sad = te_widesad(org, os, rp, rs, width, height, &x);
+            c.x = (int16_t)(c.x + (s * x << 2));
+          } else {
+            sad = te_sad(org, os, rp, rs, width, height);
+          }
+          sad += te_lambda_bits(lam, te_mv_bits(c.y - mvp.y, c.x - mvp.x));
+          if (sad < min_sad) {
+            min_sad = sad;
+            mv_opt = c;
+          }
+        }
+      mv_ref = mv_opt;
+      step >>= 1;
+    }
+  }
+  for (int idx = 0; idx < sb.mc.num[r]; idx++) {  // candidate search
+    int x = 0;
+    const TeMv cm = sb.mc.mv[r][idx];
+    c.y = (int16_t)(cm.y << 2);
+    c.x = (int16_t)(cm.x << 2);
+    c = te_clip_mv(c, ypos, xpos, F.W, F.H, size, sign);
+    const uint8_t *rp = ref + s * (c.x >> 2) + s * (c.y >> 2) * rs;
+    uint32_t sad = size == 16 ? te_widesad(org, os, rp, rs, width, height, &x) : te_sad(org, os, rp, rs, width, height);
+    c.x = (int16_t)(c.x + (s * x << 2));
+    sad += te_lambda_bits(lam, te_mv_bits(c.y - mvp.y, c.x - mvp.x));
+    if (sad < min_sad) {
+      min_sad = sad;
+      mv_opt = c;
+    }
+  }
+  mv_ref = mv_opt;
+  const int maxsteps = size <= 16 || F.speed == 0 ? 6 : 0;
+  int start = 0, end = 5;
+  for (int step = 1; step < maxsteps; step++) {  // full-pel hexagon search
+    const int diy[6] = {1, 2, 1, -1, -2, -1}, dix[6] = {-1, 0, 1, 1, 0, -1};
+    int dir = start - 1, best_dir = -1;
+    do {
+      dir++;
+      dir = dir == 6 ? 0 : dir;
+      c.y = (int16_t)(mv_ref.y + dix[dir] * 4);
+      c.x = (int16_t)(mv_ref.x + diy[dir] * 4);
+      c = te_clip_mv(c, ypos, xpos, F.W, F.H, size, sign);
+      uint32_t sad = te_sad(org, os, ref + s * (c.x >> 2) + s * (c.y >> 2) * rs, rs, width, height);
+      sad += te_lambda_bits(lam, te_mv_bits(c.y - mvp.y, c.x - mvp.x));
+      if (sad < min_sad) {
+        min_sad = sad;
+        mv_opt = c;
+        best_dir = dir;
+      }
+    } while (dir != end);
+    mv_ref = mv_opt;
+    start = best_dir ? best_dir - 1 : 5;
+    end = start + 2;
+    end -= (end >= 6) * 6;
+    if (best_dir < 0) break;
+  }
+  int ydelta_hp = 0, xdelta_hp = 0, ydelta_qp = 0, xdelta_qp = 0;
+  uint32_t cmin = min_sad;
+  if (F.speed == 0) {  // exact half- and quarter-pel search through the MC filters
+    const int hm[9] = {0, 0, -2, 2, 0, -2, -2, 2, 2}, hn[9] = {0, -2, 0, 0, 2, -2, 2, -2, 2};
+    for (int i = 1; i <= 8; i++) {
+      c.y = (int16_t)(mv_ref.y + hm[i]);
+      c.x = (int16_t)(mv_ref.x + hn[i]);
+      te_mc_luma(S.rf, width, ref, rs, width, height, c, sign, enable_bipred);
+      uint32_t sad = te_sad(org, os, S.rf, width, width, height);
+      sad += te_lambda_bits(lam, te_mv_bits(c.y - mvp.y, c.x - mvp.x));
+      if (sad < cmin) {
+        cmin = sad;
+        ydelta_hp = hm[i];
+        xdelta_hp = hn[i];
+      }
+    }
+    mv_opt.x = (int16_t)(mv_opt.x + xdelta_hp);
+    mv_opt.y = (int16_t)(mv_opt.y + ydelta_hp);
+    const int qm[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, qn[9] = {0, -1, 0, 0, 1, -1, 1, -1, 1};
+    for (int i = 1; i <= 8; i++) {
+      c.y = (int16_t)(mv_opt.y + qm[i]);
+      c.x = (int16_t)(mv_opt.x + qn[i]);
+      te_mc_luma(S.rf, width, ref, rs, width, height, c, sign, enable_bipred);
+      uint32_t sad = te_sad(org, os, S.rf, width, width, height);
+      sad += (uint32_t)(int)(lam * (double)te_mv_bits(c.y - mvp.y, c.x - mvp.x) + 0.5);
+      if (sad < cmin) {
+        cmin = sad;
+        ydelta_qp = qm[i];
+        xdelta_qp = qn[i];
+      }
+    }
+  } else {  // fast bilinear approximation
+    mv_ref.x = (int16_t)(mv_ref.x * s);
+    mv_ref.y = (int16_t)(mv_ref.y * s);
+    int spx, spy;
+    uint32_t sad = te_fasthalf(org, os, ref + (mv_ref.x >> 2) + (mv_ref.y >> 2) * rs, rs, width, height, &spx, &spy);
+    sad += te_lambda_bits(lam, te_mv_bits(mv_ref.y + s * spy - mvp.y, mv_ref.x + s * spx - mvp.x));
+    if (sad < cmin) {
+      cmin = sad;
+      xdelta_hp = s * spx;
+      ydelta_hp = s * spy;
+    }
+    spx = xdelta_hp;
+    spy = ydelta_hp;
+    mv_ref.x = (int16_t)(mv_opt.x + s * spx);
+    mv_ref.y = (int16_t)(mv_opt.y + s * spy);
+    mv_opt.x = (int16_t)(mv_opt.x + xdelta_hp);
+    mv_opt.y = (int16_t)(mv_opt.y + ydelta_hp);
+    sad = te_fastquarter(org, os, ref + s * (mv_ref.x >> 2) + s * (mv_ref.y >> 2) * rs, rs, width, height, &spx, &spy);
+    sad += (uint32_t)(int)(lam * (double)te_mv_bits(mv_ref.y + s * spy - mvp.y, mv_ref.x + s * spx - mvp.x) + 0.5);
+    if (sad < cmin) {
+      cmin = sad;
+      xdelta_qp = s * spx;
+      ydelta_qp = s * spy;
+    }
+  }
+  mv_opt.x = (int16_t)(mv_opt.x + xdelta_qp);
+  mv_opt.y = (int16_t)(mv_opt.y + ydelta_qp);
+  *mv = mv_opt;
+  return TE_MIN(cmin, min_sad);
+}
+
+// search_inter_prediction_params, enc/encode_block.c:1331-1396
+TE_FN uint32_t te_search_inter(const TeFrame &F, TeScratch &S, TeSB &sb, int r, const uint8_t *org, int os,
+                               const TeBlockInfo &bi, TeMv mvc, TeMv mvp, TeMv *mv_arr, int part, int sign,
+                               int enable_bipred) {
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, rs = F.rsy;
+  const uint8_t *ref_y = F.refy[r] + ypos * rs + xpos;
+  TeMv mv, mvp2 = mvp;
+  uint32_t sad = 0;
+  if (part == 0) {
+    sad += te_motion_estimate(F, S, sb, r, org, os, ref_y, size, size, size, &mv, mvc, mvp2, sign, xpos, ypos,
+                              enable_bipred);
+    mv_arr[0] = mv_arr[1] = mv_arr[2] = mv_arr[3] = mv;
+  } else if (part == 1) {  // PART_HOR
+    for (int index = 0; index < 4; index += 2) {
+      const int py = index >> 1;
+      sad += te_motion_estimate(F, S, sb, r, org + py * (size / 2) * os, os, ref_y + py * (size / 2) * rs, size, size,
+                                size / 2, &mv, mvc, mvp2, sign, xpos, ypos, enable_bipred);
+      mv_arr[index] = mv_arr[index + 1] = mv;
+      mvp2 = mv_arr[0];
+    }
+  } else if (part == 2) {  // PART_VER
+    for (int index = 0; index < 2; index++) {
+      sad += te_motion_estimate(F, S, sb, r, org + index * (size / 2), os, ref_y + index * (size / 2), size, size / 2,
+                                size, &mv, mvc, mvp2, sign, xpos, ypos, enable_bipred);
+      mv_arr[index] = mv_arr[index + 2] = mv;
+      mvp2 = mv_arr[0];
+    }
+  } else {  // PART_QUAD
+    for (int index = 0; index < 4; index++) {
+      const int px = index & 1, py = (index & 2) >> 1;
+      sad += te_motion_estimate(F, S, sb, r, org + py * (size / 2) * os + px * (size / 2), os,
+                                ref_y + py * (size / 2) * rs + px * (size / 2), size, size / 2, size / 2, &mv, mvc,
+                                mvp2, sign, xpos, ypos, enable_bipred);
+      mv_arr[index] = mv;
+      mvp2 = mv_arr[0];
+    }
+  }
+  return sad;
+}
+
+// copy_best_parameters, enc/encode_block.c:1983-2045.  The reconstructed
+// block and the coefficient set of the candidate become the best by swapping
+// buffer roles instead of copying (only components with cbp are ever read).
+TE_FN void te_copy_best(TeBlockInfo &bi, TeParam &tmp) {
+  TeParam &b = bi.bp;
+  uint8_t *t = bi.rec_best;
+  bi.rec_best = bi.rec;
+  bi.rec = t;
+  int16_t *c = b.coeff;
+  b.coeff = tmp.coeff;
+  tmp.coeff = c;
+  b.pb_part = tmp.pb_part;
+  b.skip_idx = tmp.skip_idx;
+  b.mode = tmp.mode;
+  b.cbp_y = tmp.cbp_y;
+  b.cbp_u = tmp.cbp_u;
+  b.cbp_v = tmp.cbp_v;
+  b.tb_param = tmp.tb_param;
+  b.tb_split = tmp.tb_split;
+  if (tmp.mode == TE_SKIP || tmp.mode == TE_MERGE) {
+    const TeInterPred &cp = tmp.mode == TE_SKIP ? bi.skip_c[tmp.skip_idx] : bi.merge_c[tmp.skip_idx];
+    b.ref_idx0 = cp.ref_idx0;
+    b.ref_idx1 = cp.ref_idx1;
+    for (int i = 0; i < 4; i++) {
+      b.mv0[i] = cp.mv0;
+      b.mv1[i] = cp.mv1;
+    }
+    b.dir = cp.bipred_flag;
+  } else if (tmp.mode == TE_INTRA) {
+    b.ref_idx0 = b.ref_idx1 = 0;
+    for (int i = 0; i < 4; i++) b.mv0[i].x = b.mv0[i].y = b.mv1[i].x = b.mv1[i].y = 0;
+    b.dir = -1;
+    b.intra_mode = tmp.intra_mode;
+  } else {  // INTER / BIPRED
+    b.ref_idx0 = tmp.ref_idx0;
+    b.ref_idx1 = tmp.ref_idx1;
+    for (int i = 0; i < 4; i++) {
+      b.mv0[i] = tmp.mv0[i];
+      b.mv1[i] = tmp.mv1[i];
+    }
+    b.dir = tmp.mode == TE_INTER ? 0 : 2;
+  }
+}
+
+// copy_block_to_frame (:1802-1819) + copy_deblock_data (:1947-1981)
+TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
+  const int size = bi.size, bw = bi.bwidth, bh = bi.bheight, sC = size / 2;
+  const uint8_t *r = bi.rec;
+  for (int e = TE_LANE; e < bw * bh; e += TE_NL) {
+    const int i = e / bw, j = e - (e / bw) * bw;
+    F.ry[(bi.ypos + i) * F.rsy + bi.xpos + j] = r[i * size + j];
+  }
+  const int cw = bw / 2, ch = bh / 2;
+  for (int e = TE_LANE; e < cw * ch; e += TE_NL) {
+    const int i = e / cw, j = e - (e / cw) * cw;
+    const int o = (bi.ypos / 2 + i) * F.rsc + bi.xpos / 2 + j;
+    F.ru[o] = te_pu((uint8_t *)r, size)[i * sC + j];
+    F.rv[o] = te_pv((uint8_t *)r, size)[i * sC + j];
+  }
+  const TeParam &p = bi.bp;
+  const int div = size / 8, bs = F.W / 4;
+  const int nw = bw / 4, nh = bh / 4;
+  for (int e = TE_LANE; e < nw * nh; e += TE_NL) {
+    const int m = e / nw, n = e - (e / nw) * nw;
+    const int m0 = div > 0 ? m / div : 0, n0 = div > 0 ? n / div : 0, index = 2 * m0 + n0;
+    TeCell c;
+    c.ip.mv0 = p.mv0[index];
+    c.ip.mv1 = p.mv1[index];
+    c.ip.ref_idx0 = p.ref_idx0;
+    c.ip.ref_idx1 = p.ref_idx1;
+    c.ip.bipred_flag = p.dir;
+    c.mode = (uint8_t)p.mode;
+    c.size = (uint8_t)size;
+    c.tb_split = (uint8_t)TE_MAX(0, p.tb_param);
+    c.pb_part = (uint8_t)(p.mode == TE_INTER ? p.pb_part : 0);
+    c.cbp_y = (uint8_t)p.cbp_y;
+    c.cbp_u = (uint8_t)p.cbp_u;
+    c.cbp_v = (uint8_t)p.cbp_v;
+    c.rsv = 0;
+    F.cells[(bi.ypos / 4 + m) * bs + bi.xpos / 4 + n] = c;
+  }
+  te_sync();
+}
+
+// search_bipred_prediction_params, enc/encode_block.c:2047-2202, me_mode 0
+// (the iterative uni-pred search on the modified target org8)
+TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch &S, TeSB &sb, TeBlockInfo &bi, int part,
+                                   TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_arr0,
+                                   TeMv *mv_arr1) {
+  const int size = bi.size;
+  const int num_iter = F.speed == 0 ? 2 : 1;
+  int ref_idx = (F.frame_type == TE_B && F.interp_ref == 1) ? 1 : 0;
+  int min_ref_idx0 = ref_idx, min_ref_idx1 = 0;
+  TeMv m0[4], m1[4], mv_all[4];
+  for (int i = 0; i < 4; i++) m0[i] = m1[i] = mvp;
+  int min_sad = 1 << 30;
+  const uint8_t *org = F.oy + bi.ypos * F.osy + bi.xpos;
+  for (int n = 0; n < num_iter; n++) {
+    const int stop = part == 0 ? 0 : 1;
+    for (int list = 1; list >= stop; list--) {
+      const TeMv mv = list ? m0[0] : m1[0];
+      ref_idx = list ? min_ref_idx0 : min_ref_idx1;
+      const int sign = F.ref_fnum[ref_idx] > F.frame_num;
+      te_pred_yuv(F, ref_idx, S.pb, bi, list ? m0 : m1, sign, 1, 1);
+      for (int e = TE_LANE; e < size * size; e += TE_NL) {
+        const int y = e / size, x = e - (e / size) * size;
+        S.org8[e] = (uint8_t)te_clip255(2 * (int)org[y * F.osy + x] - (int)S.pb[e]);
+      }
+      te_sync();
+      int ref_start, ref_end;
+      if (F.frame_type == TE_P) {
+        ref_start = 0;
+        ref_end = F.num_ref - 1;
+      } else {
+        ref_start = ref_end = list ? 1 : 0;
+        if (F.interp_ref) {
+          ref_start += 1;
+          ref_end += 1;
+        }
+      }
+      for (int r = ref_start; r <= ref_end; r++) {
+        const int sg = F.ref_fnum[r] > F.frame_num;
+        const TeMv mvp2 = (F.frame_type == TE_B && list == 1) ? mv : mvp;
+        const int sad = (int)te_search_inter(F, S, sb, r, S.org8, size, bi, mv_center[r], mvp2, mv_all, part, sg, 1);
+        for (int i = 0; i < 4; i++) te_add_mvcand(sb.mc, r, mv_all[i]);
+        if (sad < min_sad) {
+          min_sad = sad;
+          if (list) {
+            min_ref_idx1 = r;
+            for (int i = 0; i < 4; i++) m1[i] = mv_all[i];
+          } else {
+            min_ref_idx0 = r;
+            for (int i = 0; i < 4; i++) m0[i] = mv_all[i];
+          }
+        }
+      }
+    }
+  }
+  *ref_idx0 = min_ref_idx0;
+  *ref_idx1 = min_ref_idx1;
+  for (int i = 0; i < 4; i++) {
+    mv_arr0[i] = m0[i];
+    mv_arr1[i] = m1[i];
+  }
+  return (uint32_t)(min_sad / 2);
+}
+
+// mode_decision_rdo, enc/encode_block.c:2204-2479
+TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch &S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
+  TeBits &b = sb.bits;
+  const int frame_type = F.frame_type;
+  const int rectangular = bi.bwidth != size || bi.bheight != size;
+  const int intra_inter_sad = F.speed > 0 && !F.sync;
+  uint32_t min_cost = TE_MAX_UINT32, sad_intra = TE_MAX_UINT32, sad_inter = TE_MAX_UINT32, cost;
+  int do_inter = 1, do_intra = 1;
+  int intra_mode = TE_DC;
+  const int pos_ref = b.pos;
+  TeParam tmp;
+  memset(&tmp, 0, sizeof(tmp));
+  tmp.coeff = tmp_coef;
+  if (frame_type != TE_I) {  // skip candidates
+    tmp.tb_param = 0;
+    tmp.pb_part = 0;
+    for (int k = 0; k < bi.num_skip; k++) {
+      tmp.skip_idx = k;
+      tmp.ref_idx0 = bi.skip_c[k].ref_idx0;
+      tmp.ref_idx1 = bi.skip_c[k].ref_idx1;
+      tmp.mv0[0] = bi.skip_c[k].mv0;
+      tmp.mv1[0] = bi.skip_c[k].mv1;
+      tmp.dir = bi.skip_c[k].bipred_flag;
+      tmp.mode = TE_SKIP;
+      const int nbits = te_encode_block(F, S, b, bi, tmp);
+      cost = te_cost(F, bi, bi.rec, bi.bwidth, bi.bheight, nbits);
+      if (cost < min_cost) {
+        min_cost = cost;
+        te_copy_best(bi, tmp);
+      }
+    }
+  }
+  if (!rectangular && size <= 64) {
+    if (frame_type != TE_I) {
+      tmp.tb_param = 0;
+      for (int k = 0; k < bi.num_merge; k++) {  // merge candidates
+        tmp.skip_idx = k;
+        tmp.ref_idx0 = bi.merge_c[k].ref_idx0;
+        tmp.ref_idx1 = bi.merge_c[k].ref_idx1;
+        tmp.mv0[0] = bi.merge_c[k].mv0;
+        tmp.mv1[0] = bi.merge_c[k].mv1;
+        tmp.dir = bi.merge_c[k].bipred_flag;
+        tmp.mode = TE_MERGE;
+        const int nbits = te_encode_block(F, S, b, bi, tmp);
+        cost = te_cost(F, bi, bi.rec, size, size, nbits);
+        if (cost < min_cost) {
+          min_cost = cost;
+          te_copy_best(bi, tmp);
+        }
+      }
+      if (intra_inter_sad) {
+        sad_intra = (uint32_t)te_search_intra(F, S, bi, F.num_intra_modes, &intra_mode);
+        sad_intra += (uint32_t)(int)(F.sqrt_lambda * (double)2 + 0.5);
+      }
+      // inter: ME per reference
+      TeMv mv_all[4][4], mv_center[TE_MAX_REF], mvp;
+      int min_idx, max_idx;
+      if (sb.best_ref < 0 || F.speed < 2 || F.enable_bipred || F.sync) {
+        min_idx = 0;
+        max_idx = F.num_ref - 1;
+      } else {
+        min_idx = max_idx = sb.best_ref;
+      }
+      int32_t worst_cost = 0, best_cost = (int32_t)TE_MAX_UINT32;
+      for (int r = min_idx; r <= max_idx; r++) {
+        tmp.ref_idx0 = r;
+        tmp.ref_idx1 = r;
+        mvp = te_mv_pred(ypos, xpos, F.W, F.H, size, F.cells);
+        te_add_mvcand(sb.mc, r, mvp);
+        te_sync();
+        bi.mvp = mvp;
+        const int sign = F.ref_fnum[r] >= F.frame_num;
+        mv_center[r] = mvp;
+        sad_inter = TE_MAX_UINT32;
+        for (int part = 0; part < bi.max_num_pb_part; part++) {
+          const uint32_t sad = te_search_inter(F, S, sb, r, F.oy + ypos * F.osy + xpos, F.osy, bi, mv_center[r], mvp,
+                                               mv_all[part], part, sign, F.enable_bipred);
+          for (int i = 0; i < 4; i++) te_add_mvcand(sb.mc, r, mv_all[part][i]);
+          te_sync();
+          mv_center[r] = mv_all[0][0];
+          sad_inter = TE_MIN(sad_inter, sad);
+        }
+        if (intra_inter_sad) {
+          do_inter = sad_inter < sad_intra;
+          if (sad_inter < sad_intra) do_intra = 0;
+        }
+        if (do_inter) {
+          for (int part = 0; part < bi.max_num_pb_part; part++) {
+            tmp.pb_part = part;
+            for (int i = 0; i < 4; i++) tmp.mv0[i] = tmp.mv1[i] = mv_all[part][i];
+            const int min_tb = F.speed < 1 ? -1 : 0, max_tb = bi.max_num_tb_part - 1;
+            tmp.mode = TE_INTER;
+            for (int tbp = min_tb; tbp <= max_tb; tbp++) {
+              tmp.tb_param = tbp;
+              const int nbits = te_encode_block(F, S, b, bi, tmp);
+              cost = te_cost(F, bi, bi.rec, size, size, nbits);
+              // worst_cost = max(worst_cost, cost), best_cost = min(best_cost, cost): int vs uint32 compares
+              worst_cost = (uint32_t)worst_cost > cost ? worst_cost : (int32_t)cost;
+              best_cost = (uint32_t)best_cost < cost ? best_cost : (int32_t)cost;
+              if (cost < min_cost) {
+                min_cost = cost;
+                te_copy_best(bi, tmp);
+              }
+            }
+          }
+        }
+      }
+      // one reference convincingly better: remember it (best_ref_idx is always 0, :2237, :2376-2377)
+      if (worst_cost && (int32_t)((uint32_t)worst_cost * 3u) > (int32_t)((uint32_t)best_cost * 4u)) sb.best_ref = 0;
+      if (F.num_ref > 1 && F.enable_bipred && do_inter) {  // bi-pred (BIPRED_PART 0: one partition)
+        int r0, r1;
+        TeMv a0[4], a1[4];
+        const int part = 0;
+        te_search_bipred(F, S, sb, bi, part, mv_center, mvp, &r0, &r1, a0, a1);
+        tmp.pb_part = part;
+        tmp.ref_idx0 = r0;
+        tmp.ref_idx1 = r1;
+        for (int i = 0; i < 4; i++) {
+          tmp.mv0[i] = a0[i];
+          tmp.mv1[i] = a1[i];
+        }
+        tmp.mode = TE_BIPRED;
+        tmp.tb_param = 0;
+        const int nbits = te_encode_block(F, S, b, bi, tmp);
+        cost = te_cost(F, bi, bi.rec, size, size, nbits);
+        if (cost < min_cost) {
+          min_cost = cost;
+          te_copy_best(bi, tmp);
+        }
+        // B frames at speed 0 add a joint mv0 = -mv1 search (me_mode 1): rejected by the host
+      }
+    }
+    if (do_intra) {
+      const int max_tb = bi.max_num_tb_part - 1;
+      if (F.intra_rdo) {
+        uint32_t min_icost = TE_MAX_UINT32;
+        int best_mode = TE_DC;
+        for (int im = TE_DC; im < F.num_intra_modes; im++) {
+          tmp.intra_mode = im;
+          for (int tbp = 0; tbp <= max_tb; tbp++) {
+            tmp.tb_param = tbp;
+            tmp.mode = TE_INTRA;
+            const int nbits = te_encode_block(F, S, b, bi, tmp);
+            cost = te_cost(F, bi, bi.rec, size, size, nbits);
+            if (cost < min_icost) {
+              min_icost = cost;
+              best_mode = im;
+            }
+          }
+        }
+        intra_mode = best_mode;
+      } else {
+        te_search_intra(F, S, bi, F.num_intra_modes, &intra_mode);
+      }
+      tmp.intra_mode = intra_mode;
+      for (int tbp = 0; tbp <= max_tb; tbp++) {
+        tmp.tb_param = tbp;
+        tmp.mode = TE_INTRA;
+        const int nbits = te_encode_block(F, S, b, bi, tmp);
+        cost = te_cost(F, bi, bi.rec, size, size, nbits);
+        if (cost < min_cost) {
+          min_cost = cost;
+          te_copy_best(bi, tmp);
+        }
+      }
+    }
+  }
+  b.pos = pos_ref;  // rewind (:2476)
+  return min_cost;
+}
+
+// ---- early skip (enc/encode_block.c:2481-2783) -------------------------------
+// check_early_skip_sub_block (luma, :2505-2538): 2x2-average + (N/2)-point
+// transform against half the threshold (N = 4: plain 4-point transform).
+TE_FN int te_es_luma(TeScratch &S, const uint8_t *org, int os, int size, const uint8_t *pb, int thr) {
+  TeTx &X = S.tx;
+  int n = size;
+  if (size > 4) {
+    const int s2 = size / 2;
+    for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
+      const int i = e / s2, j = e - (e / s2) * s2;
+      const int i2 = 2 * i, j2 = 2 * j;
+      const int a = (int)org[i2 * os + j2] - pb[i2 * size + j2], b = (int)org[i2 * os + j2 + 1] - pb[i2 * size + j2 + 1];
+      const int c = (int)org[(i2 + 1) * os + j2] - pb[(i2 + 1) * size + j2],
+                d = (int)org[(i2 + 1) * os + j2 + 1] - pb[(i2 + 1) * size + j2 + 1];
+      X.R[e] = (int16_t)((a + b + c + d + 2) >> 2);
+    }
+    n = s2;
+  } else {
+    for (int e = TE_LANE; e < 16; e += TE_NL) {
+      const int i = e >> 2, j = e & 3;
+      X.R[e] = (int16_t)((int)org[i * os + j] - pb[i * 4 + j]);
+    }
+  }
+  te_sync();
+  te_fwd_tx(X, n, 0);
+  int flag = 0;
+  for (int e = TE_LANE; e < n * n; e += TE_NL) flag |= te_abs(X.C[e]) > thr;
+  return te_any(flag);
+}
+// check_early_skip_sub_blockC (:2540-2611): column sums of the residual
+// (8x8: all 8 columns over 8 rows; other sizes: the top-left 4x4 only, column
+// pairs) against the threshold
+TE_FN int te_es_chroma(const uint8_t *org, int os, int size, const uint8_t *pb, int thr) {
+  int flag = 0;
+  if (size == 8) {
+    for (int j = TE_LANE; j < 8; j += TE_NL) {
+      int s = 0;
+      for (int i = 0; i < 8; i++) s += (int)org[i * os + j] - pb[i * 8 + j];
+      flag |= te_wrap16(s) > (int)(int16_t)thr;
+    }
+  } else {
+    for (int jp = TE_LANE; jp < 2; jp += TE_NL) {
+      int s = 0;
+      for (int i = 0; i < 4; i++)
+        for (int k = 0; k < 2; k++) s += (int)org[i * os + 2 * jp + k] - pb[i * size + 2 * jp + k];
+      flag |= s > thr;
+    }
+  }
+  return te_any(flag);
+}
+
+// check_early_skip_block, :2613-2741.  Returns 1 when every sub-block is insignificant.
+TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch &S, const TeBlockInfo &bi, const TeParam &p) {
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, size0 = TE_MIN(size, 32);
+  const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
+  const int *T = F.es_thr + ((F.speed > 1 && size == 64) ? 52 * 4 : 0);  // 1.3x threshold for 64x64 at speed 2
+  const int thr_y = T[qpY * 4 + (size0 == 8 ? 0 : (size0 == 16 ? 1 : 2))], thr_c = T[qpC * 4 + 3];
+  const int bip = F.enable_bipred, s0c = size0 / 2;
+  uint8_t *pb = S.pb, *pb0 = S.pb0, *pb1 = S.pb1;
+  for (int i = 0; i < size; i += size0)
+    for (int j = 0; j < size; j += size0) {
+      const uint8_t *oY = F.oy + (ypos + i) * F.osy + xpos + j;
+      const uint8_t *oU = F.ou + ((ypos + i) / 2) * F.osc + (xpos + j) / 2;
+      const uint8_t *oV = F.ov + ((ypos + i) / 2) * F.osc + (xpos + j) / 2;
+      const int ry = (ypos + i) * F.rsy + xpos + j, rc = ((ypos + i) / 2) * F.rsc + (xpos + j) / 2;
+      if (p.dir == 2) {
+        const int sg0 = F.ref_fnum[p.ref_idx0] >= F.frame_num, sg1 = F.ref_fnum[p.ref_idx1] >= F.frame_num;
+        TeMv m0 = te_clip_mv(p.mv0[0], ypos, xpos, F.W, F.H, size0, sg0);
+        TeMv m1 = te_clip_mv(p.mv1[0], ypos, xpos, F.W, F.H, size0, sg1);
+        te_mc_luma(pb0, size0, F.refy[p.ref_idx0] + ry, F.rsy, size0, size0, m0, sg0, bip);
+        te_mc_luma(pb1, size0, F.refy[p.ref_idx1] + ry, F.rsy, size0, size0, m1, sg1, bip);
+        for (int e = TE_LANE; e < size0 * size0; e += TE_NL) pb[e] = (uint8_t)(((int)pb0[e] + (int)pb1[e]) >> 1);
+        te_sync();
+        if (te_es_luma(S, oY, F.osy, size0, pb, thr_y)) return 0;
+        // chroma legs use the unclipped vectors (:2680-2702)
+        for (int c = 0; c < 2; c++) {
+          te_mc_chroma(pb0, s0c, (c ? F.refv : F.refu)[p.ref_idx0] + rc, F.rsc, s0c, s0c, p.mv0[0], sg0);
+          te_mc_chroma(pb1, s0c, (c ? F.refv : F.refu)[p.ref_idx1] + rc, F.rsc, s0c, s0c, p.mv1[0], sg1);
+          for (int e = TE_LANE; e < s0c * s0c; e += TE_NL) pb[e] = (uint8_t)(((int)pb0[e] + (int)pb1[e]) >> 1);
+          te_sync();
+          if (te_es_chroma(c ? oV : oU, F.osc, s0c, pb, thr_c)) return 0;
+        }
+      } else {
+        const int sign = F.ref_fnum[p.ref_idx0] > F.frame_num;
+        // the vector is clipped in place for every sub-block (:2722), and the clipped one serves chroma
+        TeMv mv = te_clip_mv(p.mv0[0], ypos, xpos, F.W, F.H, size0, sign);
+        te_mc_luma(pb, size0, F.refy[p.ref_idx0] + ry, F.rsy, size0, size0, mv, sign, bip);
+        if (te_es_luma(S, oY, F.osy, size0, pb, thr_y)) return 0;
+        te_mc_chroma(pb, s0c, F.refu[p.ref_idx0] + rc, F.rsc, s0c, s0c, mv, sign);
+        if (te_es_chroma(oU, F.osc, s0c, pb, thr_c)) return 0;
+        te_mc_chroma(pb, s0c, F.refv[p.ref_idx0] + rc, F.rsc, s0c, s0c, mv, sign);
+        if (te_es_chroma(oV, F.osc, s0c, pb, thr_c)) return 0;
+      }
+    }
+  return 1;
+}
+
+// search_early_skip_candidates, :2743-2783
+TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch &S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+  uint32_t min_cost = TE_MAX_UINT32;
+  int early = 0;
+  TeParam tmp;
+  memset(&tmp, 0, sizeof(tmp));
+  tmp.coeff = tmp_coef;
+  for (int k = 0; k < bi.num_skip; k++) {
+    tmp.tb_param = 0;
+    tmp.skip_idx = k;
+    tmp.ref_idx0 = bi.skip_c[k].ref_idx0;
+    tmp.ref_idx1 = bi.skip_c[k].ref_idx1;
+    tmp.mv0[0] = bi.skip_c[k].mv0;
+    tmp.mv1[0] = bi.skip_c[k].mv1;
+    tmp.dir = bi.skip_c[k].bipred_flag;
+    if (te_check_early_skip(F, S, bi, tmp)) {
+      early = 1;
+      tmp.mode = TE_SKIP;
+      const int nbits = te_encode_block(F, S, sb.bits, bi, tmp);
+      const uint32_t cost = te_cost(F, bi, bi.rec, bi.size, bi.size, nbits);
+      if (cost < min_cost) {
+        min_cost = cost;
+        te_copy_best(bi, tmp);
+      }
+    }
+  }
+  return early;
+}
+
+// ---- process_block, enc/encode_block.c:2787-3033 ----------------------------
+// Template over the CU size: the quadtree recursion unrolls at compile time
+// (64 -> 32 -> 16 -> 8); level L = log2(64 / SIZE) owns TeScratch::lv[L].
+template <int SIZE>
+TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch &S, TeSB &sb, int ypos, int xpos, int qp) {
+  constexpr int L = SIZE == 64 ? 0 : (SIZE == 32 ? 1 : (SIZE == 16 ? 2 : 3));
+  const int W = F.W, H = F.H, ft = F.frame_type;
+  if (ypos >= H || xpos >= W) return 0;
+  const int encode_this = ypos + SIZE <= H && xpos + SIZE <= W;
+  const int encode_smaller = SIZE > 8 * (encode_this && ft != TE_I && !F.sync && F.speed > 0 ? 2 : 1);
+  const int top_down = !encode_smaller && SIZE > 8;
+  const int encode_rect = !encode_this && ft != TE_I;
+  if (!encode_this && !encode_smaller) return 0;
+  uint32_t cost_small = 1u << 28, cost = 1u << 28;
+  TeBits &b = sb.bits;
+  const int pos_ref = b.pos;
+  TeLevel &lv = S.lv[L];
+  TeBlockInfo bi;
+  memset(&bi, 0, sizeof(bi));
+  bi.ctx = te_block_ctx(ypos, xpos, H, W, SIZE, F.cells, F.use_block_contexts);
+  bi.size = SIZE;
+  bi.bwidth = TE_MIN(SIZE, W - xpos);
+  bi.bheight = TE_MIN(SIZE, H - ypos);
+  bi.ypos = ypos;
+  bi.xpos = xpos;
+  bi.max_num_tb_part = F.enable_tb_split == 1 ? 2 : 1;
+  bi.max_num_pb_part = F.enable_pb_split ? 4 : 1;
+  bi.delta_qp = qp - F.qp;
+  bi.rec = lv.rbuf[0];
+  bi.rec_best = lv.rbuf[1];
+  bi.bp.coeff = lv.cbuf[0];
+  int16_t *tmp_coef = lv.cbuf[1];
+  if (ft != TE_I) {
+    bi.num_skip = te_mv_skip(ypos, xpos, W, H, SIZE, F.cells, bi.skip_c);
+    bi.num_merge = te_mv_skip(ypos, xpos, W, H, SIZE, F.cells, bi.merge_c);
+  }
+  if (encode_this && ft != TE_I && F.early_skip_thr > 0.0f) {
+    bi.final_encode = 2;
+    const int early = te_search_early_skip(F, S, sb, bi, tmp_coef);
+    b.pos = pos_ref;
+    if (early) {
+      bi.final_encode = 3;
+      bi.bp.mode = TE_SKIP;
+      bi.bp.tb_param = 0;
+      const int nbit = te_encode_block(F, S, b, bi, bi.bp);
+      cost = te_cost(F, bi, bi.rec, SIZE, SIZE, nbit);
+      te_commit_block(F, bi);
+      return cost;
+    }
+  }
+  if constexpr (SIZE > 8) {
+    if (encode_smaller) {
+      constexpr int NS = SIZE / 2;
+      if (encode_this) te_write_super_mode(b, F, bi, 0, 0, 1);
+      else if (ft != TE_I) te_put(b, 1, 0);
+      if (SIZE == 64 && F.max_delta_qp) te_write_delta_qp(b, bi.delta_qp);
+      cost_small = 0;
+      cost_small += te_process_block<NS>(F, S, sb, ypos, xpos, qp);
+      cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos, qp);
+      cost_small += te_process_block<NS>(F, S, sb, ypos, xpos + NS, qp);
+      cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos + NS, qp);
+    }
+  }
+  if (encode_this) {
+    bi.final_encode = 0;
+    // the tmp coefficient set: whichever of cbuf[0..1] the best does not hold
+    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == lv.cbuf[0] ? lv.cbuf[1] : lv.cbuf[0]);
+    const int me_threshold = SIZE * SIZE * te_iq8[qp] / 8;
+    if constexpr (SIZE > 8) {
+      if (top_down && cost > (uint32_t)me_threshold) {
+        constexpr int NS = SIZE / 2;
+        te_write_super_mode(b, F, bi, 0, 0, 1);
+        cost_small = 0;
+        cost_small += te_process_block<NS>(F, S, sb, ypos, xpos, qp);
+        cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos, qp);
+        cost_small += te_process_block<NS>(F, S, sb, ypos, xpos + NS, qp);
+        cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos + NS, qp);
+      }
+    }
+    if (cost <= cost_small) {
+      b.pos = pos_ref;
+      bi.final_encode = 1;
+      te_encode_block(F, S, b, bi, bi.bp);
+      te_commit_block(F, bi);
+    }
+  } else if (encode_rect) {
+    bi.final_encode = 0;
+    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == lv.cbuf[0] ? lv.cbuf[1] : lv.cbuf[0]);
+    if (cost <= cost_small) {
+      b.pos = pos_ref;
+      bi.final_encode = 1;
+      bi.bp.mode = TE_SKIP;
+      bi.bp.tb_param = 0;
+      te_encode_block(F, S, b, bi, bi.bp);
+      te_commit_block(F, bi);
+    }
+  }
+  return TE_MIN(cost, cost_small);
+}
+
+// One superblock as encode_frame runs it (enc/encode_frame.c:114-146): reset
+// the ME candidate lists, then process_block(64) -- with the delta-qp RD
+// search when max_delta_qp is set (trials leave their candidates behind, as
+// there).  Returns the SB's bit count in sb.bits.
+TE_FN void te_encode_sb(const TeFrame &F, TeScratch &S, TeSB &sb, int k, int l) {
+  const int ypos = k * 64, xpos = l * 64;
+  for (int r = 0; r < F.num_ref; r++) {
+    sb.mc.num[r] = 0;
+    sb.mc.mask[r] = 0;
+  }
+  sb.best_ref = -1;
+  sb.bits.pos = 0;
+  if (F.max_delta_qp) {
+    int min_cost = 1 << 30, best_qp = F.qp;
+    for (int q = F.qp - F.max_delta_qp; q <= F.qp + F.max_delta_qp; q += F.delta_qp_step) {
+      const int cost = (int)te_process_block<64>(F, S, sb, ypos, xpos, q);
+      if (cost < min_cost) {
+        min_cost = cost;
+        best_qp = q;
+      }
+    }
+    sb.bits.pos = 0;
+    te_process_block<64>(F, S, sb, ypos, xpos, best_qp);
+  } else {
+    te_process_block<64>(F, S, sb, ypos, xpos, F.qp);
+  }
+}
+
+// clpf_decision + the CLPF candidate test of clpf_frame, enc/encode_frame.c:50-63,
+// common/common_frame.c:499-513 (detect_clpf_simd == detect_clpf on full SBs,
+// enc/encode_block.c:3036-3057): for SB (k, l) of the deblocked frame,
+// returns -1 when no 8x8 block is a candidate (no bit), else the flag bit.
+TE_FN int te_clpf_decide(const TeFrame &F, int k, int l) {
+  const int bs = F.W / 4;
+  int cand = 0;
+  uint32_t s0 = 0, s1 = 0;
+  for (int e = TE_LANE; e < 64 * 64; e += TE_NL) {
+    const int y = e >> 6, x = e & 63;
+    const int ypos = k * 64 + y, xpos = l * 64 + x;
+    const TeCell &c = F.cells[(ypos / 4) * bs + xpos / 4];
+    const int blk = (y & 7) == 0 && (x & 7) == 0;
+    if (blk) cand |= c.mode != TE_BIPRED && (c.cbp_y || c.cbp_u || c.cbp_v);
+    const TeCell &c8 = F.cells[((ypos & ~7) / 4) * bs + (xpos & ~7) / 4];
+    if (c8.cbp_y && c8.mode != TE_BIPRED) {
+      const uint8_t *r = F.ry;
+      const int rs = F.rsy;
+      const int X = r[ypos * rs + xpos];
+      const int A = y == 0 ? X : r[(ypos - 1) * rs + xpos];
+      const int B = x == 0 ? X : r[ypos * rs + xpos - 1];
+      const int C = x == 63 ? X : r[ypos * rs + xpos + 1];
+      const int D = y == 63 ? X : r[(ypos + 1) * rs + xpos];
+      const int delta = ((A > X) + (B > X) + (C > X) + (D > X) > 2) - ((A < X) + (B < X) + (C < X) + (D < X) > 2);
+      const int O = F.oy[ypos * F.osy + xpos];
+      s0 += (uint32_t)((O - X) * (O - X));
+      s1 += (uint32_t)((O - X - delta) * (O - X - delta));
+    }
+  }
+  cand = te_any(cand);
+  s0 = te_sum(s0);
+  s1 = te_sum(s1);
+  if (!cand) return -1;
+  return (int)s1 < (int)s0;
+}
