@@ -247,6 +247,32 @@ void thor_enc_default_params(thor_enc_params_t *p);
  * rdoq 0, no interp_ref, no speed-0 B frames). */
 int thor_enc_check_params(const thor_enc_params_t *p);
 
+/* A device-resident encoder context: the reference's frame loop
+ * (enc/mainenc.c:222-591) planned on the host, every frame's RD loop, loop
+ * filters and bit packing on the GPU (wavefront-parallel superblock rows).
+ * The output is the reference Thorenc's .bit, byte for byte. */
+typedef struct thor_enc thor_enc_t;
+thor_enc_t *thor_enc_create(const thor_enc_params_t *p, int device);
+void thor_enc_destroy(thor_enc_t *e);
+/* frames the context will code (params.num_frames after -skip) */
+int thor_enc_num_frames(const thor_enc_t *e);
+/* input frame (display order, 0 = first after -skip) the next call codes;
+ * -1 when every frame is coded */
+int thor_enc_next_input(const thor_enc_t *e);
+void *thor_enc_stream(thor_enc_t *e);
+/* Code the next frame of each of `n` DIFFERENT contexts (same device and
+ * size, n <= 16) with one launch per stage.  orig[i]: DEVICE pointer to the
+ * context's input frame thor_enc_next_input(es[i]), planar I420, luma stride
+ * orig_stride[i] (NULL: width), chroma stride half of it.  Synchronous. */
+int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
+int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride);
+/* The last coded frame's .bit chunk (4-byte big-endian length + payload,
+ * enc/putbits.c:57-95; the first chunk carries the sequence header):
+ * returns its size, copies min(size, cap) bytes to dst when non-NULL. */
+long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap);
+/* The last coded frame's reconstruction (deblocked, CLPF'd), host planes. */
+int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
+
 /* ---- temporal interpolation: luma down-sampling pyramid ----------------- */
 
 /* Number of down-sampled levels interpolate_frames builds for a width x height

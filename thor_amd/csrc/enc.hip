@@ -1,0 +1,580 @@
+// Device-resident Thor encoder for gfx950: kernels and the host C-ABI
+// (include/thor_amd.h, "device-resident encoder").
+//
+// Per frame (and per batch of up to THOR_ENC_MAX_BATCH streams, one launch
+// per stage for all of them):
+//   k_enc_rows      WPP superblock rows: one wave64 per SB row (tickets handed
+//                   out in order, so a row only ever waits on rows held by
+//                   running waves); SB (k, l) starts when SB (k-1, l+1) is
+//                   done (the up-right neighbour is the furthest one the RD
+//                   loop reads, enc/encode_block.c:2819-2879).  The RD loop of
+//                   the SB (enc_rd.h) writes the reconstruction into the ring
+//                   slot, the 4x4 side info and the SB's bit string.
+//   k_enc_cellinfo  side info -> the decoder's 16-bit cell words
+//   k_deblock_v/h   the decoder's loop filter kernels (loopfilter.hip)
+//   k_enc_clpf      CLPF decision per full SB (clpf_decision, enc/encode_frame.c:50-63)
+//   k_clpf, k_pad   the decoder's CLPF and padding kernels
+//   k_enc_pack      frame header + SB bit strings + CLPF bits -> the frame's
+//                   bytes (putbits / flush_all_bits, enc/putbits.c:57-129)
+#include "common.h"
+#include "enc_gop.h"
+#include "enc_rd.h"
+
+#define THOR_ENC_MAX_BATCH 16
+#define THOR_ENC_SB_WORDS 4096  // 131072 bits of one SB's stream (trial writes included)
+
+__global__ void k_deblock_v(const FrameBatch, int, int);
+__global__ void k_deblock_h(const FrameBatch, int, int);
+__global__ void k_clpf(const FrameBatch);
+__global__ void k_pad(const FrameBatch);
+
+// One stream's frame job (device memory, one per stream of a launch).
+struct TeJob {
+  TeFrame F;
+  uint32_t *sb_words;   // [nsb][THOR_ENC_SB_WORDS]
+  int *sb_nbits;        // [nsb]
+  unsigned *progress;   // [nsbv] SBs finished per row
+  int8_t *clpf_bits;    // [nsb_full]: -1 no bit, else the flag
+  uint8_t *clpf_flags;  // [nsb_full]: CLPF applied (k_clpf input)
+  uint16_t *cellinfo;
+  const uint32_t *hdr_words;  // frame header (+ sequence header) bits, MSB first
+  int hdr_bits;
+  uint32_t *out_words;  // packed frame
+  int *out_bits;
+  int nsbh, nsbv, clpf;
+};
+
+__device__ __forceinline__ unsigned te_ld_acquire(const unsigned *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// WPP worker: grid of persistent single-wave workgroups; ticket t -> stream
+// t % n, SB row t / n.
+__global__ __launch_bounds__(64) void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
+                                                 TeScratch *scratch, TeSB *sbs, unsigned *err) {
+  TeScratch &S = scratch[blockIdx.x];
+  TeSB &sb = sbs[blockIdx.x];
+  const int lane = threadIdx.x;
+  for (;;) {
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(ticket, 1u);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if ((int)t >= n * nrows) break;
+    const int s = (int)t % n, k = (int)t / n;
+    const TeJob &J = jobs[s];
+    if (k >= J.nsbv) continue;
+    for (int l = 0; l < J.nsbh; l++) {
+      if (k > 0) {  // SB (k-1, l+1) (or the whole row above) must be done
+        const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
+        if (lane == 0) {
+          long long spins = 0;
+          while (te_ld_acquire(&J.progress[k - 1]) < need) {
+            __builtin_amdgcn_s_sleep(4);
+            if (++spins > (1LL << 26)) {  // a wedged dependency: give up (reported), never hang the GPU
+              atomicOr(err, 1u);
+              break;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      const int sbi = k * J.nsbh + l;
+      sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
+      sb.bits.cap = THOR_ENC_SB_WORDS * 32;
+      te_encode_sb(J.F, S, sb, k, l);
+      if (lane == 0) {
+        J.sb_nbits[sbi] = sb.bits.pos;
+        if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) __hip_atomic_store(&J.progress[k], (unsigned)(l + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// TeCell (deblock_data_t) -> the 16-bit cell words the decoder's loop filter
+// kernels read (same packing as prep_body, recon.hip).
+__global__ __launch_bounds__(256) void k_enc_cellinfo(const TeJob *__restrict__ jobs) {
+  const TeJob &J = jobs[blockIdx.y];
+  const int ncell = (J.F.W >> 2) * (J.F.H >> 2);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ncell) return;
+  const TeCell c = J.F.cells[i];
+  const int size = c.size < 8 ? 8 : c.size;
+  const int lsz = size >= 64 ? 6 : (size >= 32 ? 5 : (size >= 16 ? 4 : 3));
+  const int tb = c.tb_split > 0, pb = c.pb_part;
+  const int lqv = lsz - (((tb || pb == 2 || pb == 3) && size > 8) ? 1 : 0);
+  const int lqh = lsz - (((tb || pb == 1 || pb == 3) && size > 8) ? 1 : 0);
+  const int big = (abs(c.ip.mv0.x) >= 4) | (abs(c.ip.mv0.y) >= 4) | (abs(c.ip.mv1.x) >= 4) | (abs(c.ip.mv1.y) >= 4);
+  J.cellinfo[i] = (uint16_t)((c.mode & 7) | ((c.cbp_y != 0) << 3) | ((c.cbp_u != 0) << 4) | ((c.cbp_v != 0) << 5) |
+                             (big << 6) | (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
+}
+
+// CLPF decision of every full SB (after deblocking), one wave per SB.
+__global__ __launch_bounds__(64) void k_enc_clpf(const TeJob *__restrict__ jobs) {
+  const TeJob &J = jobs[blockIdx.y];
+  const int nh = J.F.W >> 6, nv = J.F.H >> 6;
+  const int sb = blockIdx.x;
+  if (sb >= nh * nv || !J.clpf) return;
+  const int d = te_clpf_decide(J.F, sb / nh, sb % nh);
+  if (threadIdx.x == 0) {
+    J.clpf_bits[sb] = (int8_t)d;
+    J.clpf_flags[sb] = (uint8_t)(d == 1);
+  }
+}
+
+// Frame bit string: header | SB strings (raster) | [CLPF: 1, 0, one bit per
+// candidate SB] -> MSB-first words, zero padded.  One workgroup per stream.
+__device__ __forceinline__ void te_or_bits(uint32_t *dst, long long pos, const uint32_t *src, int n) {
+  for (int j = 0; j * 32 < n; j++) {
+    uint32_t w = src[j];
+    const int nb = n - j * 32 < 32 ? n - j * 32 : 32;
+    if (nb < 32) w &= ~(0xffffffffu >> nb);  // drop stale bits past the string's end
+    const long long p = pos + 32LL * j;
+    const int sh = (int)(p & 31);
+    atomicOr(&dst[p >> 5], w >> sh);
+    if (sh && (w << (32 - sh))) atomicOr(&dst[(p >> 5) + 1], w << (32 - sh));
+  }
+}
+__global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs, long long *scan_tmp, int out_cap_words) {
+  const TeJob &J = jobs[blockIdx.x];
+  const int nsb = J.nsbh * J.nsbv;
+  long long *off = scan_tmp + (size_t)blockIdx.x * (nsb + 1);
+  __shared__ long long total;
+  if (threadIdx.x == 0) {
+    long long o = J.hdr_bits;
+    for (int i = 0; i < nsb; i++) {
+      off[i] = o;
+      o += J.sb_nbits[i];
+    }
+    off[nsb] = o;
+    if (J.clpf) {
+      o += 2;
+      const int nf = (J.F.W >> 6) * (J.F.H >> 6);
+      for (int i = 0; i < nf; i++) o += J.clpf_bits[i] >= 0;
+    }
+    total = o;
+  }
+  __syncthreads();
+  const long long nw = (total + 31) >> 5;
+  if (nw > out_cap_words) {
+    if (threadIdx.x == 0) *J.out_bits = -1;
+    return;
+  }
+  for (long long i = threadIdx.x; i < nw + 1 && i < out_cap_words; i += 256) J.out_words[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) te_or_bits(J.out_words, 0, J.hdr_words, J.hdr_bits);
+  for (int i = threadIdx.x; i < nsb; i += 256)
+    te_or_bits(J.out_words, off[i], J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, J.sb_nbits[i]);
+  if (threadIdx.x == 0 && J.clpf) {
+    long long p = off[nsb];
+    const uint32_t two = 0x80000000u;  // bits 1, 0
+    te_or_bits(J.out_words, p, &two, 2);
+    p += 2;
+    const int nf = (J.F.W >> 6) * (J.F.H >> 6);
+    for (int i = 0; i < nf; i++) {
+      const int d = J.clpf_bits[i];
+      if (d < 0) continue;
+      if (d) atomicOr(&J.out_words[p >> 5], 0x80000000u >> (p & 31));
+      p++;
+    }
+  }
+  if (threadIdx.x == 0) *J.out_bits = (int)total;
+}
+
+// ============================================================================
+// Host side
+// ============================================================================
+#define EHIP(x)                                                                                        \
+  do {                                                                                                  \
+    hipError_t e_ = (x);                                                                                \
+    if (e_ != hipSuccess) {                                                                             \
+      fprintf(stderr, "thor_amd enc: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return THOR_ERR_HIP;                                                                              \
+    }                                                                                                   \
+  } while (0)
+
+struct thor_enc {
+  thor_enc_params_t p;
+  TeGop *gop;
+  size_t pos;  // next plan
+  int device;
+  hipStream_t stream;
+  int W, H, nsbh, nsbv, nsb, nsb_full;
+  int sy, sc;
+  long long offy, offu, offv, slot_bytes;
+  int nslots;
+  uint8_t *slots;
+  std::vector<int> slot_of_window;  // window index -> slot (-1: empty)
+  std::vector<int> slot_busy;
+  TeCell *cells;
+  uint16_t *cellinfo;
+  uint32_t *sb_words;
+  int *sb_nbits;
+  unsigned *progress;
+  int8_t *clpf_bits;
+  uint8_t *clpf_flags;
+  int *es_thr;
+  uint32_t *hdr_words;   // device, 64 words
+  uint32_t *out_words;   // device
+  int out_cap_words;
+  int *out_bits;         // device
+  // last coded frame
+  int last_slot, last_frame_num;
+  std::vector<uint8_t> chunk;  // 4-byte length + bytes of the last frame
+  bool first;
+};
+
+static int enc_alloc(thor_enc *e) {
+  const int W = e->W, H = e->H;
+  e->sy = (W + 2 * THOR_PAD_Y + 15) & ~15;
+  e->sc = (W / 2 + 2 * THOR_PAD_C + 15) & ~15;
+  long long yb = ((long long)(H + 2 * THOR_PAD_Y) * e->sy + 255) & ~255LL;
+  long long cb = ((long long)(H / 2 + 2 * THOR_PAD_C) * e->sc + 255) & ~255LL;
+  e->offy = (long long)THOR_PAD_Y * e->sy + THOR_PAD_Y;
+  e->offu = yb + (long long)THOR_PAD_C * e->sc + THOR_PAD_C;
+  e->offv = yb + cb + (long long)THOR_PAD_C * e->sc + THOR_PAD_C;
+  e->slot_bytes = yb + 2 * cb + 256;
+  e->nslots = 34;  // the 33-frame window + the frame being coded
+  EHIP(hipMalloc(&e->slots, e->slot_bytes * e->nslots));
+  EHIP(hipMemset(e->slots, 0, e->slot_bytes * e->nslots));
+  const size_t ncell = (size_t)(W / 4) * (H / 4);
+  EHIP(hipMalloc(&e->cells, ncell * sizeof(TeCell)));
+  EHIP(hipMalloc(&e->cellinfo, ncell * sizeof(uint16_t)));
+  EHIP(hipMalloc(&e->sb_words, (size_t)e->nsb * THOR_ENC_SB_WORDS * 4));
+  EHIP(hipMalloc(&e->sb_nbits, (size_t)e->nsb * sizeof(int)));
+  EHIP(hipMalloc(&e->progress, (size_t)e->nsbv * sizeof(unsigned)));
+  EHIP(hipMalloc(&e->clpf_bits, (size_t)e->nsb_full + 1));
+  EHIP(hipMalloc(&e->clpf_flags, (size_t)e->nsb_full + 1));
+  EHIP(hipMalloc(&e->es_thr, 2 * 52 * 4 * sizeof(int)));
+  EHIP(hipMalloc(&e->hdr_words, 64 * 4));
+  e->out_cap_words = (int)(((size_t)W * H * 2) / 4 + 1024);  // 16 bits per pixel: far above any real frame
+  EHIP(hipMalloc(&e->out_words, (size_t)e->out_cap_words * 4 + 8));
+  EHIP(hipMalloc(&e->out_bits, sizeof(int)));
+  std::vector<int> es(2 * 52 * 4);
+  te_es_thresholds(e->p.early_skip_thr, es.data());
+  EHIP(hipMemcpy(e->es_thr, es.data(), es.size() * sizeof(int), hipMemcpyHostToDevice));
+  return THOR_OK;
+}
+
+// Work pools shared by the streams of one launch (per device)
+struct EncPool {
+  int device = -1;
+  size_t nwork = 0;
+  TeScratch *scratch = nullptr;
+  TeSB *sbs = nullptr;
+  unsigned *ticket = nullptr, *err = nullptr;
+  TeJob *jobs = nullptr;
+  long long *scan = nullptr;
+  size_t scan_n = 0;
+};
+static EncPool g_pool;
+
+static int pool_reserve(int device, size_t nwork, size_t scan_n) {
+  if (g_pool.device != device) {
+    g_pool = EncPool();
+    g_pool.device = device;
+    EHIP(hipMalloc(&g_pool.ticket, 64));
+    EHIP(hipMalloc(&g_pool.err, 64));
+    EHIP(hipMemset(g_pool.err, 0, 64));
+    EHIP(hipMalloc(&g_pool.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
+  }
+  if (nwork > g_pool.nwork) {
+    if (g_pool.scratch) (void)hipFree(g_pool.scratch);
+    if (g_pool.sbs) (void)hipFree(g_pool.sbs);
+    EHIP(hipMalloc(&g_pool.scratch, nwork * sizeof(TeScratch)));
+    EHIP(hipMalloc(&g_pool.sbs, nwork * sizeof(TeSB)));
+    EHIP(hipMemset(g_pool.sbs, 0, nwork * sizeof(TeSB)));
+    g_pool.nwork = nwork;
+  }
+  if (scan_n > g_pool.scan_n) {
+    if (g_pool.scan) (void)hipFree(g_pool.scan);
+    EHIP(hipMalloc(&g_pool.scan, scan_n * sizeof(long long)));
+    g_pool.scan_n = scan_n;
+  }
+  return THOR_OK;
+}
+
+extern "C" {
+
+void thor_enc_default_params(thor_enc_params_t *p) {
+  if (p) te_default_params(p);
+}
+int thor_enc_check_params(const thor_enc_params_t *p) { return p ? te_check_params(p) : THOR_ERR_ARG; }
+
+thor_enc_t *thor_enc_create(const thor_enc_params_t *p, int device) {
+  if (!p || te_check_params(p) != THOR_OK) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  thor_enc *e = new thor_enc();
+  e->p = *p;
+  e->gop = new TeGop(*p);
+  e->pos = 0;
+  e->device = device;
+  e->W = p->width;
+  e->H = p->height;
+  e->nsbh = (e->W + 63) / 64;
+  e->nsbv = (e->H + 63) / 64;
+  e->nsb = e->nsbh * e->nsbv;
+  e->nsb_full = (e->W / 64) * (e->H / 64);
+  e->first = true;
+  e->last_slot = -1;
+  e->last_frame_num = -1;
+  e->slot_of_window.assign(33, -1);
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || enc_alloc(e) != THOR_OK) {
+    thor_enc_destroy(e);
+    return nullptr;
+  }
+  e->slot_busy.assign(e->nslots, 0);
+  return e;
+}
+
+void thor_enc_destroy(thor_enc_t *e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->progress,
+                  e->clpf_bits, e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_bits};
+  for (void *b : bufs)
+    if (b) (void)hipFree(b);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e->gop;
+  delete e;
+}
+
+int thor_enc_num_frames(const thor_enc_t *e) { return e ? (int)e->gop->plans.size() : THOR_ERR_ARG; }
+// input frame index (display order, after -skip) the next call codes; -1 when done
+int thor_enc_next_input(const thor_enc_t *e) {
+  if (!e) return THOR_ERR_ARG;
+  return e->pos < e->gop->plans.size() ? e->gop->plans[e->pos].input_index : -1;
+}
+void *thor_enc_stream(thor_enc_t *e) { return e ? (void *)e->stream : nullptr; }
+
+static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob &J, TeFramePlan &pl, int &cur_slot) {
+  pl = e->gop->plans[e->pos];
+  // the frame being coded takes a slot no window entry holds
+  std::vector<int> held(e->nslots, 0);
+  for (int w = 0; w < 33; w++)
+    if (e->slot_of_window[w] >= 0) held[e->slot_of_window[w]] = 1;
+  cur_slot = -1;
+  for (int s = 0; s < e->nslots && cur_slot < 0; s++)
+    if (!held[s]) cur_slot = s;
+  if (cur_slot < 0) return THOR_ERR_REF;
+  memset(&J, 0, sizeof(J));
+  TeFrame &F = J.F;
+  const int W = e->W, H = e->H;
+  F.oy = orig;
+  F.ou = orig + (size_t)orig_stride * H;
+  F.ov = F.ou + (size_t)(orig_stride / 2) * (H / 2);
+  F.osy = orig_stride;
+  F.osc = orig_stride / 2;
+  uint8_t *cur = e->slots + (long long)cur_slot * e->slot_bytes;
+  F.ry = cur + e->offy;
+  F.ru = cur + e->offu;
+  F.rv = cur + e->offv;
+  F.rsy = e->sy;
+  F.rsc = e->sc;
+  for (int r = 0; r < pl.num_ref; r++) {
+    const int w = pl.ref_array[r];
+    if (w < 0 || w >= 33 || e->slot_of_window[w] < 0) return THOR_ERR_REF;
+    const uint8_t *rs = e->slots + (long long)e->slot_of_window[w] * e->slot_bytes;
+    F.refy[r] = rs + e->offy;
+    F.refu[r] = rs + e->offu;
+    F.refv[r] = rs + e->offv;
+    F.ref_fnum[r] = pl.ref_fnum[r];
+  }
+  F.cells = e->cells;
+  F.W = W;
+  F.H = H;
+  F.frame_num = pl.frame_num;
+  F.frame_type = pl.frame_type;
+  F.qp = pl.qp;
+  F.num_ref = pl.num_ref;
+  F.num_intra_modes = pl.num_intra_modes;
+  F.interp_ref = pl.interp_ref;
+  F.lambda = pl.lambda;
+  F.sqrt_lambda = sqrt(pl.lambda);
+  const thor_enc_params_t &P = e->p;
+  F.speed = P.encoder_speed;
+  F.enable_tb_split = P.enable_tb_split;
+  F.enable_pb_split = P.enable_pb_split;
+  F.enable_bipred = P.enable_bipred;
+  F.max_delta_qp = P.max_delta_qp;
+  F.delta_qp_step = P.delta_qp_step;
+  F.intra_rdo = P.intra_rdo;
+  F.use_block_contexts = P.use_block_contexts;
+  F.rdoq = P.rdoq;
+  F.sync = P.sync;
+  F.early_skip_thr = P.early_skip_thr;
+  F.es_thr = e->es_thr;
+  J.sb_words = e->sb_words;
+  J.sb_nbits = e->sb_nbits;
+  J.progress = e->progress;
+  J.clpf_bits = e->clpf_bits;
+  J.clpf_flags = e->clpf_flags;
+  J.cellinfo = e->cellinfo;
+  J.hdr_words = e->hdr_words;
+  J.out_words = e->out_words;
+  J.out_bits = e->out_bits;
+  J.nsbh = e->nsbh;
+  J.nsbv = e->nsbv;
+  J.clpf = P.clpf;
+  // header bits (sequence header before the first frame)
+  TeHostBits hb;
+  if (e->first) te_seq_header(hb, P);
+  te_frame_header(hb, pl);
+  std::vector<uint32_t> hw(64, 0);
+  for (uint64_t i = 0; i < hb.nbits; i++)
+    if (hb.bytes[i >> 3] & (0x80 >> (i & 7))) hw[i >> 5] |= 0x80000000u >> (i & 31);
+  J.hdr_bits = (int)hb.nbits;
+  EHIP(hipMemcpyAsync(e->hdr_words, hw.data(), 64 * 4, hipMemcpyHostToDevice, e->stream));
+  EHIP(hipMemsetAsync(e->cells, 0, (size_t)(W / 4) * (H / 4) * sizeof(TeCell), e->stream));
+  EHIP(hipMemsetAsync(e->progress, 0, (size_t)e->nsbv * sizeof(unsigned), e->stream));
+  return THOR_OK;
+}
+
+// Encode the next frame (coding order) of each of `n` contexts with one
+// launch per stage.  orig[i]: DEVICE pointer to context i's input frame
+// thor_enc_next_input(es[i]) as planar I420 (luma stride orig_stride[i],
+// chroma stride / 2).  All contexts must share device and frame size.  The
+// coded frames are read with thor_enc_frame_bytes.
+int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
+  if (!es || !orig || n <= 0 || n > THOR_ENC_MAX_BATCH) return THOR_ERR_ARG;
+  thor_enc *lead = es[0];
+  for (int i = 0; i < n; i++) {
+    if (!es[i] || !orig[i] || es[i]->device != lead->device || es[i]->W != lead->W || es[i]->H != lead->H)
+      return THOR_ERR_ARG;
+    if (es[i]->pos >= es[i]->gop->plans.size()) return THOR_ERR_ARG;
+    for (int j = 0; j < i; j++)
+      if (es[j] == es[i]) return THOR_ERR_ARG;
+  }
+  EHIP(hipSetDevice(lead->device));
+  const int W = lead->W, H = lead->H;
+  const int nrows = lead->nsbv;
+  const int nwork = n * nrows;
+  int rc = pool_reserve(lead->device, (size_t)nwork, (size_t)n * (lead->nsb + 1));
+  if (rc != THOR_OK) return rc;
+  hipStream_t st = lead->stream;
+  std::vector<TeJob> jobs(n);
+  std::vector<TeFramePlan> plans(n);
+  std::vector<int> cur(n);
+  for (int i = 0; i < n; i++) {
+    thor_enc *e = es[i];
+    if (e->stream != st) {  // the members' earlier work on their own streams comes first
+      EHIP(hipStreamSynchronize(e->stream));
+    }
+    const int s = orig_stride ? orig_stride[i] : W;
+    if ((rc = enc_prepare(e, orig[i], s, jobs[i], plans[i], cur[i])) != THOR_OK) return rc;
+    EHIP(hipStreamSynchronize(e->stream));  // per-context header / memsets (tiny) before the shared stream
+  }
+  EHIP(hipMemcpyAsync(g_pool.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
+  EHIP(hipMemsetAsync(g_pool.ticket, 0, 4, st));
+  k_enc_rows<<<nwork, 64, 0, st>>>(g_pool.jobs, n, g_pool.ticket, nrows, g_pool.scratch, g_pool.sbs, g_pool.err);
+  EHIP(hipGetLastError());
+  const int ncell = (W / 4) * (H / 4);
+  k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(g_pool.jobs);
+  EHIP(hipGetLastError());
+  // loop filters: the decoder's kernels over each stream's frame
+  for (int o = 0; o < n; o += THOR_MAX_BATCH) {
+    const int m = n - o < THOR_MAX_BATCH ? n - o : THOR_MAX_BATCH;
+    FrameBatch fb;
+    memset(&fb, 0, sizeof(fb));
+    for (int i = 0; i < m; i++) {
+      thor_enc *e = es[o + i];
+      FrameCtx &f = fb.f[i];
+      uint8_t *c = e->slots + (long long)cur[o + i] * e->slot_bytes;
+      f.cy = c + e->offy;
+      f.cu = c + e->offu;
+      f.cv = c + e->offv;
+      f.sy = e->sy;
+      f.sc = e->sc;
+      f.W = W;
+      f.H = H;
+      f.cellinfo = e->cellinfo;
+      f.qp = plans[o + i].qp;
+      f.qpc = chroma_qp_host(plans[o + i].qp);
+      f.deblock = e->p.deblocking;
+      f.clpf_on = e->p.clpf;
+      f.clpf_flags = e->clpf_flags;
+      f.n_clpf = -1;
+      f.frame_num = plans[o + i].frame_num;
+    }
+    if (lead->p.deblocking) {
+      const int nv = ((W >> 3) - 1) * (H >> 3), nh = (W >> 3) * ((H >> 3) - 1);
+      const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
+      k_deblock_v<<<dim3(3 * bv, m), 256, 0, st>>>(fb, bv, 0);
+      k_deblock_h<<<dim3(3 * bh, m), 256, 0, st>>>(fb, bh, 0);
+      EHIP(hipGetLastError());
+    }
+    if (lead->p.clpf && lead->nsb_full > 0) {
+      k_enc_clpf<<<dim3(lead->nsb_full, m), 64, 0, st>>>(g_pool.jobs + o);
+      k_clpf<<<dim3(lead->nsb_full, m), 256, 0, st>>>(fb);
+      EHIP(hipGetLastError());
+    }
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, m), 256, 0, st>>>(fb);
+    EHIP(hipGetLastError());
+  }
+  k_enc_pack<<<n, 256, 0, st>>>(g_pool.jobs, g_pool.scan, lead->out_cap_words);
+  EHIP(hipGetLastError());
+  // read back every stream's frame
+  std::vector<int> nbits(n);
+  for (int i = 0; i < n; i++) EHIP(hipMemcpyAsync(&nbits[i], es[i]->out_bits, sizeof(int), hipMemcpyDeviceToHost, st));
+  EHIP(hipStreamSynchronize(st));
+  unsigned err = 0;
+  EHIP(hipMemcpy(&err, g_pool.err, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (err) {
+    fprintf(stderr, "thor_amd enc: device error flags 0x%x\n", err);
+    EHIP(hipMemset(g_pool.err, 0, 4));
+    return THOR_ERR_HIP;
+  }
+  for (int i = 0; i < n; i++) {
+    thor_enc *e = es[i];
+    if (nbits[i] < 0) return THOR_ERR_NOMEM;
+    const size_t nb = ((size_t)nbits[i] + 7) / 8, nw = (nb + 3) / 4;
+    std::vector<uint32_t> w(nw + 1);
+    EHIP(hipMemcpyAsync(w.data(), e->out_words, nw * 4, hipMemcpyDeviceToHost, st));
+    EHIP(hipStreamSynchronize(st));
+    e->chunk.resize(4 + nb);
+    e->chunk[0] = (uint8_t)(nb >> 24);
+    e->chunk[1] = (uint8_t)(nb >> 16);
+    e->chunk[2] = (uint8_t)(nb >> 8);
+    e->chunk[3] = (uint8_t)nb;
+    for (size_t b = 0; b < nb; b++) e->chunk[4 + b] = (uint8_t)(w[b >> 2] >> (24 - 8 * (b & 3)));
+    // slide the window: the frame shifted out of ref[32] frees its slot
+    for (int r = 32; r > 0; r--) e->slot_of_window[r] = e->slot_of_window[r - 1];
+    e->slot_of_window[0] = cur[i];
+    e->last_slot = cur[i];
+    e->last_frame_num = plans[i].frame_num;
+    e->first = false;
+    e->pos++;
+  }
+  return THOR_OK;
+}
+
+int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride) {
+  return thor_enc_frames(&e, 1, &orig, &orig_stride);
+}
+
+// Bytes of the frame the last thor_enc_frame(s) call coded: the .bit chunk
+// (4-byte big-endian length + payload, enc/putbits.c:57-95).  Returns the
+// chunk size; copies min(size, cap) bytes when dst is non-NULL.
+long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap) {
+  if (!e) return THOR_ERR_ARG;
+  if (dst) memcpy(dst, e->chunk.data(), e->chunk.size() < cap ? e->chunk.size() : cap);
+  return (long long)e->chunk.size();
+}
+
+// The reconstruction of the last coded frame (deblocked, CLPF'd), host planes.
+int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v) {
+  if (!e || e->last_slot < 0) return THOR_ERR_ARG;
+  EHIP(hipSetDevice(e->device));
+  EHIP(hipStreamSynchronize(e->stream));
+  const uint8_t *b = e->slots + (long long)e->last_slot * e->slot_bytes;
+  if (y) EHIP(hipMemcpy2D(y, e->W, b + e->offy, e->sy, e->W, e->H, hipMemcpyDeviceToHost));
+  if (u) EHIP(hipMemcpy2D(u, e->W / 2, b + e->offu, e->sc, e->W / 2, e->H / 2, hipMemcpyDeviceToHost));
+  if (v) EHIP(hipMemcpy2D(v, e->W / 2, b + e->offv, e->sc, e->W / 2, e->H / 2, hipMemcpyDeviceToHost));
+  return THOR_OK;
+}
+
+}  // extern "C"

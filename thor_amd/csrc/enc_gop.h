@@ -52,6 +52,7 @@ struct TeFramePlan {
   int frame_num;    // frame_info.frame_num
   int frame_type, qp, b_level, num_ref, interp_ref, num_intra_modes;
   int ref_array[TE_GOP_MAX_REF];  // indices into the sliding window (ref[0] = most recently coded)
+  int ref_fnum[TE_GOP_MAX_REF];   // frame numbers of those references when this frame is coded
   double lambda;
 };
 
@@ -192,6 +193,8 @@ struct TeGop {
           for (int s = r; s < f.num_ref - 1; ++s) ra[s] = ra[s + 1];
           f.num_ref--;
         }
+    for (int r = 0; r < TE_GOP_MAX_REF; r++)
+      f.ref_fnum[r] = (r < f.num_ref && ra[r] >= 0 && ra[r] < 33) ? window_fnum[ra[r]] : -1;
     f.num_intra_modes = (P.intra_rdo == 0 || (f.frame_type != 0 && P.encoder_speed > 0)) ? 4 : 10;
     // lambda (enc/encode_frame.c:77-94): float coefficients promoted to double
     float lc;

@@ -1,0 +1,110 @@
+"""Host driver of the device-resident encoder (libthor_amd.so, thor_enc_*).
+
+`GpuEncoder(params)` owns one encoder context: the reference's frame loop
+(coding order, QP, references -- enc/mainenc.c) is planned inside the library;
+each call codes the next frame on the GPU and returns its .bit chunk.  The
+input sequence is uploaded to HBM once (`upload_sequence`) so that coding reads
+only device memory.  No CPU fallback: without the library or a GPU, calls fail."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import lib as L
+from .configs import flags as config_flags
+
+
+def params_from_flags(flag_list) -> L.ThorEncParams:
+    """thor_enc_params_t from `-flag value` pairs over the reference defaults
+    (enc/strings.c:286-338)."""
+    lib = L.load()
+    p = L.ThorEncParams()
+    lib.thor_enc_default_params(C.byref(p))
+    it = list(flag_list)
+    alias = {"-n": "num_frames", "-f": "frame_rate"}
+    for k, v in zip(it[0::2], it[1::2]):
+        name = alias.get(k, k.lstrip("-"))
+        if not hasattr(p, name):
+            raise KeyError("unknown encoder parameter %s" % k)
+        cur = getattr(p, name)
+        setattr(p, name, float(v) if isinstance(cur, float) else int(v))
+    return p
+
+
+def params_for(config: str, width: int, height: int, frames: int, extra=()) -> L.ThorEncParams:
+    return params_from_flags(config_flags(config, width, height, frames, extra))
+
+
+class GpuEncoder:
+    def __init__(self, params: L.ThorEncParams, device: int = 0):
+        self.lib = L.load()
+        self.p = params
+        if self.lib.thor_enc_check_params(C.byref(params)) != 0:
+            raise ValueError("encoder parameters not supported")
+        self.h = self.lib.thor_enc_create(C.byref(params), device)
+        if not self.h:
+            raise RuntimeError("thor_enc_create failed")
+        self.W, self.H = params.width, params.height
+        self.fsize = self.W * self.H * 3 // 2
+        self.seq_dev = None
+        self.nin = 0
+
+    def close(self):
+        if self.h:
+            self.lib.thor_enc_destroy(self.h)
+            self.h = None
+        if self.seq_dev:
+            self.lib.thor_dev_free(self.seq_dev)
+            self.seq_dev = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_sequence(self, frames: np.ndarray):
+        """frames: uint8 array (n, W*H*3/2) of I420 input frames, display order."""
+        a = np.ascontiguousarray(frames, dtype=np.uint8).reshape(-1, self.fsize)
+        self.nin = a.shape[0]
+        self.seq_dev = self.lib.thor_dev_alloc(a.nbytes)
+        if not self.seq_dev:
+            raise MemoryError("thor_dev_alloc")
+        L.check(self.lib.thor_h2d(self.seq_dev, a.ctypes.data, a.nbytes), "thor_h2d")
+
+    def num_frames(self) -> int:
+        return self.lib.thor_enc_num_frames(self.h)
+
+    def next_input_ptr(self):
+        k = self.lib.thor_enc_next_input(self.h)
+        if k < 0:
+            return None
+        if k >= self.nin:
+            raise IndexError("input frame %d not uploaded" % k)
+        return self.seq_dev + k * self.fsize
+
+    def encode_next(self) -> bytes:
+        ptr = self.next_input_ptr()
+        L.check(self.lib.thor_enc_frame(self.h, ptr, self.W), "thor_enc_frame")
+        return self.chunk()
+
+    def chunk(self) -> bytes:
+        n = self.lib.thor_enc_frame_bytes(self.h, None, 0)
+        buf = C.create_string_buffer(n)
+        self.lib.thor_enc_frame_bytes(self.h, buf, n)
+        return buf.raw
+
+    def encode_all(self) -> bytes:
+        return b"".join(self.encode_next() for _ in range(self.num_frames()))
+
+
+def encode_batch(encs):
+    """Code the next frame of every encoder in `encs` with one launch per stage."""
+    n = len(encs)
+    lib = encs[0].lib
+    hs = (C.c_void_p * n)(*[e.h for e in encs])
+    ptrs = (C.c_void_p * n)(*[e.next_input_ptr() for e in encs])
+    strides = (C.c_int * n)(*[e.W for e in encs])
+    L.check(lib.thor_enc_frames(hs, n, ptrs, strides), "thor_enc_frames")
+    return [e.chunk() for e in encs]

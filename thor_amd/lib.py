@@ -21,6 +21,19 @@ class ThorFrameHdr(C.Structure):
     _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32)]
 
 
+class ThorEncParams(C.Structure):
+    """thor_enc_params_t (include/thor_amd.h) = enc_params (enc/mainenc.h:34-88)."""
+    _fields_ = [(n, C.c_int32) for n in ("width", "height", "qp", "num_frames", "skip")] + \
+        [(n, C.c_float) for n in ("frame_rate", "lambda_coeffI", "lambda_coeffP", "lambda_coeffB", "lambda_coeffB0",
+                                  "lambda_coeffB1", "lambda_coeffB2", "lambda_coeffB3", "early_skip_thr")] + \
+        [(n, C.c_int32) for n in ("enable_tb_split", "enable_pb_split", "max_num_ref", "HQperiod", "num_reorder_pics",
+                                  "dyadic_coding", "interp_ref", "dqpP", "dqpB", "dqpB0", "dqpB1", "dqpB2", "dqpB3")] + \
+        [(n, C.c_float) for n in ("mqpP", "mqpB", "mqpB0", "mqpB1", "mqpB2", "mqpB3")] + \
+        [(n, C.c_int32) for n in ("dqpI", "intra_period", "intra_rdo", "rdoq", "max_delta_qp", "delta_qp_step",
+                                  "encoder_speed", "sync", "deblocking", "clpf", "snrcalc", "use_block_contexts",
+                                  "enable_bipred")]
+
+
 class ThorFrameIn(C.Structure):
     _fields_ = [("blocks", C.c_void_p), ("nblocks", C.c_int32), ("coeffs", C.c_void_p), ("clpf_flags", C.c_void_p),
                 ("intra_list", C.c_void_p), ("n_intra", C.c_int32), ("tu_list", C.c_void_p), ("n_tu", C.c_int32),
@@ -33,6 +46,9 @@ BATCHED_SYMBOLS = [
     "thor_dec_frame_end", "thor_dec_set_band", "thor_dec_get_rows", "thor_dec_put_rows", "thor_build_intra_list", "thor_build_tu_list", "thor_build_clpf_list", "thor_dec_set_stop_stage",
     "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_stage_marks", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_enc_tu_batch", "thor_enc_cost_batch",
+    "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
+    "thor_enc_next_input", "thor_enc_stream", "thor_enc_frames", "thor_enc_frame", "thor_enc_frame_bytes",
+    "thor_enc_read_recon",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
 SIMD_SURFACE_SYMBOLS = [
@@ -101,6 +117,27 @@ def load(path: str = LIB_PATH):
     L.thor_enc_tu_batch.restype = i
     L.thor_enc_cost_batch.argtypes = [P, P, P, P, C.c_double, P, i, P]
     L.thor_enc_cost_batch.restype = i
+    EP = C.POINTER(ThorEncParams)
+    L.thor_enc_default_params.argtypes = [EP]
+    L.thor_enc_check_params.argtypes = [EP]
+    L.thor_enc_check_params.restype = i
+    L.thor_enc_create.argtypes = [EP, i]
+    L.thor_enc_create.restype = P
+    L.thor_enc_destroy.argtypes = [P]
+    L.thor_enc_num_frames.argtypes = [P]
+    L.thor_enc_num_frames.restype = i
+    L.thor_enc_next_input.argtypes = [P]
+    L.thor_enc_next_input.restype = i
+    L.thor_enc_stream.argtypes = [P]
+    L.thor_enc_stream.restype = P
+    L.thor_enc_frames.argtypes = [P, i, P, P]
+    L.thor_enc_frames.restype = i
+    L.thor_enc_frame.argtypes = [P, P, i]
+    L.thor_enc_frame.restype = i
+    L.thor_enc_frame_bytes.argtypes = [P, P, C.c_size_t]
+    L.thor_enc_frame_bytes.restype = C.c_longlong
+    L.thor_enc_read_recon.argtypes = [P, P, P, P]
+    L.thor_enc_read_recon.restype = i
     L.thor_pyramid_levels.argtypes = [i, i]
     L.thor_pyramid_levels.restype = i
     L.thor_scale_pyramid.argtypes = [P, i, i, i, P, P, i, P]
