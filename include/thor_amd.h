@@ -224,6 +224,30 @@ int thor_enc_tu_batch(const thor_enc_tu_t *tus, int n, const uint8_t *orig, cons
 int thor_enc_cost_batch(const uint32_t *ssd, const int32_t *tu_first, const int32_t *tu_count, const int32_t *nbits,
                         double lambda, uint32_t *cost, int ncu, void *stream);
 
+/* ---- the .bit parser (host) that feeds the batched decoder -------------- *
+ * Restates the reference's serial syntax layer (dec/getbits.c, dec/getvlc.c,
+ * dec/read_bits.c, decode_frame / process_block_dec): one frame payload (the
+ * bytes after a chunk's 4-byte length, dec/getbits.c:48-69) in, the frame's
+ * descriptors, compact coefficient pool and CLPF flags out -- thor_dec_frame's
+ * inputs (copy them to device memory).  The first payload carries the sequence
+ * header.  Output pointers stay valid until the next call. */
+typedef struct thor_parser thor_parser_t;
+typedef struct thor_parsed_frame {
+  thor_seq_t seq;
+  thor_frame_hdr_t hdr;
+  int32_t decode_order, num_ref;
+  const thor_block_t *blocks;
+  int32_t nblocks;
+  const int16_t *coeffs;
+  int32_t ncoeffs;
+  const uint8_t *clpf_flags; /* per full SB, raster (W/64 x H/64) */
+  int32_t nclpf;
+} thor_parsed_frame_t;
+thor_parser_t *thor_parser_create(void);
+void thor_parser_destroy(thor_parser_t *p);
+int thor_parser_seq(const thor_parser_t *p, thor_seq_t *seq);
+int thor_parse_frame(thor_parser_t *p, const uint8_t *payload, size_t nbytes, thor_parsed_frame_t *out);
+
 /* ---- device-resident encoder (the full RD loop) ---- *
  * Encoder parameters: enc_params (enc/mainenc.h:34-88), the flags of the
  * reference's configuration files / command line (enc/strings.c:286-338),

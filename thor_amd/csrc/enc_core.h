@@ -26,12 +26,14 @@
 #define TE_LANE 0
 #define TE_NL 1
 #define TE_CONST static const
+#define TE_HD static inline
 #else
 #define TE_FN __device__ __forceinline__
 #define TE_NOINL __device__ __noinline__
 #define TE_LANE ((int)threadIdx.x)
 #define TE_NL 64
 #define TE_CONST __constant__ static const
+#define TE_HD __host__ __device__ inline
 #endif
 
 // ---- wave helpers -----------------------------------------------------------
@@ -154,7 +156,7 @@ TE_CONST uint16_t te_iq8[52] = {6,   7,   8,   8,   10,  11,  12,  13,  15,  17,
 // zigzag scans (common/common_block.c:38-73; zigzag16 / 64 / 256 all follow
 // this rule): anti-diagonals, alternating direction; te_zz(q, raster) = scan
 // position.
-TE_FN int te_zz(int q, int r) {
+TE_HD int te_zz(int q, int r) {
   const int i = r / q, j = r - (r / q) * q, d = i + j;
   // positions before diagonal d
   int before;
@@ -248,9 +250,9 @@ TE_FN void te_write_mv(TeBits &b, TeMv mv, TeMv mvp) {
 }
 
 // ---- availability (common/common_block.c:100-129) ----------------------------
-TE_FN int te_up_avail(int ypos) { return ypos > 0; }
-TE_FN int te_left_avail(int xpos) { return xpos > 0; }
-TE_FN int te_upright_avail(int ypos, int xpos, int size, int width) {
+TE_HD int te_up_avail(int ypos) { return ypos > 0; }
+TE_HD int te_left_avail(int xpos) { return xpos > 0; }
+TE_HD int te_upright_avail(int ypos, int xpos, int size, int width) {
   int a = (ypos > 0) && (xpos + size < width);
   if (size == 32 && (ypos % 64) == 32) a = 0;
   if (size == 16 && ((ypos % 32) == 16 || ((ypos % 64) == 32 && (xpos % 32) == 16))) a = 0;
@@ -258,7 +260,7 @@ TE_FN int te_upright_avail(int ypos, int xpos, int size, int width) {
     a = 0;
   return a;
 }
-TE_FN int te_downleft_avail(int ypos, int xpos, int size, int height) {
+TE_HD int te_downleft_avail(int ypos, int xpos, int size, int height) {
   int a = (xpos > 0) && (ypos + size < height);
   if (size == 64) a = 0;
   if (size == 32 && (ypos % 64) == 32) a = 0;
@@ -268,7 +270,7 @@ TE_FN int te_downleft_avail(int ypos, int xpos, int size, int height) {
   return a;
 }
 
-TE_FN TeInterPred te_zero_pred() {
+TE_HD TeInterPred te_zero_pred() {
   TeInterPred z;
   z.mv0.x = z.mv0.y = z.mv1.x = z.mv1.y = 0;
   z.ref_idx0 = z.ref_idx1 = z.bipred_flag = 0;
@@ -277,7 +279,7 @@ TE_FN TeInterPred te_zero_pred() {
 
 // get_mv_pred, common/inter_prediction.c:182-294: median of three neighbours
 // chosen by the availability pattern.
-TE_FN TeMv te_mv_pred(int ypos, int xpos, int width, int height, int size, const TeCell *db) {
+TE_HD TeMv te_mv_pred(int ypos, int xpos, int width, int height, int size, const TeCell *db) {
   const int bsz = size / 4, bs = width / 4, bi = (ypos / 4) * bs + xpos / 4;
   const int up0 = bi - bs, up1 = bi - bs + (bsz - 1) / 2, up2 = bi - bs + bsz - 1;
   const int l0 = bi - 1, l1 = bi + bs * ((bsz - 1) / 2) - 1, l2 = bi + bs * (bsz - 1) - 1;
@@ -313,7 +315,7 @@ TE_FN TeMv te_mv_pred(int ypos, int xpos, int width, int height, int size, const
   return p;
 }
 
-TE_FN int te_pred_equal(const TeInterPred &t, const TeInterPred &c) {
+TE_HD int te_pred_equal(const TeInterPred &t, const TeInterPred &c) {
   // duplicate test of get_mv_skip / get_mv_merge (inter_prediction.c:434-438, :587-591)
   return t.mv0.x == c.mv0.x && t.mv0.y == c.mv0.y && t.ref_idx0 == c.ref_idx0 && t.mv1.x == c.mv1.x &&
          t.mv1.y == c.mv1.y && t.ref_idx1 == c.ref_idx1 && (t.bipred_flag == c.bipred_flag || t.bipred_flag == -1);
@@ -324,7 +326,7 @@ TE_FN int te_pred_equal(const TeInterPred &t, const TeInterPred &c) {
 // up-right (else up, right-most) neighbours, duplicates removed.  The merge
 // list is the same derivation (both functions are identical under
 // LIMITED_SKIP; bipred_copy is unused there).
-TE_FN int te_mv_skip(int ypos, int xpos, int width, int height, int size, const TeCell *db, TeInterPred *out) {
+TE_HD int te_mv_skip(int ypos, int xpos, int width, int height, int size, const TeCell *db, TeInterPred *out) {
   const int bsz = size / 4, bs = width / 4, bi = (ypos / 4) * bs + xpos / 4;
   int up0 = bi - bs, up2 = bi - bs + bsz - 1, l0 = bi - 1, l2 = bi + bs * (bsz - 1) - 1, ur = bi - bs + bsz;
   const int U = te_up_avail(ypos), L = te_left_avail(xpos), UR = te_upright_avail(ypos, xpos, size, width);
@@ -339,7 +341,7 @@ TE_FN int te_mv_skip(int ypos, int xpos, int width, int height, int size, const 
 }
 
 // find_block_contexts, common/common_block.c:158-178
-TE_FN TeCtx te_block_ctx(int ypos, int xpos, int height, int width, int size, const TeCell *db, int enable) {
+TE_HD TeCtx te_block_ctx(int ypos, int xpos, int height, int width, int size, const TeCell *db, int enable) {
   TeCtx c;
   if (ypos >= 8 && xpos >= 8 && ypos + size < height && xpos + size < width && enable && size <= 64) {
     const int bs = width / 4, bi = (ypos / 4) * bs + xpos / 4;

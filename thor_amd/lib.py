@@ -40,6 +40,13 @@ class ThorFrameIn(C.Structure):
                 ("clpf_list", C.c_void_p), ("n_clpf", C.c_int32)]
 
 
+class ThorParsedFrame(C.Structure):
+    """thor_parsed_frame_t (include/thor_amd.h)."""
+    _fields_ = [("seq", ThorSeq), ("hdr", ThorFrameHdr), ("decode_order", C.c_int32), ("num_ref", C.c_int32),
+                ("blocks", C.c_void_p), ("nblocks", C.c_int32), ("coeffs", C.c_void_p), ("ncoeffs", C.c_int32),
+                ("clpf_flags", C.c_void_p), ("nclpf", C.c_int32)]
+
+
 # Every symbol the public headers declare (checked by tests/test_capi.py).
 BATCHED_SYMBOLS = [
     "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_dec_frames", "thor_dec_frame_begin",
@@ -49,6 +56,7 @@ BATCHED_SYMBOLS = [
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_frames", "thor_enc_frame", "thor_enc_frame_bytes",
     "thor_enc_read_recon",
+    "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
 SIMD_SURFACE_SYMBOLS = [
@@ -138,6 +146,12 @@ def load(path: str = LIB_PATH):
     L.thor_enc_frame_bytes.restype = C.c_longlong
     L.thor_enc_read_recon.argtypes = [P, P, P, P]
     L.thor_enc_read_recon.restype = i
+    L.thor_parser_create.restype = P
+    L.thor_parser_destroy.argtypes = [P]
+    L.thor_parser_seq.argtypes = [P, C.POINTER(ThorSeq)]
+    L.thor_parser_seq.restype = i
+    L.thor_parse_frame.argtypes = [P, P, C.c_size_t, C.POINTER(ThorParsedFrame)]
+    L.thor_parse_frame.restype = i
     L.thor_pyramid_levels.argtypes = [i, i]
     L.thor_pyramid_levels.restype = i
     L.thor_scale_pyramid.argtypes = [P, i, i, i, P, P, i, P]
