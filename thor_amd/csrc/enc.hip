@@ -51,8 +51,12 @@ __device__ __forceinline__ unsigned te_ld_acquire(const unsigned *p) {
 // WPP worker: grid of persistent single-wave workgroups; ticket t -> stream
 // t % n, SB row t / n.
 __global__ __launch_bounds__(64) void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
-                                                 TeScratch *scratch, TeSB *sbs, unsigned *err) {
-  TeScratch &S = scratch[blockIdx.x];
+                                                 TeScratchMem *scratch, TeSB *sbs, unsigned *err) {
+  __shared__ TeTx s_tx;
+  __shared__ TeNbr s_nb;
+  __shared__ uint8_t s_pb[TE_BLK];
+  const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb);
+  te_load_basis(s_tx);
   TeSB &sb = sbs[blockIdx.x];
   const int lane = threadIdx.x;
   for (;;) {
@@ -66,11 +70,13 @@ __global__ __launch_bounds__(64) void k_enc_rows(const TeJob *__restrict__ jobs,
     for (int l = 0; l < J.nsbh; l++) {
       if (k > 0) {  // SB (k-1, l+1) (or the whole row above) must be done
         const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
+        TE_P(TP_WAIT);
         if (lane == 0) {
-          long long spins = 0;
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
           while (te_ld_acquire(&J.progress[k - 1]) < need) {
-            __builtin_amdgcn_s_sleep(4);
-            if (++spins > (1LL << 26)) {  // a wedged dependency: give up (reported), never hang the GPU
+            __builtin_amdgcn_s_sleep(8);
+            // a wedged dependency (5 minutes): give up, reported; never hang the GPU
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 30000000000ULL) {
               atomicOr(err, 1u);
               break;
             }
@@ -263,7 +269,7 @@ static int enc_alloc(thor_enc *e) {
 struct EncPool {
   int device = -1;
   size_t nwork = 0;
-  TeScratch *scratch = nullptr;
+  TeScratchMem *scratch = nullptr;
   TeSB *sbs = nullptr;
   unsigned *ticket = nullptr, *err = nullptr;
   TeJob *jobs = nullptr;
@@ -284,7 +290,7 @@ static int pool_reserve(int device, size_t nwork, size_t scan_n) {
   if (nwork > g_pool.nwork) {
     if (g_pool.scratch) (void)hipFree(g_pool.scratch);
     if (g_pool.sbs) (void)hipFree(g_pool.sbs);
-    EHIP(hipMalloc(&g_pool.scratch, nwork * sizeof(TeScratch)));
+    EHIP(hipMalloc(&g_pool.scratch, nwork * sizeof(TeScratchMem)));
     EHIP(hipMalloc(&g_pool.sbs, nwork * sizeof(TeSB)));
     EHIP(hipMemset(g_pool.sbs, 0, nwork * sizeof(TeSB)));
     g_pool.nwork = nwork;
@@ -578,3 +584,9 @@ int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v) {
 }
 
 }  // extern "C"
+
+#if defined(THOR_ENC_PROFILE)
+extern "C" int thor_enc_profile_buffer(void *dev_buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(te_prof_buf), &dev_buf, sizeof(void *)) == hipSuccess ? THOR_OK : THOR_ERR_HIP;
+}
+#endif

@@ -27,6 +27,7 @@
 #define TE_NL 1
 #define TE_CONST static const
 #define TE_HD static inline
+#define TE_MFN inline
 #else
 #define TE_FN __device__ __forceinline__
 #define TE_NOINL __device__ __noinline__
@@ -34,15 +35,20 @@
 #define TE_NL 64
 #define TE_CONST __constant__ static const
 #define TE_HD __host__ __device__ inline
+#define TE_MFN __device__ __forceinline__
 #endif
 
 // ---- wave helpers -----------------------------------------------------------
 // te_sync: every lane's earlier global / LDS writes are visible to every lane
-// of the wave afterwards (one wave = one workgroup: the workgroup barrier +
-// fences).
+// of the wave afterwards.  One wave per worker: the memory operations of a
+// wavefront are performed in order, so a wavefront-scope fence (no
+// instruction, it only stops the compiler from moving memory operations
+// across it) plus a wave barrier is all that is needed -- no s_waitcnt drain.
 TE_FN void te_sync() {
 #if !defined(TE_HOST)
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #endif
 }
 TE_FN uint32_t te_sum(uint32_t v) {
@@ -67,6 +73,39 @@ TE_FN int te_any(int v) {
   return v != 0;
 #endif
 }
+
+// e / w for the lane-strided 2-D loops: a shift for the (usual) power-of-two
+// widths, a division otherwise (rectangular edge blocks)
+TE_FN int te_dv(int e, int w) {
+#if !defined(TE_HOST)
+  return (w & (w - 1)) == 0 ? e >> __builtin_ctz(w) : e / w;
+#else
+  return e / w;
+#endif
+}
+
+// Optional per-function cycle accounting (built only with -DTHOR_ENC_PROFILE,
+// tools/enc_profile.py): s_memtime deltas and call counts per category.
+#if defined(THOR_ENC_PROFILE) && !defined(TE_HOST)
+__device__ unsigned long long *te_prof_buf;
+struct TeProf {
+  int c;
+  unsigned long long t;
+  __device__ __forceinline__ TeProf(int c_) : c(c_), t(__builtin_amdgcn_s_memtime()) {}
+  __device__ __forceinline__ ~TeProf() {
+    if (threadIdx.x == 0 && te_prof_buf) {
+      atomicAdd(&te_prof_buf[2 * c], __builtin_amdgcn_s_memtime() - t);
+      atomicAdd(&te_prof_buf[2 * c + 1], 1ULL);
+    }
+  }
+};
+#define TE_P(c) TeProf te_prof_scope_(c)
+#else
+#define TE_P(c)
+#endif
+enum { TP_WCOEF, TP_WBLOCK, TP_INTER_COMP, TP_INTRA_COMP, TP_ENC_BLOCK, TP_COST, TP_SEARCH_INTRA, TP_ME, TP_MODE,
+       TP_ES_CHECK, TP_ES_SEARCH, TP_COMMIT, TP_MC_Y, TP_MC_C, TP_FWD, TP_QUANT, TP_INV, TP_IPRED, TP_TOPLEFT, TP_SAD,
+       TP_SB, TP_WAIT, TP_N };
 
 #define TE_MIN(a, b) ((a) < (b) ? (a) : (b))
 #define TE_MAX(a, b) ((a) > (b) ? (a) : (b))
@@ -154,49 +193,87 @@ TE_CONST uint16_t te_iq8[52] = {6,   7,   8,   8,   10,  11,  12,  13,  15,  17,
                                 768, 862, 968, 1086, 1219, 1368, 1536, 1724, 1935, 2172};
 
 // zigzag scans (common/common_block.c:38-73; zigzag16 / 64 / 256 all follow
-// this rule): anti-diagonals, alternating direction; te_zz(q, raster) = scan
-// position.
-TE_HD int te_zz(int q, int r) {
-  const int i = r / q, j = r - (r / q) * q, d = i + j;
-  // positions before diagonal d
-  int before;
-  if (d < q) before = d * (d + 1) / 2;
-  else {
-    const int e = 2 * q - 1 - d;  // diagonals after (and including) d have e, e-1, ... elements
-    before = q * q - e * (e + 1) / 2;
+// this rule): anti-diagonals, alternating direction.  te_zz(q, raster) = scan
+// position, te_izz(q, pos) = raster index, from tables built at compile time.
+struct TeZigzag {
+  uint8_t zz[3][256], iz[3][256];  // q = 4, 8, 16
+  constexpr TeZigzag() : zz(), iz() {
+    for (int t = 0; t < 3; t++) {
+      const int q = 4 << t;
+      for (int r = 0; r < q * q; r++) {
+        const int i = r / q, j = r % q, d = i + j;
+        int before = 0;
+        if (d < q) before = d * (d + 1) / 2;
+        else {
+          const int e = 2 * q - 1 - d;
+          before = q * q - e * (e + 1) / 2;
+        }
+        const int lo = d < q ? 0 : d - q + 1, hi = d < q ? d : q - 1;
+        const int z = (d & 1) ? before + (i - lo) : before + (hi - i);
+        zz[t][r] = (uint8_t)z;
+        iz[t][z] = (uint8_t)r;
+      }
+    }
   }
-  const int lo = d < q ? 0 : d - q + 1;  // smallest row index on diagonal d
-  const int hi = d < q ? d : q - 1;
-  // even d: bottom-left to top-right (rows descending), odd d: rows ascending
-  return (d & 1) ? before + (i - lo) : before + (hi - i);
+};
+TE_CONST TeZigzag te_zig = TeZigzag();
+#if defined(TE_HOST)
+static const TeZigzag &te_zig_h = te_zig;
+#else
+static const TeZigzag te_zig_h = TeZigzag();  // host copy (the parser)
+#endif
+TE_HD int te_zz(int q, int r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return te_zig.zz[q == 4 ? 0 : (q == 8 ? 1 : 2)][r];
+#else
+  return te_zig_h.zz[q == 4 ? 0 : (q == 8 ? 1 : 2)][r];
+#endif
 }
+TE_FN int te_izz(int q, int pos) { return te_zig.iz[q == 4 ? 0 : (q == 8 ? 1 : 2)][pos]; }
 
 // ---- bit writer (enc/putbits.c:112-146) -------------------------------------
-// One stream per superblock: MSB-first bits into 32-bit words.  Rewinding
-// (write_stream_pos) sets the position back; later writes overwrite.  Only
-// lane 0 touches the words; every lane tracks the position.
+// One stream per superblock: MSB-first bits into 32-bit words.  The word being
+// filled lives in a register (`cur`, zeros past `pos`); a completed word is
+// stored once (lane 0).  Rewinding (write_stream_pos) restores the partial
+// word at the old position; later writes overwrite what followed.
 struct TeBits {
   uint32_t *w;
   int pos, cap;  // bits
+  uint32_t cur;
 };
+TE_FN void te_bits_start(TeBits &b) {
+  b.pos = 0;
+  b.cur = 0;
+}
 TE_FN void te_put(TeBits &b, int n, uint32_t val) {
   if (n <= 0) return;
   if (n < 32) val &= (1u << n) - 1;
-  if (TE_LANE == 0 && b.pos + n <= b.cap) {
-    const int wi = b.pos >> 5, off = b.pos & 31;  // bit `off` from the MSB of word wi
-    const int r0 = 32 - off;                        // room in word wi
-    if (n <= r0) {
-      const uint32_t m = (n == 32 ? 0xffffffffu : ((1u << n) - 1)) << (r0 - n);
-      b.w[wi] = (b.w[wi] & ~m) | (val << (r0 - n));
-    } else {
-      const int n1 = n - r0;  // bits spilling into word wi + 1
-      const uint32_t m0 = r0 == 32 ? 0xffffffffu : ((1u << r0) - 1);
-      b.w[wi] = (b.w[wi] & ~m0) | (val >> n1);
-      const uint32_t m1 = ((1u << n1) - 1) << (32 - n1);
-      b.w[wi + 1] = (b.w[wi + 1] & ~m1) | ((val & ((1u << n1) - 1)) << (32 - n1));
-    }
+  const int room = 32 - (b.pos & 31);
+  if (n < room) {
+    b.cur |= val << (room - n);
+  } else {
+    const int n1 = n - room;  // bits that spill into the next word
+    const uint32_t full = b.cur | (n1 ? val >> n1 : val);
+    if (TE_LANE == 0 && b.pos + room <= b.cap) b.w[b.pos >> 5] = full;
+    b.cur = n1 ? (val & ((1u << n1) - 1)) << (32 - n1) : 0u;
   }
   b.pos += n;
+}
+TE_FN void te_rewind(TeBits &b, int p) {
+  const int off = p & 31;
+  const uint32_t keep = off ? ~(0xffffffffu >> off) : 0u;
+  if ((p >> 5) != (b.pos >> 5)) {
+    // the word at p was completed and stored: reload it (lane 0 wrote it, and
+    // a wave's memory operations are performed in order)
+    b.cur = off ? (b.w[p >> 5] & keep) : 0u;
+  } else {
+    b.cur &= keep;
+  }
+  b.pos = p;
+}
+// store the partial last word (end of a superblock)
+TE_FN void te_bits_flush(TeBits &b) {
+  if ((b.pos & 31) && TE_LANE == 0 && b.pos <= b.cap) b.w[b.pos >> 5] = b.cur;
 }
 
 // quote_vlc / put_vlc, enc/putvlc.c:34-229 (tables 0-5, 10, 11; the others
@@ -426,21 +503,74 @@ TE_FN int te_find_code(int run, int level, int maxrun, int chroma, int eob) {
 }
 
 // write_coeff, write_bits.c:110-253: run-level VLC of one transform block's
-// q x q tile `c` (raster) of an N x N block.  Serial (lane-uniform).
-TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, int16_t *scan /* 256 scratch */) {
+// q x q tile `c` (raster) of an N x N block.  The scan-order levels sit in
+// registers (device: lane l holds positions l, l+64, l+128, l+192, read back
+// with readlane) with a non-zero bitmap, so the serial coder steps only over
+// coded events: runs of zeros are skipped with bit scans.
+struct TeScanRegs {
+#if defined(TE_HOST)
+  int v[256];
+  uint64_t nz[4];
+  TE_MFN int at(int pos) const { return v[pos]; }
+#else
+  int v0, v1, v2, v3;
+  uint64_t nz[4];
+  __device__ __forceinline__ int at(int pos) const {
+    const int k = pos >> 6;
+    const int r = k == 0 ? v0 : (k == 1 ? v1 : (k == 2 ? v2 : v3));
+    return __builtin_amdgcn_readlane(r, pos & 63);
+  }
+#endif
+  // first non-zero position >= pos (pos < 256), or 256
+  TE_MFN int next_nz(int pos) const {
+    for (int k = pos >> 6; k < 4; k++) {
+      const uint64_t m = nz[k] & (k == (pos >> 6) ? (~0ULL << (pos & 63)) : ~0ULL);
+      if (m) return k * 64 + __builtin_ctzll(m);
+    }
+    return 256;
+  }
+  TE_MFN int last_nz() const {
+    for (int k = 3; k >= 0; k--)
+      if (nz[k]) return k * 64 + 63 - __builtin_clzll(nz[k]);
+    return -1;
+  }
+};
+TE_FN void te_load_scan(TeScanRegs &R, const int16_t *c, int q) {
+  const int N = q * q;
+#if defined(TE_HOST)
+  for (int k = 0; k < 4; k++) R.nz[k] = 0;
+  for (int pos = 0; pos < 256; pos++) {
+    R.v[pos] = pos < N ? c[te_izz(q, pos)] : 0;
+    if (R.v[pos]) R.nz[pos >> 6] |= 1ULL << (pos & 63);
+  }
+#else
+  const int l = TE_LANE;
+  R.v0 = l < N ? c[te_izz(q, l)] : 0;
+  R.v1 = l + 64 < N ? c[te_izz(q, l + 64)] : 0;
+  R.v2 = l + 128 < N ? c[te_izz(q, l + 128)] : 0;
+  R.v3 = l + 192 < N ? c[te_izz(q, l + 192)] : 0;
+  R.nz[0] = __ballot(R.v0 != 0);
+  R.nz[1] = __ballot(R.v1 != 0);
+  R.nz[2] = __ballot(R.v2 != 0);
+  R.nz[3] = __ballot(R.v3 != 0);
+#endif
+}
+TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, int16_t *scan /* unused */) {
+  TE_P(TP_WCOEF);
+  (void)scan;
   const int q = TE_MIN(16, size), N = q * q;
   const int chroma = type & 1, intra = (type >> 1) & 1;
   int vlc_adaptive = intra && !chroma;
-  for (int r = TE_LANE; r < N; r += TE_NL) scan[te_zz(q, r)] = c[r];
-  te_sync();
-  int pos = N - 1;
-  while (scan[pos] == 0 && pos > 0) pos--;
-  const int last_pos = pos;  // cbp != 0 guarantees a non-zero level (fatalerror otherwise, :142-143)
-  pos = 0;
+  TeScanRegs R;
+  te_load_scan(R, c, q);
+  int last_pos = R.last_nz();
+  if (last_pos < 0) last_pos = 0;  // cbp != 0 guarantees a non-zero level (fatalerror otherwise, :142-143)
+  int pos = 0;
   if (chroma) {
-    if (last_pos == 0 && te_abs(scan[0]) == 1) {
+    const int s0 = R.at(0);
+    if (last_pos == 0 && te_abs(s0) == 1) {
       te_put(b, 1, 1);
-      te_put(b, 1, scan[0] < 0 ? 1 : 0);
+      te_put(b, 1, s0 < 0 ? 1 : 0);
       pos = N;
     } else {
       te_put(b, 1, 0);
@@ -450,7 +580,7 @@ TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, in
   while (pos <= last_pos) {
     if (level_mode) {
       while (pos <= last_pos && level > 0) {
-        const int cc = scan[pos];
+        const int cc = R.at(pos);
         level = te_abs(cc);
         te_put_vlc(b, vlc_adaptive, level);
         if (level > 0) te_put(b, 1, cc < 0 ? 1 : 0);
@@ -458,36 +588,29 @@ TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, in
         pos++;
       }
     }
-    const int maxrun = N - pos - 1;
-    int run = 0, cc = 0;
-    while (cc == 0 && pos <= last_pos) {
-      cc = scan[pos];
-      if (cc == 0) {
-        run++;
+    if (pos <= last_pos) {  // run mode: the next non-zero lies at or before last_pos
+      const int maxrun = N - pos - 1;
+      const int np = R.next_nz(pos);
+      const int run = np - pos;
+      const int cc = R.at(np);
+      level = te_abs(cc);
+      const int sign = cc < 0 ? 1 : 0;
+      const int cn = te_find_code(run, level, maxrun, chroma, 0);
+      if (chroma && size <= 8) {
+        te_put_vlc(b, 10, cn);
       } else {
-        level = te_abs(cc);
-        const int sign = cc < 0 ? 1 : 0;
-        const int cn = te_find_code(run, level, maxrun, chroma, 0);
-        if (chroma && size <= 8) {
-          te_put_vlc(b, 10, cn);
-        } else {
-          if (cn == 0) te_put(b, 2, 2);
-          else te_put_vlc(b, 2, cn + 1);
-        }
-        if (level > 1) te_put_vlc(b, 0, 2 * (level - 2) + sign);
-        else te_put(b, 1, sign);
-        run = 0;
+        if (cn == 0) te_put(b, 2, 2);
+        else te_put_vlc(b, 2, cn + 1);
       }
-      pos++;
+      if (level > 1) te_put_vlc(b, 0, 2 * (level - 2) + sign);
+      else te_put(b, 1, sign);
+      pos = np + 1;
       level_mode = level > 1;
     }
   }
   if (pos < N) {
     if (level_mode) {  // terminated in level mode: one extra zero before EOB (:223-236)
-      const int cc = scan[pos];
-      level = te_abs(cc);
-      te_put_vlc(b, vlc_adaptive, level);
-      if (level > 0) te_put(b, 1, cc < 0 ? 1 : 0);
+      te_put_vlc(b, vlc_adaptive, 0);
       pos++;
     }
   }
@@ -500,7 +623,6 @@ TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, in
       else te_put_vlc(b, 2, cn + 1);
     }
   }
-  te_sync();  // `scan` is reused by the next call
 }
 
 // write_delta_qp, write_bits.c:255-265
@@ -564,6 +686,7 @@ TE_FN const int16_t *te_tile(const TeParam &p, int comp, int idx) { return p.coe
 
 // write_block, write_bits.c:364-650.  Returns the number of bits written.
 TE_NOINL int te_write_block(TeBits &b, const TeFrame &F, const TeBlockInfo &bi, const TeParam &p, int16_t *scan) {
+  TE_P(TP_WBLOCK);
   const int start = b.pos;
   const int size = bi.size, mode = p.mode, tb_split = p.tb_split;
   const int coeff_type = (mode == TE_INTRA) << 1;

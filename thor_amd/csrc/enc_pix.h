@@ -39,18 +39,19 @@ TE_CONST int8_t te_chroma_f[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54
 // dispatch, common/common_kernels.c:165-784, computes the same values):
 // `ref` points at the block's co-located position in the padded reference.
 TE_FN void te_mc_luma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, int h, TeMv mv, int sign, int bipred) {
+  TE_P(TP_MC_Y);
   const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
   const int fy = my & 3, fx = mx & 3;
   const uint8_t *r = ref + (my >> 2) * rs + (mx >> 2);
   const int n = w * h;
   if (!fx && !fy) {
     for (int e = TE_LANE; e < n; e += TE_NL) {
-      const int i = e / w, j = e - (e / w) * w;
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
       dst[i * ds + j] = r[i * rs + j];
     }
   } else if (fx == 2 && fy == 2) {  // (2,2): 4x4 low-pass centre, :145-157
     for (int e = TE_LANE; e < n; e += TE_NL) {
-      const int i = e / w, j = e - (e / w) * w;
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
       const uint8_t *p = r + i * rs + j;
       int s = p[-rs] + p[-rs + 1] + p[-1] + 2 * p[0] + 2 * p[1] + p[2] + p[rs - 1] + 2 * p[rs] + 2 * p[rs + 1] + p[rs + 2] +
               p[2 * rs] + p[2 * rs + 1];
@@ -60,7 +61,7 @@ TE_FN void te_mc_luma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, i
     const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
     const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
     for (int e = TE_LANE; e < n; e += TE_NL) {
-      const int i = e / w, j = e - (e / w) * w;
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
       const uint8_t *p = r + (i - 2) * rs + j - 2;
       int s = 0;
       for (int m = 0; m < 6; m++) {
@@ -77,19 +78,20 @@ TE_FN void te_mc_luma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, i
 // get_inter_prediction_chroma, common/inter_prediction.c:72-118: the luma MV
 // read as 1/8-pel on the chroma plane.
 TE_FN void te_mc_chroma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, int h, TeMv mv, int sign) {
+  TE_P(TP_MC_C);
   const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
   const int fy = my & 7, fx = mx & 7;
   const uint8_t *r = ref + (my >> 3) * rs + (mx >> 3);
   const int n = w * h;
   if (!fx && !fy) {
     for (int e = TE_LANE; e < n; e += TE_NL) {
-      const int i = e / w, j = e - (e / w) * w;
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
       dst[i * ds + j] = r[i * rs + j];
     }
   } else {
     const int8_t *fh = te_chroma_f[fx], *fv = te_chroma_f[fy];
     for (int e = TE_LANE; e < n; e += TE_NL) {
-      const int i = e / w, j = e - (e / w) * w;
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
       const uint8_t *p = r + (i - 1) * rs + j - 1;
       int s = 0;
       for (int m = 0; m < 4; m++) {
@@ -105,9 +107,10 @@ TE_FN void te_mc_chroma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w,
 
 // sad_calc (enc/encode_block.c:740-755) / ssd_calc (:782-797): exact sums
 TE_FN uint32_t te_sad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
+  TE_P(TP_SAD);
   uint32_t s = 0;
   for (int e = TE_LANE; e < w * h; e += TE_NL) {
-    const int i = e / w, j = e - (e / w) * w;
+    const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
     s += (uint32_t)te_abs((int)a[i * as + j] - (int)b[i * bs + j]);
   }
   return te_sum(s);
@@ -115,7 +118,7 @@ TE_FN uint32_t te_sad(const uint8_t *a, int as, const uint8_t *b, int bs, int w,
 TE_FN uint32_t te_ssd(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
   uint32_t s = 0;
   for (int e = TE_LANE; e < w * h; e += TE_NL) {
-    const int i = e / w, j = e - (e / w) * w;
+    const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
     const int d = (int)a[i * as + j] - (int)b[i * bs + j];
     s += (uint32_t)(d * d);
   }
@@ -129,7 +132,7 @@ TE_FN uint32_t te_widesad(const uint8_t *a, int as, const uint8_t *b, int bs, in
   const int off[5] = {-3, -1, 0, 1, 3};
   uint32_t s[5] = {0, 0, 0, 0, 0};
   for (int e = TE_LANE; e < w * h; e += TE_NL) {
-    const int i = e / w, j = e - (e / w) * w;
+    const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
     const int av = a[i * as + j];
     for (int k = 0; k < 5; k++) s[k] += (uint32_t)te_abs(av - (int)b[i * bs + j + off[k]]);
   }
@@ -151,7 +154,7 @@ TE_FN uint32_t te_widesad(const uint8_t *a, int as, const uint8_t *b, int bs, in
 TE_FN uint32_t te_fasthalf(const uint8_t *a, int as, const uint8_t *b, int bs, int width, int height, int *x, int *y) {
   uint32_t tl = 0, tr = 0, br = 0, bl = 0, top = 0, right = 0, down = 0, left = 0;
   for (int e = TE_LANE; e < width * height; e += TE_NL) {
-    const int i = e / width, j = e - (e / width) * width;
+    const int i = te_dv(e, width), j = e - te_dv(e, width) * width;
     const uint8_t *q = b + i * bs;
     const int A = a[i * as + j];
     int t1, t2, t3, t4, t5, t6, t7, t8, ptl, ptr, pbr, pbl;
@@ -228,7 +231,7 @@ TE_FN uint32_t te_fastquarter(const uint8_t *o, int os, const uint8_t *r, int rs
   uint32_t tl = 0, tr = 0, br = 0, bl = 0, top = 0, right = 0, down = 0, left = 0;
   const int X = *x, Y = *y;
   for (int e = TE_LANE; e < width * height; e += TE_NL) {
-    const int i = e / width, j = e - (e / width) * width;
+    const int i = te_dv(e, width), j = e - te_dv(e, width) * width;
     const uint8_t *q = r + i * rs;
     const int O = o[i * os + j];
     if (X & Y) {
@@ -306,6 +309,7 @@ struct TeNbr {
 };
 TE_FN void te_make_top_and_left(TeNbr &nb, const uint8_t *rf, int fs, const uint8_t *rb, int rbs, int i, int j, int ypos,
                                 int xpos, int size, int cb_ur, int cb_dl, int tb_split) {
+  TE_P(TP_TOPLEFT);
   int dl, ur;
   if (!tb_split) {
     dl = cb_dl;
@@ -357,6 +361,7 @@ TE_FN void te_f121(const uint8_t *in, uint8_t *out, int len) {
 // compact n x n block.  search_dc: search_intra_prediction_params' DC
 // (enc/encode_block.c:1250, always (left, top)) instead of the position-aware one.
 TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int mode, int search_dc) {
+  TE_P(TP_IPRED);
   const int nn = n * n;
   switch (mode) {
     case TE_PLANAR: {  // :182-214, C division truncating toward zero
@@ -374,16 +379,16 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       te_sync();
       const int TL = nb.left[1] + 2 * nb.left[0] + 2 * nb.tl + 2 * nb.top[0] + nb.top[1];
       for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = e / n, j = e - (e / n) * n;
+        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
         pb[e] = (uint8_t)te_clip255((nb.L[i] + nb.T[j] - TL + 4) / 8);
       }
       break;
     }
     case TE_HOR:
-      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.left[e / n];
+      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.left[te_dv(e, n)];
       break;
     case TE_VER:
-      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.top[e - (e / n) * n];
+      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.top[e - te_dv(e, n) * n];
       break;
     case TE_UPLEFT:
     case TE_UPUPLEFT:
@@ -393,7 +398,7 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       const int tlF = (2 * nb.tl + nb.left[0] + nb.top[0] + 2) >> 2;
       te_sync();
       for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = e / n, j = e - (e / n) * n;
+        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
         int v;
         if (mode == TE_UPLEFT) {  // :216-240
           const int d = i - j;
@@ -422,7 +427,7 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       te_f121(nb.top, nb.tF, 2 * n);
       te_sync();
       for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = e / n, j = e - (e / n) * n;
+        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
         if (mode == TE_UPRIGHT) {  // :242-256
           pb[e] = nb.tF[i + j + 1];
         } else {  // :258-277
@@ -436,7 +441,7 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       te_f121(nb.left, nb.lF, 2 * n);
       te_sync();
       for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = e / n, j = e - (e / n) * n;
+        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
         const int d = 2 * i + j;
         pb[e] = (d & 1) ? nb.lF[(d + 1) / 2] : (uint8_t)((nb.lF[d / 2] + nb.lF[d / 2 + 1]) >> 1);
       }
@@ -462,11 +467,18 @@ struct TeTx {
   int16_t R[64 * 64];  // residual (N x N), reconstructed residual
   int16_t A[32 * 32];  // pre-summed input of the 32 / 64 paths
   int16_t T[32 * 32];  // pass-1 output
-  int C[256];          // q x q coefficients / levels (raster)
-  int S[256];          // levels in scan order
-  int O[256];          // coefficients in scan order (RDOQ light)
+  int16_t C[256];      // q x q coefficients / levels (raster; every value fits 16 bits)
+  int16_t S[256];      // levels in scan order
+  int16_t O[256];      // coefficients in scan order (RDOQ light)
   int16_t scan[256];   // write_coeff scratch
+  int8_t M[32 * 32];   // 32-point DCT basis (te_dct), loaded once per worker
 };
+TE_FN void te_load_basis(TeTx &X) {
+  for (int e = TE_LANE; e < 1024; e += TE_NL) X.M[e] = te_dct.m[e >> 5][e & 31];
+  te_sync();
+}
+// row k of the N-point basis = row k * 32 / N of the 32-point one
+#define TE_DCT(X, N, k, n) ((int)(X).M[((k) * (32 / (N))) * 32 + (n)])
 
 // One output of the reference SIMD 8-point forward pass (transform8,
 // common/common_kernels.c:1887-1967): 16-bit wrapping butterflies.
@@ -494,6 +506,7 @@ TE_FN int te_fwd8(const int16_t *s, int k, int shift) {
 // transform, common/transform.c:249-330 (SIMD transform_simd for the 8x8
 // butterfly wrap): X.R (size x size, stride size) -> X.C (q x q raster).
 TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
+  TE_P(TP_FWD);
   const int lg = te_log2(size);
   int N = size, sh1 = lg, sh2 = lg + 5;
   const int16_t *in = X.R;
@@ -505,7 +518,7 @@ TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
     te_sync();
     for (int e = TE_LANE; e < 64; e += TE_NL) {
       const int row = e >> 3, k = e & 7;
-      X.C[k * 8 + row] = te_fwd8(&X.T[row * 8], k, sh2);
+      X.C[k * 8 + row] = (int16_t)te_fwd8(&X.T[row * 8], k, sh2);
     }
     te_sync();
     return;
@@ -538,19 +551,19 @@ TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
   const int q = TE_MIN(size, 16);
   const int add1 = 1 << (sh1 - 1), add2 = 1 << (sh2 - 1);
   for (int e = TE_LANE; e < q * N; e += TE_NL) {  // :309-316, int16 store
-    const int i = e / N, j = e - (e / N) * N;
+    const int i = te_dv(e, N), j = e - te_dv(e, N) * N;
     const int16_t *x = &in[j * N];
     int s = 0;
-    for (int k = 0; k < N; k++) s += te_dctN(N, i, k) * (int)x[k];
+    for (int k = 0; k < N; k++) s += TE_DCT(X, N, i, k) * (int)x[k];
     X.T[i * N + j] = (int16_t)te_wrap16((s + add1) >> sh1);
   }
   te_sync();
   for (int e = TE_LANE; e < q * q; e += TE_NL) {  // :319-327
-    const int i = e / q, j = e - (e / q) * q;
+    const int i = te_dv(e, q), j = e - te_dv(e, q) * q;
     const int16_t *t = &X.T[j * N];
     int s = 0;
-    for (int k = 0; k < N; k++) s += te_dctN(N, i, k) * (int)t[k];
-    X.C[i * q + j] = te_wrap16((s + add2) >> sh2);
+    for (int k = 0; k < N; k++) s += TE_DCT(X, N, i, k) * (int)t[k];
+    X.C[i * q + j] = (int16_t)te_wrap16((s + add2) >> sh2);
   }
   te_sync();
 }
@@ -558,6 +571,7 @@ TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
 // quantize, enc/encode_block.c:75-172 (rdoq = 0): X.C -> levels (q x q
 // raster) in X.C.  Returns cbp.
 TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
+  TE_P(TP_QUANT);
   const int intra = (type >> 1) & 1, chroma = type & 1;
   const int lg = te_log2(size), q = TE_MIN(size, 16), nq = q * q;
   const int scale = te_gquant[qp % 6], shift2 = 21 - lg + qp / 6;
@@ -581,25 +595,55 @@ TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
       lev = c < 0 ? -l : l;
       any |= l != 0;
     }
-    X.S[pos] = lev;
+    X.S[pos] = (int16_t)lev;
     X.O[pos] = X.C[r];
   }
   const int cbp = te_any(any);
   te_sync();
-  if (cbp && TE_LANE == 0) {  // "RDOQ light" (:134-168): serial over the scan
+  if (cbp) {  // "RDOQ light" (:134-168), serial over the scan.  Only positions whose
+    // initial level exceeds 1 can trigger: earlier iterations modify indices
+    // below the one they visit, so S[pos] is still its initial value when pos
+    // is visited.  Visit just those, in order, with the current levels.
     const int n = chroma ? last_pos + 1 : nq;
     const int thr = (73 * te_gdequant[qp % 6] << (qp / 6)) >> (4 + lg);
-    for (int pos = 2; pos < n; pos++) {
-      int flag = 1;
-      if (pos > 2 && te_abs(X.S[pos - 3]) > 1) flag = 0;
-      if (pos > 3 && te_abs(X.S[pos - 4]) > 1 && te_abs(X.S[pos - 3]) > 0) flag = 0;
-      if (pos == 2 && (chroma == 0 || last_pos >= 6)) flag = 0;
-      if (flag && X.S[pos - 2] == 0 && X.S[pos - 1] == 0 && te_abs(X.S[pos]) > 1) {
-        const int c1 = X.O[pos], c2 = X.O[pos - 1], c3 = X.O[pos - 2];
-        const int K1 = te_abs(c1), K2 = te_abs(c2), K3 = te_abs(c3), K4 = TE_MAX(K2, K3);
-        if (K1 + K4 < thr) X.S[pos] = c1 < 0 ? -1 : 1;
-        else if (K2 > K3) X.S[pos - 1] = c2 < 0 ? -1 : 1;
-        else X.S[pos - 2] = c3 < 0 ? -1 : 1;
+    uint64_t cand[4];
+#if defined(TE_HOST)
+    for (int k = 0; k < 4; k++) cand[k] = 0;
+    for (int pos = 2; pos < n; pos++)
+      if (te_abs(X.S[pos]) > 1) cand[pos >> 6] |= 1ULL << (pos & 63);
+#else
+    for (int k = 0; k < 4; k++) {
+      const int pos = TE_LANE + 64 * k;
+      cand[k] = __ballot(pos >= 2 && pos < n && te_abs(X.S[pos]) > 1);
+    }
+#endif
+    for (int k = 0; k < 4; k++) {
+      uint64_t m = cand[k];
+      while (m) {
+        const int pos = k * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        int flag = 1;
+        if (pos > 2 && te_abs(X.S[pos - 3]) > 1) flag = 0;
+        if (pos > 3 && te_abs(X.S[pos - 4]) > 1 && te_abs(X.S[pos - 3]) > 0) flag = 0;
+        if (pos == 2 && (chroma == 0 || last_pos >= 6)) flag = 0;
+        if (flag && X.S[pos - 2] == 0 && X.S[pos - 1] == 0 && te_abs(X.S[pos]) > 1) {
+          const int c1 = X.O[pos], c2 = X.O[pos - 1], c3 = X.O[pos - 2];
+          const int K1 = te_abs(c1), K2 = te_abs(c2), K3 = te_abs(c3), K4 = TE_MAX(K2, K3);
+          int at, v;
+          if (K1 + K4 < thr) {
+            at = pos;
+            v = c1 < 0 ? -1 : 1;
+          } else if (K2 > K3) {
+            at = pos - 1;
+            v = c2 < 0 ? -1 : 1;
+          } else {
+            at = pos - 2;
+            v = c3 < 0 ? -1 : 1;
+          }
+          te_sync();
+          if (TE_LANE == 0) X.S[at] = (int16_t)v;
+          te_sync();
+        }
       }
     }
   }
@@ -614,25 +658,26 @@ TE_FN void te_dequant(TeTx &X, int qp, int size) {
   const int q = TE_MIN(size, 16);
   const int rshift = te_log2(size) - 1, add = 1 << (rshift - 1);
   const int lshift = qp / 6, scale = te_gdequant[qp % 6];
-  for (int e = TE_LANE; e < q * q; e += TE_NL) X.C[e] = te_wrap16(((X.C[e] * scale) * (1 << lshift) + add) >> rshift);
+  for (int e = TE_LANE; e < q * q; e += TE_NL) X.C[e] = (int16_t)te_wrap16(((X.C[e] * scale) * (1 << lshift) + add) >> rshift);
   te_sync();
 }
 
 // inverse_transform (common/transform.c:432-518): X.C (q x q) -> X.R
 // (n x n, n = min(size, 32); 64 = the 32-point output, replicated 2x2 by the reader).
 TE_FN void te_inv_tx(TeTx &X, int size) {
+  TE_P(TP_INV);
   const int n = size == 64 ? 32 : size, q = TE_MIN(n, 16);
   for (int e = TE_LANE; e < q * n; e += TE_NL) {
-    const int k = e / n, yp = e - (e / n) * n;  // coefficient column k
+    const int k = te_dv(e, n), yp = e - te_dv(e, n) * n;  // coefficient column k
     int s = 0;
-    for (int m = 0; m < q; m++) s += te_dctN(n, m, yp) * X.C[m * q + k];
+    for (int m = 0; m < q; m++) s += TE_DCT(X, n, m, yp) * X.C[m * q + k];
     X.T[k * n + yp] = (int16_t)te_clip16((s + 64) >> 7);
   }
   te_sync();
   for (int e = TE_LANE; e < n * n; e += TE_NL) {
-    const int yp = e / n, xp = e - (e / n) * n;
+    const int yp = te_dv(e, n), xp = e - te_dv(e, n) * n;
     int s = 0;
-    for (int k = 0; k < q; k++) s += te_dctN(n, k, xp) * (int)X.T[k * n + yp];
+    for (int k = 0; k < q; k++) s += TE_DCT(X, n, k, xp) * (int)X.T[k * n + yp];
     X.R[yp * n + xp] = (int16_t)te_clip16((s + 2048) >> 12);
   }
   te_sync();

@@ -11,14 +11,35 @@ struct TeLevel {             // one quadtree level (64, 32, 16, 8)
   uint8_t rbuf[2][TE_BLK];   // rec_block / rec_block_best (roles swap, see te_copy_best)
   int16_t cbuf[3][3 * TE_COEF_COMP];  // coefficient sets: best, tmp, spare
 };
-struct TeScratch {
+struct TeScratchMem {         // global memory, one per worker wave
   TeLevel lv[4];
-  uint8_t pb[TE_BLK], pb0[TE_BLK], pb1[TE_BLK];  // predictions (Y | U | V, compact)
-  uint8_t org8[64 * 64];                         // bi-pred search target (search_bipred_prediction_params)
-  uint8_t rf[64 * 64];                           // exact sub-pel ME prediction
-  TeTx tx;
+  uint8_t pb0[TE_BLK], pb1[TE_BLK];  // bi-pred legs (Y | U | V, compact)
+  uint8_t org8[64 * 64];             // bi-pred search target (search_bipred_prediction_params)
+  uint8_t rf[64 * 64];               // exact sub-pel ME prediction
+  TeTx tx;                           // (host build: the LDS-resident buffers live here)
   TeNbr nb;
+  uint8_t pb[TE_BLK];
 };
+// The worker's buffers, passed by value: on the device the hot ones (the
+// transform chain, intra neighbours, the current prediction) point into LDS.
+struct TeScratch {
+  TeLevel *lv;
+  uint8_t *pb, *pb0, *pb1, *org8, *rf;
+  TeTx *tx;
+  TeNbr *nb;
+};
+TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb) {
+  TeScratch S;
+  S.lv = M.lv;
+  S.pb = pb;
+  S.pb0 = M.pb0;
+  S.pb1 = M.pb1;
+  S.org8 = M.org8;
+  S.rf = M.rf;
+  S.tx = tx;
+  S.nb = nb;
+  return S;
+}
 // State of the superblock being encoded (frame_info mvcand / best_ref are
 // reset per SB, enc/encode_frame.c:117-121) and its bit stream.
 struct TeSB {
@@ -72,12 +93,12 @@ TE_FN void te_pred_yuv(const TeFrame &F, int r, uint8_t *pb, const TeBlockInfo &
 TE_FN void te_avg_yuv(uint8_t *d, const uint8_t *a, const uint8_t *b, const TeBlockInfo &bi) {
   const int size = bi.size, bw = bi.bwidth, bh = bi.bheight;
   for (int e = TE_LANE; e < bw * bh; e += TE_NL) {
-    const int i = e / bw, j = e - (e / bw) * bw;
+    const int i = te_dv(e, bw), j = e - te_dv(e, bw) * bw;
     d[i * size + j] = (uint8_t)(((int)a[i * size + j] + (int)b[i * size + j]) >> 1);
   }
   const int cw = bw / 2, ch = bh / 2, cs = size / 2, co = size * size, cq = cs * cs;
   for (int e = TE_LANE; e < cw * ch; e += TE_NL) {
-    const int i = e / cw, j = e - (e / cw) * cw;
+    const int i = te_dv(e, cw), j = e - te_dv(e, cw) * cw;
     d[co + i * cs + j] = (uint8_t)(((int)a[co + i * cs + j] + (int)b[co + i * cs + j]) >> 1);
     d[co + cq + i * cs + j] = (uint8_t)(((int)a[co + cq + i * cs + j] + (int)b[co + cq + i * cs + j]) >> 1);
   }
@@ -93,9 +114,10 @@ TE_FN int te_sign_of(const TeFrame &F, int ref_idx, int bi) {
 // encode_and_reconstruct_block_inter, enc/encode_block.c:1469-1532, one
 // component: orig (frame, stride os) - pred -> levels (tiles of `coef`) ->
 // rec (compact, stride size).  Returns cbp (4-bit mask when tb-split).
-TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *org, int os, int size, int qp,
+TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch S, const uint8_t *org, int os, int size, int qp,
                                const uint8_t *pb, int16_t *coef, uint8_t *rec, int type, int tb_split) {
-  TeTx &X = S.tx;
+  TE_P(TP_INTER_COMP);
+  TeTx &X = *S.tx;
   int cbp = 0;
   if (tb_split) {
     const int s2 = size / 2, fast = size == 64 || F.speed > 1;
@@ -104,7 +126,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
     for (int t = 0; t < 4; t++) {
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
       for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = e / s2, x = e - (e / s2) * s2;
+        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
         X.R[e] = (int16_t)((int)org[(i + y) * os + j + x] - (int)pb[(i + y) * size + j + x]);
       }
       te_sync();
@@ -117,7 +139,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
         te_inv_tx(X, s2);
       }
       for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = e / s2, x = e - (e / s2) * s2;
+        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
         const int p = pb[(i + y) * size + j + x];
         rec[(i + y) * size + j + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, s2, y, x) + p) : p);
       }
@@ -128,7 +150,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
   }
   const int fast = (size == 64 && F.speed > 0) || F.speed > 1;
   for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = e / size, x = e - (e / size) * size;
+    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
     X.R[e] = (int16_t)((int)org[y * os + x] - (int)pb[e]);
   }
   te_sync();
@@ -141,7 +163,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
     te_inv_tx(X, size);
   }
   for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = e / size, x = e - (e / size) * size;
+    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
     rec[e] = (uint8_t)(cbp ? te_clip255(te_res_at(X, size, y, x) + pb[e]) : pb[e]);
   }
   te_sync();
@@ -150,20 +172,21 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
 
 // encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
 // component.  rf / fs: the frame being reconstructed at the CU origin.
-TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch &S, const uint8_t *org, int os, const uint8_t *rf, int fs,
+TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch S, const uint8_t *org, int os, const uint8_t *rf, int fs,
                                int ypos, int xpos, int size, int qp, uint8_t *pb, int16_t *coef, uint8_t *rec, int type,
                                int tb_split, int mode, int ur, int dl) {
-  TeTx &X = S.tx;
+  TE_P(TP_INTRA_COMP);
+  TeTx &X = *S.tx;
   const int fast = F.speed > 1;
   if (tb_split) {
     const int s2 = size / 2, q = TE_MIN(s2, 16);
     int cbp = 0;
     for (int t = 0; t < 4; t++) {
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
-      te_make_top_and_left(S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
-      te_intra_pred(S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
+      te_make_top_and_left(*S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
+      te_intra_pred(*S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
       for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = e / s2, x = e - (e / s2) * s2;
+        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
         X.R[e] = (int16_t)((int)org[(i + y) * os + j + x] - (int)pb[e]);
       }
       te_sync();
@@ -175,7 +198,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
         te_inv_tx(X, s2);
       }
       for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = e / s2, x = e - (e / s2) * s2;
+        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
         rec[(i + y) * size + j + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, s2, y, x) + pb[e]) : pb[e]);
       }
       te_sync();
@@ -183,10 +206,10 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
     }
     return cbp;
   }
-  te_make_top_and_left(S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
-  te_intra_pred(S.nb, ypos, xpos, size, pb, mode, 0);
+  te_make_top_and_left(*S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
+  te_intra_pred(*S.nb, ypos, xpos, size, pb, mode, 0);
   for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = e / size, x = e - (e / size) * size;
+    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
     X.R[e] = (int16_t)((int)org[y * os + x] - (int)pb[e]);
   }
   te_sync();
@@ -199,7 +222,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
     te_inv_tx(X, size);
   }
   for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = e / size, x = e - (e / size) * size;
+    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
     rec[e] = (uint8_t)(cbp ? te_clip255(te_res_at(X, size, y, x) + pb[e]) : pb[e]);
   }
   te_sync();
@@ -208,14 +231,15 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch &S, const uint8_t *or
 
 // encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
 // bi.rec, write the block's syntax.  Returns the bit count.
-TE_NOINL int te_encode_block(const TeFrame &F, TeScratch &S, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+TE_NOINL int te_encode_block(const TeFrame &F, TeScratch S, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  TE_P(TP_ENC_BLOCK);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, yC = ypos / 2, xC = xpos / 2, sC = size / 2;
   const int mode = p.mode;
   const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
   const int re_use = (bi.final_encode & 1) && !F.enable_tb_split;
   if (re_use) {
     te_copy_bytes(bi.rec, bi.rec_best, size * size + 2 * sC * sC);
-    return te_write_block(b, F, bi, p, S.tx.scan);
+    return te_write_block(b, F, bi, p, S.tx->scan);
   }
   uint8_t *recY = bi.rec, *recU = te_pu(bi.rec, size), *recV = te_pv(bi.rec, size);
   const int tb_split = TE_MAX(0, p.tb_param), zero_block = p.tb_param == -1;
@@ -271,13 +295,14 @@ TE_NOINL int te_encode_block(const TeFrame &F, TeScratch &S, TeBits &b, TeBlockI
   p.cbp_y = cy;
   p.cbp_u = cu;
   p.cbp_v = cv;
-  const int nbits = te_write_block(b, F, bi, p, S.tx.scan);
+  const int nbits = te_write_block(b, F, bi, p, S.tx->scan);
   if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
   return nbits;
 }
 
 // cost_calc, enc/encode_block.c:1218-1228
 TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *rec, int w, int h, int nbits) {
+  TE_P(TP_COST);
   const int size = bi.size, sC = size / 2;
   const int ypos = bi.ypos, xpos = bi.xpos;
   const uint32_t sy = te_ssd(F.oy + ypos * F.osy + xpos, F.osy, rec, size, w, h);
@@ -291,17 +316,18 @@ TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *r
 
 // search_intra_prediction_params, enc/encode_block.c:1230-1329: SAD over the
 // first `num_modes` modes in the order DC, HOR, VER, PLANAR, [UPLEFT ...].
-TE_NOINL int te_search_intra(const TeFrame &F, TeScratch &S, const TeBlockInfo &bi, int num_modes, int *mode_out) {
+TE_NOINL int te_search_intra(const TeFrame &F, TeScratch S, const TeBlockInfo &bi, int num_modes, int *mode_out) {
+  TE_P(TP_SEARCH_INTRA);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
   const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
-  te_make_top_and_left(S.nb, F.ry + ypos * F.rsy + xpos, F.rsy, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
+  te_make_top_and_left(*S.nb, F.ry + ypos * F.rsy + xpos, F.rsy, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
   const int order[10] = {TE_DC, TE_HOR, TE_VER, TE_PLANAR, TE_UPLEFT, TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT,
                          TE_UPLEFTLEFT, TE_DOWNLEFTLEFT};
   int min_sad = 1 << 30, best = TE_DC;
   const int n = num_modes == 4 ? 4 : 10;
   const uint8_t *o = F.oy + ypos * F.osy + xpos;
   for (int k = 0; k < n; k++) {
-    te_intra_pred(S.nb, ypos, xpos, size, S.pb, order[k], 1);
+    te_intra_pred(*S.nb, ypos, xpos, size, S.pb, order[k], 1);
     const int sad = (int)te_sad(o, F.osy, S.pb, size, size, size);
     if (sad < min_sad) {
       best = order[k];
@@ -317,9 +343,10 @@ TE_FN uint32_t te_lambda_bits(double lam, int bits) { return (uint32_t)(lam * (d
 // motion_estimate, enc/encode_block.c:830-1016 (params->sync = 0).  `org` /
 // `os`: the block (or partition) of the original; `ref`: the reference at the
 // block (partition) origin; size: the CU size (clip_mv, the size-16 rules).
-TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch &S, TeSB &sb, int r, const uint8_t *org, int os,
+TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, int r, const uint8_t *org, int os,
                                      const uint8_t *ref, int size, int width, int height, TeMv *mv, TeMv mvc, TeMv mvp,
                                      int sign, int xpos, int ypos, int enable_bipred) {
+  TE_P(TP_ME);
   const int rs = F.rsy, s = sign ? -1 : 1;
   const double lam = F.sqrt_lambda;
   uint32_t min_sad = TE_MAX_UINT32;
@@ -460,7 +487,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch &S, TeSB &sb, i
 }
 
 // search_inter_prediction_params, enc/encode_block.c:1331-1396
-TE_FN uint32_t te_search_inter(const TeFrame &F, TeScratch &S, TeSB &sb, int r, const uint8_t *org, int os,
+TE_FN uint32_t te_search_inter(const TeFrame &F, TeScratch S, TeSB &sb, int r, const uint8_t *org, int os,
                                const TeBlockInfo &bi, TeMv mvc, TeMv mvp, TeMv *mv_arr, int part, int sign,
                                int enable_bipred) {
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, rs = F.rsy;
@@ -545,15 +572,16 @@ TE_FN void te_copy_best(TeBlockInfo &bi, TeParam &tmp) {
 
 // copy_block_to_frame (:1802-1819) + copy_deblock_data (:1947-1981)
 TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
+  TE_P(TP_COMMIT);
   const int size = bi.size, bw = bi.bwidth, bh = bi.bheight, sC = size / 2;
   const uint8_t *r = bi.rec;
   for (int e = TE_LANE; e < bw * bh; e += TE_NL) {
-    const int i = e / bw, j = e - (e / bw) * bw;
+    const int i = te_dv(e, bw), j = e - te_dv(e, bw) * bw;
     F.ry[(bi.ypos + i) * F.rsy + bi.xpos + j] = r[i * size + j];
   }
   const int cw = bw / 2, ch = bh / 2;
   for (int e = TE_LANE; e < cw * ch; e += TE_NL) {
-    const int i = e / cw, j = e - (e / cw) * cw;
+    const int i = te_dv(e, cw), j = e - te_dv(e, cw) * cw;
     const int o = (bi.ypos / 2 + i) * F.rsc + bi.xpos / 2 + j;
     F.ru[o] = te_pu((uint8_t *)r, size)[i * sC + j];
     F.rv[o] = te_pv((uint8_t *)r, size)[i * sC + j];
@@ -562,7 +590,7 @@ TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
   const int div = size / 8, bs = F.W / 4;
   const int nw = bw / 4, nh = bh / 4;
   for (int e = TE_LANE; e < nw * nh; e += TE_NL) {
-    const int m = e / nw, n = e - (e / nw) * nw;
+    const int m = te_dv(e, nw), n = e - te_dv(e, nw) * nw;
     const int m0 = div > 0 ? m / div : 0, n0 = div > 0 ? n / div : 0, index = 2 * m0 + n0;
     TeCell c;
     c.ip.mv0 = p.mv0[index];
@@ -585,7 +613,7 @@ TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
 
 // search_bipred_prediction_params, enc/encode_block.c:2047-2202, me_mode 0
 // (the iterative uni-pred search on the modified target org8)
-TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch &S, TeSB &sb, TeBlockInfo &bi, int part,
+TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch S, TeSB &sb, TeBlockInfo &bi, int part,
                                    TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_arr0,
                                    TeMv *mv_arr1) {
   const int size = bi.size;
@@ -604,7 +632,7 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch &S, TeSB &sb, TeB
       const int sign = F.ref_fnum[ref_idx] > F.frame_num;
       te_pred_yuv(F, ref_idx, S.pb, bi, list ? m0 : m1, sign, 1, 1);
       for (int e = TE_LANE; e < size * size; e += TE_NL) {
-        const int y = e / size, x = e - (e / size) * size;
+        const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
         S.org8[e] = (uint8_t)te_clip255(2 * (int)org[y * F.osy + x] - (int)S.pb[e]);
       }
       te_sync();
@@ -647,7 +675,8 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch &S, TeSB &sb, TeB
 }
 
 // mode_decision_rdo, enc/encode_block.c:2204-2479
-TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch &S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+  TE_P(TP_MODE);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
   TeBits &b = sb.bits;
   const int frame_type = F.frame_type;
@@ -814,20 +843,20 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch &S, TeSB &sb, TeB
       }
     }
   }
-  b.pos = pos_ref;  // rewind (:2476)
+  te_rewind(b, pos_ref);  // rewind (:2476)
   return min_cost;
 }
 
 // ---- early skip (enc/encode_block.c:2481-2783) -------------------------------
 // check_early_skip_sub_block (luma, :2505-2538): 2x2-average + (N/2)-point
 // transform against half the threshold (N = 4: plain 4-point transform).
-TE_FN int te_es_luma(TeScratch &S, const uint8_t *org, int os, int size, const uint8_t *pb, int thr) {
-  TeTx &X = S.tx;
+TE_FN int te_es_luma(TeScratch S, const uint8_t *org, int os, int size, const uint8_t *pb, int thr) {
+  TeTx &X = *S.tx;
   int n = size;
   if (size > 4) {
     const int s2 = size / 2;
     for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-      const int i = e / s2, j = e - (e / s2) * s2;
+      const int i = te_dv(e, s2), j = e - te_dv(e, s2) * s2;
       const int i2 = 2 * i, j2 = 2 * j;
       const int a = (int)org[i2 * os + j2] - pb[i2 * size + j2], b = (int)org[i2 * os + j2 + 1] - pb[i2 * size + j2 + 1];
       const int c = (int)org[(i2 + 1) * os + j2] - pb[(i2 + 1) * size + j2],
@@ -870,7 +899,8 @@ TE_FN int te_es_chroma(const uint8_t *org, int os, int size, const uint8_t *pb, 
 }
 
 // check_early_skip_block, :2613-2741.  Returns 1 when every sub-block is insignificant.
-TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch &S, const TeBlockInfo &bi, const TeParam &p) {
+TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch S, const TeBlockInfo &bi, const TeParam &p) {
+  TE_P(TP_ES_CHECK);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, size0 = TE_MIN(size, 32);
   const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
   const int *T = F.es_thr + ((F.speed > 1 && size == 64) ? 52 * 4 : 0);  // 1.3x threshold for 64x64 at speed 2
@@ -916,7 +946,8 @@ TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch &S, const TeBlockIn
 }
 
 // search_early_skip_candidates, :2743-2783
-TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch &S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+  TE_P(TP_ES_SEARCH);
   uint32_t min_cost = TE_MAX_UINT32;
   int early = 0;
   TeParam tmp;
@@ -948,7 +979,7 @@ TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch &S, TeSB &sb, TeBl
 // Template over the CU size: the quadtree recursion unrolls at compile time
 // (64 -> 32 -> 16 -> 8); level L = log2(64 / SIZE) owns TeScratch::lv[L].
 template <int SIZE>
-TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch &S, TeSB &sb, int ypos, int xpos, int qp) {
+TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch S, TeSB &sb, int ypos, int xpos, int qp) {
   constexpr int L = SIZE == 64 ? 0 : (SIZE == 32 ? 1 : (SIZE == 16 ? 2 : 3));
   const int W = F.W, H = F.H, ft = F.frame_type;
   if (ypos >= H || xpos >= W) return 0;
@@ -983,7 +1014,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch &S, TeSB &sb, int
   if (encode_this && ft != TE_I && F.early_skip_thr > 0.0f) {
     bi.final_encode = 2;
     const int early = te_search_early_skip(F, S, sb, bi, tmp_coef);
-    b.pos = pos_ref;
+    te_rewind(b, pos_ref);
     if (early) {
       bi.final_encode = 3;
       bi.bp.mode = TE_SKIP;
@@ -1024,7 +1055,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch &S, TeSB &sb, int
       }
     }
     if (cost <= cost_small) {
-      b.pos = pos_ref;
+      te_rewind(b, pos_ref);
       bi.final_encode = 1;
       te_encode_block(F, S, b, bi, bi.bp);
       te_commit_block(F, bi);
@@ -1033,7 +1064,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch &S, TeSB &sb, int
     bi.final_encode = 0;
     cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == lv.cbuf[0] ? lv.cbuf[1] : lv.cbuf[0]);
     if (cost <= cost_small) {
-      b.pos = pos_ref;
+      te_rewind(b, pos_ref);
       bi.final_encode = 1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
@@ -1048,14 +1079,15 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch &S, TeSB &sb, int
 // the ME candidate lists, then process_block(64) -- with the delta-qp RD
 // search when max_delta_qp is set (trials leave their candidates behind, as
 // there).  Returns the SB's bit count in sb.bits.
-TE_FN void te_encode_sb(const TeFrame &F, TeScratch &S, TeSB &sb, int k, int l) {
+TE_FN void te_encode_sb(const TeFrame &F, TeScratch S, TeSB &sb, int k, int l) {
+  TE_P(TP_SB);
   const int ypos = k * 64, xpos = l * 64;
   for (int r = 0; r < F.num_ref; r++) {
     sb.mc.num[r] = 0;
     sb.mc.mask[r] = 0;
   }
   sb.best_ref = -1;
-  sb.bits.pos = 0;
+  te_bits_start(sb.bits);
   if (F.max_delta_qp) {
     int min_cost = 1 << 30, best_qp = F.qp;
     for (int q = F.qp - F.max_delta_qp; q <= F.qp + F.max_delta_qp; q += F.delta_qp_step) {
@@ -1065,11 +1097,12 @@ TE_FN void te_encode_sb(const TeFrame &F, TeScratch &S, TeSB &sb, int k, int l) 
         best_qp = q;
       }
     }
-    sb.bits.pos = 0;
+    te_rewind(sb.bits, 0);
     te_process_block<64>(F, S, sb, ypos, xpos, best_qp);
   } else {
     te_process_block<64>(F, S, sb, ypos, xpos, F.qp);
   }
+  te_bits_flush(sb.bits);
 }
 
 // clpf_decision + the CLPF candidate test of clpf_frame, enc/encode_frame.c:50-63,

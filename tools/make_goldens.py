@@ -48,6 +48,8 @@ STREAMS = [
     # round 2: BASELINE config 4 (bi-pred at 4K), a width = 8 mod 16 clip (enc/strings.c:437)
     ("k4_med", 3840, 2160, 8, "config_LDB_medium_complexity.txt", [], 7),
     ("w8_low", 360, 288, 6, "config_LDB_low_complexity.txt", [], 8),
+    # BASELINE config 3 operating point at 1080p (3 frames: the reference needs ~75 s)
+    ("hd_high", 1920, 1080, 3, "config_LDB_high_efficiency.txt", [], 9),
 ]
 
 
