@@ -1,27 +1,30 @@
 #!/usr/bin/env python3
-"""Benchmark: Thor per-block reconstruction on MI355X.
+"""Benchmark: Thor encode + decode of a 4K LDB-low stream on MI355X.
 
-Workload (config.workload): the reference's own 4K (3840x2160) 8-frame
-config_LDB_low_complexity stream of a seeded synthetic clip
-(tests/golden/k4_low.*).  One step = GPU reconstruction of the whole stream,
-frame after frame as the decoder must (frame n+1 references frame n): per
-frame, per-4x4 side info, inter MC + dequant + inverse transform +
-reconstruction, intra, deblock Y/UV, CLPF and reference padding, all through
-libthor_amd.so's C-ABI.  The parse output (block descriptors, coefficients,
-intra list, CLPF flags) is resident in HBM before timing starts; bit parsing
-is CPU work outside the hot path.  The decoded frames are checked bit-exact
-against the reference decoder's md5s (every context) after warmup.
+Metric (BASELINE.json): Mpixels/s encode+decode, 4K (3840x2160)
+config_LDB_low_complexity, bit-exact vs the reference.  Workload
+(config.workload): the seeded synthetic 8-frame 4K clip of tests/golden/k4_low
+(thor_amd/synth.py; no real clips or network), input frames resident in HBM.
 
-Per GPU, --streams K (default 24: 3 groups of 8, THOR_MAX_BATCH) independent decoder contexts each decode
-their own copy of the stream on their own HIP stream, interleaved frame by
-frame (a server decoding K streams): value = K x stream pixels / time.  The
-single-stream latency of one pass is reported next to it
-(config.single_stream_ms_per_pass).
+One step, per GPU, for K independent streams (a server coding K clips):
+  encode  every stream's 8 frames through the device-resident encoder
+          (thor_enc_frames: WPP RD loop, loop filters, CLPF decision and bit
+          packing on the GPU, one launch per stage for the K streams) -> the
+          streams' .bit, each checked byte for byte against the reference
+          Thorenc's tests/golden/k4_low.bit;
+  decode  every .bit: host parse (thor_parse_frame, 16 threads) -> upload of
+          the parse output -> batched GPU reconstruction (thor_dec_frames),
+          each decoded sequence checked against the reference Thordec md5.
+value = K x W x H x frames / (t_enc + t_dec), wall clock, both legs complete
+(host parse and the H2D of its output included in t_dec).
 
-N > 1: one process per GPU, each with its own K streams (independent
-streams, no data-path collective): scaling "weak".
+Reported beside it (not part of `value`): the single-stream enc+dec latency,
+decode_only (the reconstruction of resident parse output, the round-1
+figure), the k_recon roofline (the north-star 4K inter-reconstruction kernel,
+hipEvents on its stream) and a few kernel legs.
 
-Prints one JSON line (rank 0).
+N > 1: one process per GPU, each with its own K streams (no data-path
+collective): scaling "weak".  Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -30,14 +33,16 @@ import ctypes as C
 import hashlib
 import json
 import os
+import shlex
 import subprocess
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# one hardware queue per decoder context (HIP's default is 4 per process);
-# must be set before the HIP runtime initialises
+# one hardware queue per decoder group (HIP's default is 4 per process); must be
+# set before the HIP runtime initialises
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
@@ -46,6 +51,7 @@ import numpy as np  # noqa: E402
 METRIC = "Mpixels/s encode+decode, 4K LDB_low_complexity; bit-exact vs ref"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 STAGES = ["prep", "inter", "intra", "deblock", "clpf", "pad"]
+HOST_THREADS = 16  # the GPU box's CPU share per GPU
 
 
 def recon_alg_bytes(fr, width: int, height: int) -> float:
@@ -84,9 +90,9 @@ def encoder_leg(torch, lib, reps: int = 10):
     CU at every quadtree level (64, 32, 16, 8) over a whole 1080p frame --
     orig = synthetic frame 1, pred = frame 0 co-located -- residual -> forward
     T -> quantize -> dequant -> inverse T -> recon -> SSD per TU
-    (thor_enc_tu_batch), then cost_calc per CU (thor_enc_cost_batch).  The
-    serial RD search that would issue these batches is not on the GPU
-    (SURVEY.md sec. 8(f) #4)."""
+    (thor_enc_tu_batch), then cost_calc per CU (thor_enc_cost_batch): the
+    batched entry points of the encoder's TU chain.  The device-resident
+    encoder (k_enc_rows) runs the same chain inline in its RD loop."""
     from thor_amd import synth
 
     W, H, qp = 1920, 1080, 32
@@ -255,50 +261,105 @@ def interp_leg(torch, lib, reps: int = 50):
             "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
 
 
-def cpu_baseline(meta, gold, budget_s: float = 20.0):
-    """Reference decoder (oracle/_ref/Thordec, SIMD build, 1 thread) on the
-    same .bit, repeated up to ~budget_s; falls back to the oracle port."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "Thordec")
-    bit = os.path.join(gold, "k4_low.bit")
-    px = meta["width"] * meta["height"] * meta["frames"]
-    if os.path.exists(exe):
-        out = "/tmp/thor_bench_dec_%d.yuv" % os.getpid()
-        runs, t_tot = 0, 0.0
-        while t_tot < budget_s and runs < 30:
-            t0 = time.perf_counter()
-            subprocess.run([exe, bit, out], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-            t_tot += time.perf_counter() - t0
-            runs += 1
-        ok = hashlib.md5(open(out, "rb").read()).hexdigest() == meta["dec_md5"]
-        os.remove(out)
-        return {"value": round(px * runs / t_tot / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
-                "sample": "reference Thordec (SIMD build, -O3, 1 thread) decoding the same 4K 8-frame .bit "
-                          "%d times (bit parsing included); output md5 %s" % (runs, "ok" if ok else "MISMATCH")}
-    from oracle import OracleDecoder
-    from thor_amd.trace import load_trace
+def cpu_baseline(meta, clip: np.ndarray, procs: int = HOST_THREADS, budget_s: float = 8.0):
+    """The reference encoder + decoder (oracle/_ref/Thorenc, Thordec: SIMD
+    build, -O3) on the same clip and configuration: `procs` concurrent
+    encode->decode pipelines on the host cores (one stream each), plus one
+    pipeline alone (1 core).  Returns None when the reference binaries are not
+    present (they are built from /root/reference by oracle/Makefile)."""
+    from thor_amd.configs import flags
 
-    seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
-    t0 = time.perf_counter()
-    dec = OracleDecoder(seq)
-    for _ in dec.run(frames):
-        pass
-    dt = time.perf_counter() - t0
-    return {"value": round(px / dt / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "oracle restatement (plain C, 1 thread), full 8-frame stream"}
+    enc = os.path.join(ROOT, "oracle", "_ref", "Thorenc")
+    dec = os.path.join(ROOT, "oracle", "_ref", "Thordec")
+    if not (os.path.exists(enc) and os.path.exists(dec)):
+        return None
+    W, H, n = meta["width"], meta["height"], meta["frames"]
+    px = W * H * n
+    tmp = "/tmp/thor_bench_%d" % os.getpid()
+    os.makedirs(tmp, exist_ok=True)
+    yuv = os.path.join(tmp, "in.yuv")
+    clip.tofile(yuv)
+    fl = flags(meta["config"], W, H, n, meta["extra"])
+
+    def pipeline(k):
+        bit, out = os.path.join(tmp, "%d.bit" % k), os.path.join(tmp, "%d.yuv" % k)
+        cmd = "%s -if %s -of %s %s >/dev/null 2>&1 && %s %s %s >/dev/null 2>&1" % (
+            shlex.quote(enc), yuv, bit, " ".join(shlex.quote(f) for f in fl), shlex.quote(dec), bit, out)
+        return subprocess.Popen(["/bin/sh", "-c", cmd])
+
+    try:
+        # one pipeline alone, repeated within the budget
+        runs, t1 = 0, 0.0
+        while runs < 1 or (t1 < budget_s and runs < 5):
+            t0 = time.perf_counter()
+            assert pipeline(0).wait() == 0
+            t1 += time.perf_counter() - t0
+            runs += 1
+        ok = hashlib.md5(open(os.path.join(tmp, "0.bit"), "rb").read()).hexdigest() == meta["bit_md5"]
+        ok &= hashlib.md5(open(os.path.join(tmp, "0.yuv"), "rb").read()).hexdigest() == meta["dec_md5"]
+        one = px * runs / t1 / 1e6
+        # `procs` pipelines at once on the host cores
+        t0 = time.perf_counter()
+        ps = [pipeline(k) for k in range(procs)]
+        rcs = [p.wait() for p in ps]
+        tp = time.perf_counter() - t0
+        assert all(r == 0 for r in rcs), rcs
+        for k in range(procs):
+            ok &= hashlib.md5(open(os.path.join(tmp, "%d.yuv" % k), "rb").read()).hexdigest() == meta["dec_md5"]
+    finally:
+        for f in os.listdir(tmp):
+            os.remove(os.path.join(tmp, f))
+        os.rmdir(tmp)
+    return {"value": round(px * procs / tp / 1e6, 3), "unit": "Mpixels/s", "cores": procs, "kind": "reference",
+            "sample": "reference Thorenc -> Thordec (SIMD build, -O3) on the same 4K 8-frame LDB-low clip: "
+                      "%d concurrent single-threaded pipelines (one per host core of the GPU's share), %.1f s wall; "
+                      "bitstream + decoded md5 %s" % (procs, tp, "ok" if ok else "MISMATCH"),
+            "single_core_mpx_s": round(one, 3), "single_core_s_per_pass": round(t1 / runs, 3)}
+
+
+def roofline_pass(lib, decs, groups, devs, frames, seq, isteps):
+    """Instrumented decode of group 0 alone (resident parse output): hipEvents
+    around every stage of every batched launch on its stream -> the stage
+    breakdown and the k_recon roofline (one launch = the group's B frames)."""
+    lead = decs[groups[0][0]]
+    B = len(groups[0])
+    nf = len(frames)
+    from thor_amd.decoder import decode_batch
+
+    lib.thor_dec_set_timing(lead.h, 1)
+    cap = 8 * nf * (isteps + 1)
+    mk_stage, mk_ms = (C.c_int * cap)(), (C.c_double * cap)()
+    lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
+    for _ in range(isteps):
+        for i in range(nf):
+            decode_batch([decs[k] for k in groups[0]], [devs[k][i] for k in groups[0]])
+    nm = lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
+    lib.thor_dec_set_timing(lead.h, 0)
+    per_frame, cur = [], None
+    for k in range(nm):  # every frame opens with its side-info stage (0)
+        if mk_stage[k] == 0:
+            cur = [0.0] * 6
+            per_frame.append(cur)
+        cur[mk_stage[k]] += mk_ms[k]
+    assert len(per_frame) == isteps * nf, (len(per_frame), isteps, nf)
+    stage_ms = [sum(f[i] for f in per_frame) / isteps / B for i in range(6)]  # per stream pass
+    pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]  # the I frame has no inter pixels
+    recon_ms = sum(per_frame[s * nf + i][1] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
+    alg = B * sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
+    return stage_ms, recon_ms, alg, B
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=24, help="independent decoder contexts per GPU")
-    ap.add_argument("--groups", type=int, default=3,
-                    help="batches per frame slot (contexts of a group share one launch per stage)")
+    ap.add_argument("--no-legs", action="store_true", help="skip the kernel legs reported beside `value`")
+    ap.add_argument("--streams", type=int, default=32, help="independent streams (encoder + decoder) per GPU")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
-                    help="streams: independent streams per GPU (default); rows: ONE stream's SB rows split "
-                         "across the ranks with an RCCL all-gather of the bands before intra/deblock")
+                    help="streams: independent enc+dec streams per GPU (default); rows: decode-only, ONE "
+                         "stream's SB rows split across the ranks with an RCCL all-gather before intra/deblock")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per k_recon launch (default tools/traffic_latest.json, "
                          "copied from profiles/<tag>_traffic.json by tools/prof_summary.py)")
@@ -307,135 +368,108 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gold = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold, "streams.json")))["k4_low"]
+    W, H, nf = meta["width"], meta["height"], meta["frames"]
+
+    clip = None
+    if a.shard == "streams":  # synthesise the input before anything touches the GPU (worker processes fork)
+        from thor_amd import synth
+
+        clip = synth.synth_frames(W, H, nf, meta["seed"], workers=8)
+        assert hashlib.md5(clip.tobytes()).hexdigest() == meta["synth_md5"], "synthetic clip drifted"
 
     import torch
 
     dist = None
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-
     if a.shard == "rows":
         return rows_mode(a, torch, dist, rank, world, local)
 
     from thor_amd import lib as L
+    from thor_amd.bitstream import parse_stream
     from thor_amd.decoder import GpuDecoder, decode_batch
-    from thor_amd.trace import load_trace
+    from thor_amd.encoder import GpuEncoder, encode_batch, params_for
 
-    gold = os.path.join(ROOT, "tests", "golden")
-    meta = json.load(open(os.path.join(gold, "streams.json")))["k4_low"]
-    seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
-    # K decoder contexts per GPU, each decoding its own copy of the stream on its
-    # own HIP stream (independent streams, as a server decodes many): the I
-    # frame's intra chain occupies ~100 waves, so other streams' frames fill the
-    # GPU meanwhile.  Context 0 alone gives the single-stream latency.
-    K = max(1, a.streams)
-    # each context enqueues on its own non-blocking HIP stream (created by
-    # thor_dec_create, consecutively, so they spread over the hardware queues)
-    decs, devs = [], []
-    for k in range(K):
-        dk = GpuDecoder(seq, device=local)
-        decs.append(dk)
-        devs.append([dk.upload(fr) for fr in frames])
-    dec = decs[0]
-    torch.cuda.synchronize(local)
-
-    # Contexts are split into G groups; a group decodes its contexts' next frames
-    # with one launch per stage (thor_dec_frames) on its leader's HIP stream.
-    # Every context decodes the stream cyclically (frames 0..7, 0..7, ...) and
-    # group g runs (8g/G) frames out of phase with group 0, so the groups' I
-    # frames (the latency-bound intra chains) overlap other groups' P frames.
-    nf = len(frames)
-    G = max(1, min(a.groups, K))
-    groups = [list(range(g, K, G)) for g in range(G)]
-    gphase = [(g * nf) // G for g in range(G)]
-    phase = [0] * K
-    for g, ks in enumerate(groups):
-        for k in ks:
-            phase[k] = gphase[g]
-
+    lib = L.load()
+    want_bit = open(os.path.join(gold, "k4_low.bit"), "rb").read()
+    K = max(1, min(a.streams, 64))
+    encs = []
+    for _ in range(K):
+        e = GpuEncoder(params_for(meta["config"], W, H, nf, meta["extra"]), device=local)
+        e.upload_sequence(clip)
+        encs.append(e)
+    seq, _ = parse_stream(want_bit)
+    decs = [GpuDecoder(seq, device=local) for _ in range(K)]
+    groups = [list(range(g, min(g + 8, K))) for g in range(0, K, 8)]  # THOR_MAX_BATCH contexts per launch
     for gk in groups:  # a group's members enqueue on their leader's stream
         for k in gk[1:]:
             decs[k].set_stream(C.c_void_p(decs[gk[0]].stream()))
+    pools = [[{} for _ in range(nf)] for _ in range(K)]  # per stream and frame: re-used device buffers
+    pool = ThreadPoolExecutor(HOST_THREADS)
 
-    def step(ks=None, gs=None):
-        for i in range(nf):  # interleave the groups frame by frame
-            if ks is not None:
-                for k in ks:
-                    decs[k].decode(devs[k][(phase[k] + i) % nf])
-                continue
-            for g in (range(G) if gs is None else gs):
-                gk = groups[g]
-                decode_batch([decs[k] for k in gk], [devs[k][(gphase[g] + i) % nf] for k in gk])
+    def encode(ks):
+        for k in ks:
+            encs[k].reset()
+        bits = [[] for _ in ks]
+        fms = []
+        for _ in range(nf):
+            t0 = time.perf_counter()
+            for j, ch in enumerate(encode_batch([encs[k] for k in ks])):
+                bits[j].append(ch)
+            fms.append((time.perf_counter() - t0) * 1e3)
+        return [b"".join(b) for b in bits], fms
 
-    def sync_all():
-        for dk in decs:
-            dk.sync()
-        torch.cuda.synchronize(local)
+    def decode(ks, bits):
+        def host(j):  # parse + upload of one stream (GIL released inside the C calls)
+            k = ks[j]
+            _, frames = parse_stream(bits[j])
+            return [decs[k].upload(fr, pools[k][i]) for i, fr in enumerate(frames)]
 
-    for k in range(K):  # one plain pass (every reference resident), then shift to the context's phase
-        for i in range(nf + phase[k]):
-            decs[k].decode(devs[k][i % nf])
-    for _ in range(a.warmup):
-        step()
-    sync_all()
+        devs = list(pool.map(host, range(len(ks))))
+        gs = [[j for j, k in enumerate(ks) if k in gk] for gk in groups]
+        for i in range(nf):
+            for g in gs:
+                if g:
+                    decode_batch([decs[ks[j]] for j in g], [devs[j][i] for j in g])
+        for k in ks:
+            decs[k].sync()
+        return devs
 
-    # check bit-exactness of what every context produced
-    bit_exact = True
-    for dk in decs:
-        got = {fr.frame_num: dk.read_i420(fr.frame_num) for fr in frames}
-        yuv = b"".join(got[k] for k in sorted(got))
-        bit_exact &= hashlib.md5(yuv).hexdigest() == meta["dec_md5"]
+    def step(ks):
+        t0 = time.perf_counter()
+        bits, fms = encode(ks)
+        t1 = time.perf_counter()
+        devs = decode(ks, bits)
+        t2 = time.perf_counter()
+        return t1 - t0, t2 - t1, bits, devs, fms
 
-    lib = L.load()
+    allk = list(range(K))
+    for _ in range(max(1, a.warmup)):
+        _, _, bits, devs, _ = step(allk)
+    # bit-exactness: every stream's .bit vs the reference Thorenc, every decode vs the reference Thordec
+    bit_exact = all(b == want_bit for b in bits)
+    for k in allk:
+        got = {fr: decs[k].read_i420(fr) for fr in range(nf)}
+        bit_exact &= hashlib.md5(b"".join(got[i] for i in range(nf))).hexdigest() == meta["dec_md5"]
+
     if dist is not None:
         dist.barrier()
-    sync_all()
-    t0 = time.perf_counter()
+    torch.cuda.synchronize(local)
+    t_enc = t_dec = 0.0
+    enc_frame_ms = [0.0] * nf
     for _ in range(a.steps):
-        step()
-    sync_all()
-    elapsed = time.perf_counter() - t0
-
-    # single-stream latency of one pass over the stream (context 0 alone)
-    lsteps = max(1, min(a.steps, 10))
-    t1 = time.perf_counter()
-    for _ in range(lsteps):
-        step(ks=[0])
-    sync_all()
-    latency_ms = (time.perf_counter() - t1) / lsteps * 1e3
-
-    # instrumented pass (not part of `value`): group 0 alone, hipEvents around
-    # every stage of every batched launch on its stream, for the stage breakdown
-    # and the roofline (one launch = the group's B frames)
-    isteps = max(1, min(a.steps, 5))
-    lead = decs[groups[0][0]]
-    B = len(groups[0])
-    lib.thor_dec_set_timing(lead.h, 1)
-    cap = 8 * len(frames) * (isteps + 1)
-    mk_stage, mk_ms = (C.c_int * cap)(), (C.c_double * cap)()
-    lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
-    for _ in range(isteps):
-        step(gs=[0])
-    nm = lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
-    lib.thor_dec_set_timing(lead.h, 0)
-    # attribute the marks to frames: every frame opens with its side-info stage (0)
-    per_frame, cur = [], None
-    for k in range(nm):
-        if mk_stage[k] == 0:
-            cur = [0.0] * 6
-            per_frame.append(cur)
-        cur[mk_stage[k]] += mk_ms[k]
-    assert len(per_frame) == isteps * len(frames), (len(per_frame), isteps, len(frames))
-    stage_ms = [sum(f[i] for f in per_frame) / isteps / B for i in range(6)]  # per stream pass
-    # k_recon roofline over the P frames (the I frame has no inter pixels)
-    pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]
-    recon_ms = sum(per_frame[s * len(frames) + i][1] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
-    alg = B * sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
+        te, td, bits, devs, fms = step(allk)
+        t_enc += te
+        t_dec += td
+        enc_frame_ms = [x + y / a.steps for x, y in zip(enc_frame_ms, fms)]
+        bit_exact &= all(b == want_bit for b in bits)
+    torch.cuda.synchronize(local)
+    elapsed = t_enc + t_dec
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -443,11 +477,27 @@ def main():
         ok = torch.tensor([1 if bit_exact else 0], device="cuda")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         bit_exact = bool(ok.item())
+    px_stream = W * H * nf
+    value = world * K * px_stream * a.steps / elapsed / 1e6
 
-    px_step = seq.width * seq.height * len(frames)
-    value = world * K * px_step * a.steps / elapsed / 1e6
-    ms_per_step = elapsed / a.steps * 1e3
-
+    # ---- beside `value` ----
+    # single-stream latency: stream 0 alone, encode + decode
+    lat = [step([0])[:2] for _ in range(2)]
+    lat_enc, lat_dec = min(x[0] for x in lat), min(x[1] for x in lat)
+    # decode_only: reconstruction of every stream's resident parse output (no parse, no upload)
+    frames = parse_stream(want_bit)[1]
+    dsteps = 5
+    for k in allk:
+        decs[k].sync()
+    t0 = time.perf_counter()
+    for _ in range(dsteps):
+        for i in range(nf):
+            for gk in groups:
+                decode_batch([decs[k] for k in gk], [devs[k][i] for k in gk])
+    for k in allk:
+        decs[k].sync()
+    t_do = (time.perf_counter() - t0) / dsteps
+    stage_ms, recon_ms, alg, B = roofline_pass(lib, decs, groups, devs, frames, seq, 3)
     achieved = alg / (recon_ms / 1e3) / 1e9 if recon_ms > 0 else 0.0
     traffic = None
     tj = a.traffic_json or os.path.join(ROOT, "tools", "traffic_latest.json")
@@ -462,29 +512,33 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8/i16",
-            "data": "synthetic (seeded clip, thor_amd/synth.py) encoded by the reference Thorenc; "
-                    "parse output resident in HBM",
+            "data": "synthetic (seeded 4K clip, thor_amd/synth.py), input frames resident in HBM",
             "bit_exact": bit_exact,
             "config": {
-                "workload": "decode-side per-block reconstruction of the 4K (3840x2160) 8-frame "
-                            "config_LDB_low_complexity reference stream: inter MC + dequant + inverse transform + "
-                            "recon, intra, deblock, CLPF, padding (encode-side reconstruction not yet on GPU)",
-                "frames": len(frames),
-                "width": seq.width,
-                "height": seq.height,
-                "parallelism": "streams: %d GPU(s) x %d independent decoder contexts" % (world, K),
+                "workload": "encode + decode of the 4K (3840x2160) 8-frame config_LDB_low_complexity stream: "
+                            "device-resident encoder (RD loop, loop filters, CLPF, bit packing) -> .bit == reference "
+                            "Thorenc's; host parse -> upload -> GPU reconstruction == reference Thordec's output",
+                "frames": nf, "width": W, "height": H,
+                "parallelism": "streams: %d GPU(s) x %d independent streams" % (world, K),
                 "streams_per_gpu": K,
-                "batch_groups": G,
+                "t_enc_ms_per_step": round(t_enc / a.steps * 1e3, 2),
+                "t_dec_ms_per_step": round(t_dec / a.steps * 1e3, 2),
+                "enc_mpx_s": round(K * px_stream * a.steps / t_enc / 1e6, 2),
+                "dec_mpx_s": round(K * px_stream * a.steps / t_dec / 1e6, 2),
+                "enc_batch_frame_ms": [round(x, 2) for x in enc_frame_ms],
+                "single_stream_enc_ms": round(lat_enc * 1e3, 2),
+                "single_stream_dec_ms": round(lat_dec * 1e3, 2),
+                "single_stream_mpx_s": round(px_stream / (lat_enc + lat_dec) / 1e6, 2),
+                "decode_only_mpx_s": round(K * px_stream / t_do / 1e6, 1),
+                "decode_only_note": "GPU reconstruction of the K streams' resident parse output (no parse, "
+                                    "no upload): the round-1 headline",
+                "stage_ms_per_stream_pass": {k: round(v, 4) for k, v in zip(STAGES, stage_ms)},
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                "single_stream_ms_per_pass": round(latency_ms, 4),
-                "single_stream_mpx_s": round(px_step / latency_ms / 1e3, 1),
-                "stage_ms_per_step": {k: round(v, 4) for k, v in zip(STAGES, stage_ms)},
-                "stage_note": "per stream pass: hipEvent-bracketed batched stages of group 0 alone / frames per launch",
             },
             "roofline": {
                 "bound": "hbm",
@@ -497,18 +551,21 @@ def main():
                 "alg_bytes_per_launch": round(alg),
                 "avg_launch_us": round(recon_ms * 1e3, 2),
                 "frames_per_launch": B,
-                "launches": "batched P-frame launches of group 0 alone; hipEvents on its stream",
+                "launches": "batched P-frame decode launches of group 0 alone; hipEvents on its stream",
             },
         }
-        if world == 1:
+        if world == 1 and not a.no_legs:
             out["encoder_tu_chain"] = encoder_leg(torch, lib)
             out["temporal_pyramid"] = pyramid_leg(torch, lib)
             out["temporal_interp_comp"] = interp_leg(torch, lib)
         if not a.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(meta, gold)
+            cb = cpu_baseline(meta, clip)
+            if cb is not None:
+                out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
-    for dk in decs:
-        dk.close()
+    pool.shutdown()
+    for x in encs + decs:
+        x.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -285,7 +285,7 @@ int thor_enc_num_frames(const thor_enc_t *e);
 int thor_enc_next_input(const thor_enc_t *e);
 void *thor_enc_stream(thor_enc_t *e);
 /* Code the next frame of each of `n` DIFFERENT contexts (same device and
- * size, n <= 16) with one launch per stage.  orig[i]: DEVICE pointer to the
+ * size, n <= 64) with one launch per stage.  orig[i]: DEVICE pointer to the
  * context's input frame thor_enc_next_input(es[i]), planar I420, luma stride
  * orig_stride[i] (NULL: width), chroma stride half of it.  Synchronous. */
 int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
@@ -296,6 +296,10 @@ int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride);
 long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap);
 /* The last coded frame's reconstruction (deblocked, CLPF'd), host planes. */
 int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
+/* Restart the context at the first frame of its sequence (the reference
+ * window emptied, the sequence header due again): a server re-using a
+ * context for the next clip of the same parameters. */
+int thor_enc_reset(thor_enc_t *e);
 
 /* ---- temporal interpolation: luma down-sampling pyramid ----------------- */
 

@@ -22,9 +22,8 @@ def _frames(b):
 
 
 def _input(meta, n):
-    w, h = meta["width"], meta["height"]
-    return np.stack([np.concatenate([p.reshape(-1) for p in synth.synth_frame(w, h, t, meta["seed"])])
-                     for t in range(n)])
+    # serial: no fork from a process that has initialised the GPU
+    return synth.synth_frames(meta["width"], meta["height"], n, meta["seed"], workers=1)
 
 
 @pytest.mark.parametrize("name,nframes", [("cif_low", 10), ("w8_low", 6), ("cif_med", 10), ("hd_low", 17)])
@@ -86,10 +85,11 @@ def test_gpu_decode_from_bitstream(name, streams):
         dec.close()
 
 
-@pytest.mark.parametrize("name,nframes", [("cif_high", 4), ("k4_low", 8), ("k4_med", 3)])
+@pytest.mark.parametrize("name,nframes", [("cif_high", 4), ("k4_low", 8), ("k4_med", 3), ("hd_high", 2)])
 def test_device_encoder_more_configs(name, nframes, streams):
     """LDB high-efficiency (speed 0: telescope + exact sub-pel ME, tb / pb split,
-    4 references, delta-qp RD search) and 4K LDB-low / medium."""
+    4 references, delta-qp RD search; CIF at -qp 22 and 1080p at the config's
+    qp 32) and 4K LDB-low / medium."""
     from thor_amd.encoder import GpuEncoder, params_for
 
     meta = streams[name]
@@ -101,5 +101,22 @@ def test_device_encoder_more_configs(name, nframes, streams):
         for i in range(enc.num_frames()):
             got = enc.encode_next()
             assert got == want[i], (name, i, len(got), len(want[i]))
+    finally:
+        enc.close()
+
+
+def test_encoder_reset_recodes_the_sequence(streams):
+    """thor_enc_reset: the context codes its sequence again, same .bit."""
+    from thor_amd.encoder import GpuEncoder, params_for
+
+    meta = streams["cif_low"]
+    want = _frames(open("tests/golden/cif_low.bit", "rb").read())
+    enc = GpuEncoder(params_for(meta["config"], meta["width"], meta["height"], 4, meta["extra"]))
+    try:
+        enc.upload_sequence(_input(meta, 4))
+        first = [enc.encode_next() for _ in range(3)]
+        enc.reset()
+        again = [enc.encode_next() for _ in range(4)]
+        assert first == want[:3] and again == want[:4]
     finally:
         enc.close()

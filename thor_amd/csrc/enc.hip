@@ -20,7 +20,7 @@
 #include "enc_gop.h"
 #include "enc_rd.h"
 
-#define THOR_ENC_MAX_BATCH 16
+#define THOR_ENC_MAX_BATCH 64
 #define THOR_ENC_SB_WORDS 4096  // 131072 bits of one SB's stream (trial writes included)
 
 __global__ void k_deblock_v(const FrameBatch, int, int);
@@ -558,6 +558,19 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   return THOR_OK;
 }
 
+int thor_enc_reset(thor_enc_t *e) {
+  if (!e) return THOR_ERR_ARG;
+  EHIP(hipSetDevice(e->device));
+  EHIP(hipStreamSynchronize(e->stream));
+  e->pos = 0;
+  e->first = true;
+  e->last_slot = -1;
+  e->last_frame_num = -1;
+  e->slot_of_window.assign(33, -1);
+  e->chunk.clear();
+  return THOR_OK;
+}
+
 int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride) {
   return thor_enc_frames(&e, 1, &orig, &orig_stride);
 }
@@ -584,6 +597,17 @@ int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v) {
 }
 
 }  // extern "C"
+
+#if defined(THOR_ENC_TRACE)
+// debug builds only (tools/enc_trace.py): record the RD decision trace of frame
+// `frame` into dev_buf (int [8 + 8 * cap], dev_buf[0] = record count)
+extern "C" int thor_enc_trace_buffer(void *dev_buf, unsigned cap, int frame) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(te_trace_buf), &dev_buf, sizeof(void *)) != hipSuccess) return THOR_ERR_HIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(te_trace_cap), &cap, sizeof(cap)) != hipSuccess) return THOR_ERR_HIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(te_trace_frame), &frame, sizeof(frame)) != hipSuccess) return THOR_ERR_HIP;
+  return THOR_OK;
+}
+#endif
 
 #if defined(THOR_ENC_PROFILE)
 extern "C" int thor_enc_profile_buffer(void *dev_buf) {

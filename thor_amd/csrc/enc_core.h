@@ -103,6 +103,43 @@ struct TeProf {
 #else
 #define TE_P(c)
 #endif
+// Optional decision trace (built only with -DTHOR_ENC_TRACE: tools/enc_trace.py
+// on the device, tools/enc_host on the host): 8 ints per record -- frame,
+// kind, ypos, xpos, a, b, c, d -- for the frame number te_trace_frame, so the
+// RD decisions of the device and host builds can be compared record by record
+// (per superblock; WPP interleaves superblocks on the device).
+#if defined(THOR_ENC_TRACE)
+#if defined(TE_HOST)
+static int *te_trace_buf;  // [0]: record count, records from [8]
+static unsigned te_trace_cap;
+static int te_trace_frame = -1;
+static inline void te_trace_put(int fr, int k, int y, int x, int a, int b, int c, int d) {
+  if (!te_trace_buf || fr != te_trace_frame) return;
+  const unsigned i = (unsigned)te_trace_buf[0]++;
+  if (i >= te_trace_cap) return;
+  int *r = te_trace_buf + 8 + 8 * (size_t)i;
+  r[0] = fr, r[1] = k, r[2] = y, r[3] = x, r[4] = a, r[5] = b, r[6] = c, r[7] = d;
+}
+#else
+__device__ int *te_trace_buf;
+__device__ unsigned te_trace_cap;
+__device__ int te_trace_frame;
+__device__ __forceinline__ void te_trace_put(int fr, int k, int y, int x, int a, int b, int c, int d) {
+  if (!te_trace_buf || fr != te_trace_frame) return;
+  if (threadIdx.x == 0) {
+    const unsigned i = atomicAdd((unsigned *)te_trace_buf, 1u);
+    if (i < te_trace_cap) {
+      int *r = te_trace_buf + 8 + 8 * (size_t)i;
+      r[0] = fr, r[1] = k, r[2] = y, r[3] = x, r[4] = a, r[5] = b, r[6] = c, r[7] = d;
+    }
+  }
+}
+#endif
+#define TE_TR(fr, k, y, x, a, b, c, d) te_trace_put(fr, k, y, x, (int)(a), (int)(b), (int)(c), (int)(d))
+#else
+#define TE_TR(fr, k, y, x, a, b, c, d)
+#endif
+
 enum { TP_WCOEF, TP_WBLOCK, TP_INTER_COMP, TP_INTRA_COMP, TP_ENC_BLOCK, TP_COST, TP_SEARCH_INTRA, TP_ME, TP_MODE,
        TP_ES_CHECK, TP_ES_SEARCH, TP_COMMIT, TP_MC_Y, TP_MC_C, TP_FWD, TP_QUANT, TP_INV, TP_IPRED, TP_TOPLEFT, TP_SAD,
        TP_SB, TP_WAIT, TP_N };

@@ -296,6 +296,8 @@ TE_NOINL int te_encode_block(const TeFrame &F, TeScratch S, TeBits &b, TeBlockIn
   p.cbp_u = cu;
   p.cbp_v = cv;
   const int nbits = te_write_block(b, F, bi, p, S.tx->scan);
+  TE_TR(F.frame_num, 2, bi.ypos, bi.xpos, bi.size | p.mode << 8 | (p.tb_param + 1) << 12 | p.skip_idx << 16,
+        p.ref_idx0 | p.ref_idx1 << 4 | p.pb_part << 8 | p.intra_mode << 12, nbits, cy | cu << 1 | cv << 2);
   if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
   return nbits;
 }
@@ -311,6 +313,7 @@ TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *r
   const double prod = F.lambda * (double)nbits;
   uint32_t cost = sy + su + sv + (uint32_t)(int32_t)(prod + 0.5);
   if (cost > (1u << 30)) cost = 1u << 30;
+  TE_TR(F.frame_num, 3, ypos, xpos, size, sy, su + sv, cost);
   return cost;
 }
 
@@ -424,6 +427,8 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, in
     end -= (end >= 6) * 6;
     if (best_dir < 0) break;
   }
+  TE_TR(F.frame_num, 9, ypos, xpos, size | width << 8 | height << 16, r, min_sad,
+        (mv_ref.x & 0xffff) | (int)mv_ref.y << 16);
   int ydelta_hp = 0, xdelta_hp = 0, ydelta_qp = 0, xdelta_qp = 0;
   uint32_t cmin = min_sad;
   if (F.speed == 0) {  // exact half- and quarter-pel search through the MC filters
@@ -483,6 +488,8 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, in
   mv_opt.x = (int16_t)(mv_opt.x + xdelta_qp);
   mv_opt.y = (int16_t)(mv_opt.y + ydelta_qp);
   *mv = mv_opt;
+  TE_TR(F.frame_num, 1, ypos, xpos, size | width << 8 | height << 16, r | sb.mc.num[r] << 8, TE_MIN(cmin, min_sad),
+        (mv_opt.x & 0xffff) | (int)mv_opt.y << 16);
   return TE_MIN(cmin, min_sad);
 }
 
@@ -636,6 +643,37 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
         S.org8[e] = (uint8_t)te_clip255(2 * (int)org[y * F.osy + x] - (int)S.pb[e]);
       }
       te_sync();
+#if defined(THOR_ENC_TRACE)
+      {
+        uint32_t sp = 0, so = 0, sc = 0;
+        for (int e = TE_LANE; e < size * size; e += TE_NL) {
+          sp += S.pb[e] * (e + 1);
+          so += S.org8[e] * (e + 1);
+        }
+        for (int e = TE_LANE; e < size * size / 2; e += TE_NL) sc += S.pb[size * size + e] * (e + 1);
+        TE_TR(F.frame_num, 7, bi.ypos, bi.xpos, ref_idx | list << 4, te_sum(sp), te_sum(so),
+              (m0[0].x & 0xffff) | (int)m0[0].y << 16);
+        TE_TR(F.frame_num, 8, bi.ypos, bi.xpos, (m0[1].x & 0xffff) | (int)m0[1].y << 16,
+              (m0[2].x & 0xffff) | (int)m0[2].y << 16, (m0[3].x & 0xffff) | (int)m0[3].y << 16, te_sum(sc));
+        if (size == 8)
+          for (int q = 0; q < 64; q += 16) {
+            int w[4];
+            for (int k = 0; k < 4; k++)
+              w[k] = S.pb[q + 4 * k] | S.pb[q + 4 * k + 1] << 8 | S.pb[q + 4 * k + 2] << 16 | S.pb[q + 4 * k + 3] << 24;
+            TE_TR(F.frame_num, 10, bi.ypos, bi.xpos, w[0], w[1], w[2], w[3]);
+          }
+        {
+          const uint8_t *rp = F.refy[ref_idx] + bi.ypos * F.rsy + bi.xpos - 8;
+          for (int q = 0; q < 2; q++) {
+            int w[4];
+            for (int k = 0; k < 4; k++)
+              w[k] = rp[q * F.rsy + 4 * k] | rp[q * F.rsy + 4 * k + 1] << 8 | rp[q * F.rsy + 4 * k + 2] << 16 |
+                     rp[q * F.rsy + 4 * k + 3] << 24;
+            TE_TR(F.frame_num, 11, bi.ypos, bi.xpos, w[0], w[1], w[2], w[3]);
+          }
+        }
+      }
+#endif
       int ref_start, ref_end;
       if (F.frame_type == TE_P) {
         ref_start = 0;
@@ -665,6 +703,8 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
       }
     }
   }
+  TE_TR(F.frame_num, 4, bi.ypos, bi.xpos, size, min_ref_idx0 | min_ref_idx1 << 4, min_sad,
+        (m0[0].x & 0xffff) | (int)m1[0].x << 16);
   *ref_idx0 = min_ref_idx0;
   *ref_idx1 = min_ref_idx1;
   for (int i = 0; i < 4; i++) {
@@ -844,6 +884,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
     }
   }
   te_rewind(b, pos_ref);  // rewind (:2476)
+  TE_TR(F.frame_num, 5, ypos, xpos, size, min_cost, bi.bp.mode, sad_intra);
   return min_cost;
 }
 
@@ -1092,6 +1133,7 @@ TE_FN void te_encode_sb(const TeFrame &F, TeScratch S, TeSB &sb, int k, int l) {
     int min_cost = 1 << 30, best_qp = F.qp;
     for (int q = F.qp - F.max_delta_qp; q <= F.qp + F.max_delta_qp; q += F.delta_qp_step) {
       const int cost = (int)te_process_block<64>(F, S, sb, ypos, xpos, q);
+      TE_TR(F.frame_num, 6, ypos, xpos, q, cost, 0, 0);
       if (cost < min_cost) {
         min_cost = cost;
         best_qp = q;

@@ -86,13 +86,26 @@ class GpuDecoder:
         except Exception:
             pass
 
-    def _buf(self, arr: np.ndarray) -> DeviceBuffer:
+    def _buf(self, arr: np.ndarray, pool=None, key=None) -> DeviceBuffer:
+        if pool is not None:  # re-use the buffer `key` of `pool` when it is big enough
+            b = pool.get(key)
+            if b is None or b.nbytes < arr.nbytes:
+                if b is not None:
+                    b.free()
+                    self._bufs.remove(b)
+                b = DeviceBuffer(self.lib, arr.nbytes + (arr.nbytes >> 2))
+                self._bufs.append(b)
+                pool[key] = b
+            b.upload(arr)
+            return b
         b = DeviceBuffer(self.lib, arr.nbytes)
         b.upload(arr)
         self._bufs.append(b)
         return b
 
-    def upload(self, fr) -> DeviceFrame:
+    def upload(self, fr, pool=None) -> DeviceFrame:
+        """Upload frame `fr`'s parse output.  `pool` (a dict the caller keeps
+        per in-flight frame) re-uses that frame slot's device buffers."""
         blocks = np.ascontiguousarray(fr.blocks, dtype=BLOCK_DTYPE)
         coeffs = np.ascontiguousarray(fr.coeffs, dtype=np.int16)
         flags = np.ascontiguousarray(fr.clpf_flags, dtype=np.uint8)
@@ -106,8 +119,8 @@ class GpuDecoder:
         clist = np.zeros(max(n_clpf, 1), np.uint32)
         if flags.size:
             self.lib.thor_build_clpf_list(flags.ctypes.data, len(flags), clist.ctypes.data)
-        bb, cb, fb, ib = self._buf(blocks), self._buf(coeffs), self._buf(flags), self._buf(ilist)
-        tb, lb = self._buf(tlist), self._buf(clist)
+        bb, cb, fb = self._buf(blocks, pool, 0), self._buf(coeffs, pool, 1), self._buf(flags, pool, 2)
+        ib, tb, lb = self._buf(ilist, pool, 3), self._buf(tlist, pool, 4), self._buf(clist, pool, 5)
         hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
         nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + TU_DTYPE.itemsize * n_tu
         return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, tb.ptr,

@@ -73,6 +73,10 @@ class GpuEncoder:
             raise MemoryError("thor_dev_alloc")
         L.check(self.lib.thor_h2d(self.seq_dev, a.ctypes.data, a.nbytes), "thor_h2d")
 
+    def reset(self):
+        """Start the sequence again (thor_enc_reset): same input, same .bit."""
+        L.check(self.lib.thor_enc_reset(self.h), "thor_enc_reset")
+
     def num_frames(self) -> int:
         return self.lib.thor_enc_num_frames(self.h)
 

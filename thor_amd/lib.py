@@ -55,7 +55,7 @@ BATCHED_SYMBOLS = [
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_frames", "thor_enc_frame", "thor_enc_frame_bytes",
-    "thor_enc_read_recon",
+    "thor_enc_read_recon", "thor_enc_reset",
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
@@ -136,6 +136,8 @@ def load(path: str = LIB_PATH):
     L.thor_enc_num_frames.restype = i
     L.thor_enc_next_input.argtypes = [P]
     L.thor_enc_next_input.restype = i
+    L.thor_enc_reset.argtypes = [P]
+    L.thor_enc_reset.restype = i
     L.thor_enc_stream.argtypes = [P]
     L.thor_enc_stream.restype = P
     L.thor_enc_frames.argtypes = [P, i, P, P]

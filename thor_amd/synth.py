@@ -44,17 +44,16 @@ def _value_noise(X: np.ndarray, Y: np.ndarray, cell_log2: int, seed: int) -> np.
     x0, y0 = int(cx.min()), int(cy.min())
     gx = np.arange(x0, int(cx.max()) + 2, dtype=np.int64)
     gy = np.arange(y0, int(cy.max()) + 2, dtype=np.int64)
-    lat = (_hash2(gx[None, :] & 0xFFFFFFFF, gy[:, None] & 0xFFFFFFFF, seed) >> np.uint32(24)).astype(np.int64) - 128
-    ix = (cx - x0)[None, :]
-    iy = (cy - y0)[:, None]
-    v00 = lat[iy, ix]
-    v10 = lat[iy, ix + 1]
-    v01 = lat[iy + 1, ix]
-    v11 = lat[iy + 1, ix + 1]
-    fxr = fx[None, :]
-    fyr = fy[:, None]
-    v = (v00 * (256 - fxr) * (256 - fyr) + v10 * fxr * (256 - fyr) + v01 * (256 - fxr) * fyr + v11 * fxr * fyr) >> 16
-    return v
+    lat = (_hash2(gx[None, :] & 0xFFFFFFFF, gy[:, None] & 0xFFFFFFFF, seed) >> np.uint32(24)).astype(np.int32) - 128
+    ix = cx - x0
+    iy = cy - y0
+    # separable evaluation of the same exact sum (|value| < 2^23, int32 is exact):
+    # lattice rows interpolated horizontally first, then the row pairs vertically
+    fx32 = fx.astype(np.int32)[None, :]
+    hrow = lat[:, ix] * (256 - fx32) + lat[:, ix + 1] * fx32
+    fy32 = fy.astype(np.int32)[:, None]
+    v = (hrow[iy] * (256 - fy32) + hrow[iy + 1] * fy32) >> 16
+    return v.astype(np.int64)
 
 
 def _texture(X, Y, seed, octaves):
@@ -96,9 +95,12 @@ def _plane(width, height, t, seed, sub, octaves, noise_taps, noise_span, base):
         iny = (ly >= 0) & (ly < _OBJ_H * 256)
         if not inx.any() or not iny.any():
             continue
-        tex = base + 16 * (o - 1) + _texture(lx + (1 << 20), ly + (1 << 20), seed + 101 * (o + 1), octaves)
-        mask = iny[:, None] & inx[None, :]
-        img = np.where(mask, tex, img)
+        # the object covers a rectangle: texture only that window
+        c = np.flatnonzero(inx)
+        r = np.flatnonzero(iny)
+        c0, c1, r0, r1 = c[0], c[-1] + 1, r[0], r[-1] + 1
+        img[r0:r1, c0:c1] = base + 16 * (o - 1) + _texture(lx[c0:c1] + (1 << 20), ly[r0:r1] + (1 << 20),
+                                                           seed + 101 * (o + 1), octaves)
     img = img + _temporal_noise(img.shape, seed, t, noise_taps, noise_span)
     return np.clip(img, 0, 255).astype(np.uint8)
 
@@ -109,6 +111,22 @@ def synth_frame(width: int, height: int, t: int, seed: int = 1):
     u = _plane(width // 2, height // 2, t, seed + 1000, 2, _CHROMA_OCT, 2, 1, 120)
     v = _plane(width // 2, height // 2, t, seed + 2000, 2, _CHROMA_OCT, 2, 1, 136)
     return y, u, v
+
+
+def _i420(args):
+    return np.concatenate([p.reshape(-1) for p in synth_frame(*args)])
+
+
+def synth_frames(width: int, height: int, frames: int, seed: int = 1, workers: int = 8) -> np.ndarray:
+    """(frames, W*H*3/2) uint8 I420 array, frames generated in parallel
+    processes (fork: call before the process initialises a GPU)."""
+    args = [(width, height, t, seed) for t in range(frames)]
+    if workers <= 1 or frames <= 1:
+        return np.stack([_i420(a) for a in args])
+    import multiprocessing as mp
+
+    with mp.get_context("fork").Pool(min(workers, frames)) as pool:
+        return np.stack(pool.map(_i420, args))
 
 
 def synth_clip(width: int, height: int, frames: int, seed: int = 1) -> bytes:

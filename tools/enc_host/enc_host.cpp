@@ -36,12 +36,18 @@ int main(int argc, char **argv) {
   thor_enc_params_t P;
   te_default_params(&P);
   const char *in = nullptr, *out = nullptr, *recf = nullptr;
+  const char *trace_out = nullptr;
+  (void)trace_out;
   int verbose = 0;
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "-if")) in = argv[i + 1];
     else if (!strcmp(argv[i], "-of")) out = argv[i + 1];
     else if (!strcmp(argv[i], "-rf")) recf = argv[i + 1];
     else if (!strcmp(argv[i], "-v")) verbose = atoi(argv[i + 1]);
+#if defined(THOR_ENC_TRACE)
+    else if (!strcmp(argv[i], "-trace_frame")) te_trace_frame = atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "-trace_out")) trace_out = argv[i + 1];
+#endif
     else if (te_set_param(&P, argv[i], argv[i + 1])) {
       fprintf(stderr, "unknown parameter %s\n", argv[i]);
       return 2;
@@ -52,6 +58,12 @@ int main(int argc, char **argv) {
     return 2;
   }
   const int W = P.width, H = P.height;
+#if defined(THOR_ENC_TRACE)
+  if (trace_out) {
+    te_trace_cap = 1u << 24;
+    te_trace_buf = (int *)calloc(8 + 8 * (size_t)te_trace_cap, sizeof(int));
+  }
+#endif
   FILE *fi = fopen(in, "rb"), *fo = fopen(out, "wb"), *fr = recf ? fopen(recf, "wb") : nullptr;
   if (!fi || !fo) return 3;
   const size_t fsz = (size_t)W * H * 3 / 2;
@@ -178,6 +190,14 @@ int main(int argc, char **argv) {
     tmp->f.frame_num = pl.frame_num;
     or_pad_frame(&tmp->f, W, H, 96, 48);
   }
+#if defined(THOR_ENC_TRACE)
+  if (trace_out && te_trace_buf) {
+    FILE *ft = fopen(trace_out, "wb");
+    const unsigned n = (unsigned)te_trace_buf[0] < te_trace_cap ? (unsigned)te_trace_buf[0] : te_trace_cap;
+    fwrite(te_trace_buf + 8, 32, n, ft);
+    fclose(ft);
+  }
+#endif
   fclose(fi);
   fclose(fo);
   if (fr) fclose(fr);

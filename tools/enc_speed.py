@@ -8,7 +8,6 @@ import os
 import sys
 import time
 
-import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -25,7 +24,7 @@ def main():
     meta = json.load(open(os.path.join(ROOT, "tests", "golden", "streams.json")))[a.name]
     n = a.frames or meta["frames"]
     w, h = meta["width"], meta["height"]
-    frames = np.stack([np.concatenate([p.reshape(-1) for p in synth.synth_frame(w, h, t, meta["seed"])]) for t in range(n)])
+    frames = synth.synth_frames(w, h, n, meta["seed"], workers=8)  # before any GPU call (fork)
     want = open(os.path.join(ROOT, "tests", "golden", a.name + ".bit"), "rb").read()
     res = {}
     for B in a.batch:
