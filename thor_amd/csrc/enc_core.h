@@ -19,8 +19,8 @@
 #include <stdint.h>
 #include <string.h>
 
-#if defined(TE_HOST)
 #include <stdlib.h>
+#if defined(TE_HOST)
 #define TE_FN static inline
 #define TE_NOINL static
 #define TE_LANE 0
@@ -84,6 +84,64 @@ TE_FN int te_dv(int e, int w) {
 #endif
 }
 
+// ---- 4-pixel (dword) helpers ----------------------------------------------------
+// Pixel loops that can take four horizontally adjacent pixels per lane do so:
+// one (possibly unaligned) dword load / store instead of four byte accesses,
+// and the byte-SIMD ALU ops of CDNA (v_sad_u8, v_dot4_u32_u8).  The host build
+// computes the same values byte by byte.
+typedef uint32_t __attribute__((aligned(1))) te_u32u;
+#if !defined(TE_HOST)
+TE_FN uint32_t te_ld4(const uint8_t *p) { return *(const te_u32u *)p; }
+TE_FN void te_st4(uint8_t *p, uint32_t v) { *(te_u32u *)p = v; }
+#else
+TE_FN uint32_t te_ld4(const uint8_t *p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+TE_FN void te_st4(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+#endif
+TE_FN int te_b(uint32_t v, int k) { return (int)((v >> (8 * k)) & 255u); }
+// sum |a_k - b_k| + acc
+TE_FN uint32_t te_sad4(uint32_t a, uint32_t b, uint32_t acc) {
+#if !defined(TE_HOST)
+  return __builtin_amdgcn_sad_u8(a, b, acc);
+#else
+  for (int k = 0; k < 4; k++) acc += (uint32_t)abs(te_b(a, k) - te_b(b, k));
+  return acc;
+#endif
+}
+// sum a_k * b_k + acc (unsigned bytes)
+TE_FN uint32_t te_dot4(uint32_t a, uint32_t b, uint32_t acc) {
+#if !defined(TE_HOST)
+  return __builtin_amdgcn_udot4(a, b, acc, false);
+#else
+  for (int k = 0; k < 4; k++) acc += (uint32_t)(te_b(a, k) * te_b(b, k));
+  return acc;
+#endif
+}
+// bytes (lo | hi << 32) >> (8 * s), s in 0..3
+TE_FN uint32_t te_align4(uint32_t hi, uint32_t lo, int s) {
+#if !defined(TE_HOST)
+  return __builtin_amdgcn_alignbyte(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * s));
+#endif
+}
+// per byte: (a + b) >> 1 (truncating) and (a + b + 1) >> 1 (rounding), exact
+TE_FN uint32_t te_avg4(uint32_t a, uint32_t b) { return (a & b) + (((a ^ b) >> 1) & 0x7f7f7f7fu); }
+TE_FN uint32_t te_ravg4(uint32_t a, uint32_t b) { return (a | b) - (((a ^ b) >> 1) & 0x7f7f7f7fu); }
+// four values in 0..255 -> bytes.  The empty asm keeps the compiler from
+// fusing a clamp-and-pack into gfx950's v_ashr_pk_u8_i32, whose result this
+// hipcc (ROCm 7.2) ORs with the stale upper half of the destination register
+// (byte 2 of the packed word comes out corrupted; tools/probes/pix_check.hip).
+TE_FN uint32_t te_pack4(int a, int b, int c, int d) {
+#if !defined(TE_HOST)
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+#endif
+  return (uint32_t)a | (uint32_t)b << 8 | (uint32_t)c << 16 | (uint32_t)d << 24;
+}
+
 // Optional per-function cycle accounting (built only with -DTHOR_ENC_PROFILE,
 // tools/enc_profile.py): s_memtime deltas and call counts per category.
 #if defined(THOR_ENC_PROFILE) && !defined(TE_HOST)
@@ -126,7 +184,7 @@ __device__ unsigned te_trace_cap;
 __device__ int te_trace_frame;
 __device__ __forceinline__ void te_trace_put(int fr, int k, int y, int x, int a, int b, int c, int d) {
   if (!te_trace_buf || fr != te_trace_frame) return;
-  if (threadIdx.x == 0) {
+  if ((int)threadIdx.x == __builtin_ctzll(__builtin_amdgcn_read_exec())) {  // first active lane
     const unsigned i = atomicAdd((unsigned *)te_trace_buf, 1u);
     if (i < te_trace_cap) {
       int *r = te_trace_buf + 8 + 8 * (size_t)i;

@@ -43,6 +43,70 @@ TE_FN void te_mc_luma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, i
   const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
   const int fy = my & 3, fx = mx & 3;
   const uint8_t *r = ref + (my >> 2) * rs + (mx >> 2);
+  if ((w & 3) == 0) {  // four outputs per lane: dword loads, taps from registers
+    const int w4 = w >> 2, n4 = w4 * h;
+    if (!fx && !fy) {
+      for (int g = TE_LANE; g < n4; g += TE_NL) {
+        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+        te_st4(dst + i * ds + j, te_ld4(r + i * rs + j));
+      }
+    } else if (fx == 2 && fy == 2) {  // rows -1..2, columns -1..6
+      for (int g = TE_LANE; g < n4; g += TE_NL) {
+        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+        const uint8_t *p = r + (i - 1) * rs + j - 1;
+        int c[4][8];
+        for (int t = 0; t < 4; t++) {
+          const uint32_t lo = te_ld4(p + t * rs), hi = te_ld4(p + t * rs + 4);
+          for (int k = 0; k < 4; k++) {
+            c[t][k] = te_b(lo, k);
+            c[t][k + 4] = te_b(hi, k);
+          }
+        }
+        int o[4];
+        for (int x = 0; x < 4; x++) {  // c[dy + 1][dx + 1]
+          const int k = x + 1;
+          const int v = c[0][k] + c[0][k + 1] + c[1][k - 1] + 2 * c[1][k] + 2 * c[1][k + 1] + c[1][k + 2] + c[2][k - 1] +
+                        2 * c[2][k] + 2 * c[2][k + 1] + c[2][k + 2] + c[3][k] + c[3][k + 1];
+          o[x] = te_clip255((v + 8) >> 4);
+        }
+        te_st4(dst + i * ds + j, te_pack4(o[0], o[1], o[2], o[3]));
+      }
+    } else {
+      const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
+      const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
+      const int k0 = fy ? 0 : 2, k1 = fy ? 6 : 3;  // fy == 0: the vertical taps are (0, 0, 64, 0, 0, 0)
+      for (int g = TE_LANE; g < n4; g += TE_NL) {
+        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+        int s[4] = {0, 0, 0, 0};
+        for (int k = k0; k < k1; k++) {
+          const uint8_t *p = r + (i - 2 + k) * rs + j - 2;
+          int hk[4];
+          if (fx) {  // columns -2..9 of the row, 6 taps
+            const uint32_t d0 = te_ld4(p), d1 = te_ld4(p + 4), d2 = te_ld4(p + 8);
+            int c[12];
+            for (int b = 0; b < 4; b++) {
+              c[b] = te_b(d0, b);
+              c[b + 4] = te_b(d1, b);
+              c[b + 8] = te_b(d2, b);
+            }
+            for (int x = 0; x < 4; x++) {
+              int t = 0;
+              for (int m = 0; m < 6; m++) t += fh[m] * c[x + m];
+              hk[x] = t;
+            }
+          } else {  // horizontal taps (0, 0, 64, 0, 0, 0)
+            const uint32_t d = te_ld4(p + 2);
+            for (int x = 0; x < 4; x++) hk[x] = 64 * te_b(d, x);
+          }
+          for (int x = 0; x < 4; x++) s[x] += fv[k] * hk[x];
+        }
+        te_st4(dst + i * ds + j, te_pack4(te_clip255((s[0] + 2048) >> 12), te_clip255((s[1] + 2048) >> 12),
+                                          te_clip255((s[2] + 2048) >> 12), te_clip255((s[3] + 2048) >> 12)));
+      }
+    }
+    te_sync();
+    return;
+  }
   const int n = w * h;
   if (!fx && !fy) {
     for (int e = TE_LANE; e < n; e += TE_NL) {
@@ -82,6 +146,39 @@ TE_FN void te_mc_chroma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w,
   const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
   const int fy = my & 7, fx = mx & 7;
   const uint8_t *r = ref + (my >> 3) * rs + (mx >> 3);
+  if ((w & 3) == 0) {  // four outputs per lane
+    const int w4 = w >> 2, n4 = w4 * h;
+    if (!fx && !fy) {
+      for (int g = TE_LANE; g < n4; g += TE_NL) {
+        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+        te_st4(dst + i * ds + j, te_ld4(r + i * rs + j));
+      }
+    } else {
+      const int8_t *fh = te_chroma_f[fx], *fv = te_chroma_f[fy];
+      for (int g = TE_LANE; g < n4; g += TE_NL) {
+        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+        int s[4] = {0, 0, 0, 0};
+        for (int m = 0; m < 4; m++) {  // rows -1..2, columns -1..6
+          const uint8_t *p = r + (i - 1 + m) * rs + j - 1;
+          const uint32_t lo = te_ld4(p), hi = te_ld4(p + 4);
+          int c[8];
+          for (int b = 0; b < 4; b++) {
+            c[b] = te_b(lo, b);
+            c[b + 4] = te_b(hi, b);
+          }
+          for (int x = 0; x < 4; x++) {
+            int t = 0;
+            for (int k = 0; k < 4; k++) t += fh[k] * c[x + k];
+            s[x] += fv[m] * t;
+          }
+        }
+        te_st4(dst + i * ds + j, te_pack4(te_clip255((s[0] + 2048) >> 12), te_clip255((s[1] + 2048) >> 12),
+                                          te_clip255((s[2] + 2048) >> 12), te_clip255((s[3] + 2048) >> 12)));
+      }
+    }
+    te_sync();
+    return;
+  }
   const int n = w * h;
   if (!fx && !fy) {
     for (int e = TE_LANE; e < n; e += TE_NL) {
@@ -109,6 +206,14 @@ TE_FN void te_mc_chroma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w,
 TE_FN uint32_t te_sad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
   TE_P(TP_SAD);
   uint32_t s = 0;
+  if ((w & 3) == 0) {
+    const int w4 = w >> 2, n4 = w4 * h;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      s = te_sad4(te_ld4(a + i * as + j), te_ld4(b + i * bs + j), s);
+    }
+    return te_sum(s);
+  }
   for (int e = TE_LANE; e < w * h; e += TE_NL) {
     const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
     s += (uint32_t)te_abs((int)a[i * as + j] - (int)b[i * bs + j]);
@@ -117,6 +222,17 @@ TE_FN uint32_t te_sad(const uint8_t *a, int as, const uint8_t *b, int bs, int w,
 }
 TE_FN uint32_t te_ssd(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
   uint32_t s = 0;
+  if ((w & 3) == 0) {  // sum (a - b)^2 = sum a^2 + sum b^2 - 2 sum ab, exact modulo 2^32
+    const int w4 = w >> 2, n4 = w4 * h;
+    uint32_t ab = 0;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      const uint32_t x = te_ld4(a + i * as + j), y = te_ld4(b + i * bs + j);
+      s = te_dot4(y, y, te_dot4(x, x, s));
+      ab = te_dot4(x, y, ab);
+    }
+    return te_sum(s - 2u * ab);
+  }
   for (int e = TE_LANE; e < w * h; e += TE_NL) {
     const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
     const int d = (int)a[i * as + j] - (int)b[i * bs + j];
@@ -131,6 +247,20 @@ TE_FN uint32_t te_ssd(const uint8_t *a, int as, const uint8_t *b, int bs, int w,
 TE_FN uint32_t te_widesad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h, int *x) {
   const int off[5] = {-3, -1, 0, 1, 3};
   uint32_t s[5] = {0, 0, 0, 0, 0};
+  if ((w & 3) == 0) {  // b columns j-4..j+7 as three dwords, the five offsets by byte alignment
+    const int w4 = w >> 2, n4 = w4 * h;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      const uint32_t av = te_ld4(a + i * as + j);
+      const uint8_t *q = b + i * bs + j;
+      const uint32_t d0 = te_ld4(q - 4), d1 = te_ld4(q), d2 = te_ld4(q + 4);
+      s[0] = te_sad4(av, te_align4(d1, d0, 1), s[0]);
+      s[1] = te_sad4(av, te_align4(d1, d0, 3), s[1]);
+      s[2] = te_sad4(av, d1, s[2]);
+      s[3] = te_sad4(av, te_align4(d2, d1, 1), s[3]);
+      s[4] = te_sad4(av, te_align4(d2, d1, 3), s[4]);
+    }
+  } else
   for (int e = TE_LANE; e < w * h; e += TE_NL) {
     const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
     const int av = a[i * as + j];

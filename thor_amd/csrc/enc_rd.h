@@ -52,7 +52,68 @@ TE_FN uint8_t *te_pu(uint8_t *b, int size) { return b + size * size; }
 TE_FN uint8_t *te_pv(uint8_t *b, int size) { return b + size * size + (size / 2) * (size / 2); }
 
 TE_FN void te_copy_bytes(uint8_t *d, const uint8_t *s, int n) {
-  for (int e = TE_LANE; e < n; e += TE_NL) d[e] = s[e];
+  if ((n & 3) == 0)
+    for (int e = 4 * TE_LANE; e < n; e += 4 * TE_NL) te_st4(d + e, te_ld4(s + e));
+  else
+    for (int e = TE_LANE; e < n; e += TE_NL) d[e] = s[e];
+  te_sync();
+}
+// d[y * ds + x] = (a[y * as + x] + b[y * bs + x]) >> 1 over a w x h block
+TE_FN void te_avg_rect(uint8_t *d, int ds, const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h) {
+  if ((w & 3) == 0) {
+    const int w4 = w >> 2, n4 = w4 * h;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      te_st4(d + i * ds + j, te_avg4(te_ld4(a + i * as + j), te_ld4(b + i * bs + j)));
+    }
+  } else {
+    for (int e = TE_LANE; e < w * h; e += TE_NL) {
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
+      d[i * ds + j] = (uint8_t)(((int)a[i * as + j] + (int)b[i * bs + j]) >> 1);
+    }
+  }
+}
+// d[y * ds + x] = s[y * ss + x] over a w x h block
+TE_FN void te_copy_rect(uint8_t *d, int ds, const uint8_t *s, int ss, int w, int h) {
+  if ((w & 3) == 0) {
+    const int w4 = w >> 2, n4 = w4 * h;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      te_st4(d + i * ds + j, te_ld4(s + i * ss + j));
+    }
+  } else {
+    for (int e = TE_LANE; e < w * h; e += TE_NL) {
+      const int i = te_dv(e, w), j = e - te_dv(e, w) * w;
+      d[i * ds + j] = s[i * ss + j];
+    }
+  }
+}
+// four int16 at an 8-byte aligned address
+TE_FN void te_st4x16(int16_t *p, int a, int b, int c, int d) {
+  const uint32_t lo = ((uint32_t)a & 0xffffu) | (uint32_t)b << 16, hi = ((uint32_t)c & 0xffffu) | (uint32_t)d << 16;
+#if !defined(TE_HOST)
+  *(uint2 *)p = make_uint2(lo, hi);
+#else
+  memcpy(p, &lo, 4);
+  memcpy(p + 2, &hi, 4);
+#endif
+}
+// R[y * n + x] = o[y * os + x] - p[y * ps + x] (n x n, int16)
+TE_FN void te_residual(int16_t *R, const uint8_t *o, int os, const uint8_t *p, int ps, int n) {
+  if ((n & 3) == 0) {
+    const int w4 = n >> 2, n4 = w4 * n;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      const uint32_t a = te_ld4(o + i * os + j), b = te_ld4(p + i * ps + j);
+      te_st4x16(R + i * n + j, te_b(a, 0) - te_b(b, 0), te_b(a, 1) - te_b(b, 1), te_b(a, 2) - te_b(b, 2),
+                te_b(a, 3) - te_b(b, 3));
+    }
+  } else {
+    for (int e = TE_LANE; e < n * n; e += TE_NL) {
+      const int y = te_dv(e, n), x = e - te_dv(e, n) * n;
+      R[e] = (int16_t)((int)o[y * os + x] - (int)p[y * ps + x]);
+    }
+  }
   te_sync();
 }
 
@@ -77,11 +138,23 @@ TE_FN void te_pred_yuv(const TeFrame &F, int r, uint8_t *pb, const TeBlockInfo &
                        int split) {
   const int div = split + 1, bw = bi.bwidth / div, bh = bi.bheight / div, size = bi.size;
   const int ypos = bi.ypos, xpos = bi.xpos;
+#if defined(THOR_ENC_TRACE) && !defined(TE_HOST)
+  if (size == 8 && split) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    TE_TR(F.frame_num, 13, ypos, xpos, (uint32_t)ex, (uint32_t)(ex >> 32), r, 0);
+  }
+#endif
   for (int index = 0; index < div * div; index++) {
     const int idx = index & 1, idy = (index >> 1) & 1;
     const TeMv m = te_clip_mv(mv[index], ypos, xpos, F.W, F.H, size, sign);
     te_mc_luma(pb + idy * bh * size + idx * bw, size, F.refy[r] + (ypos + idy * bh) * F.rsy + xpos + idx * bw, F.rsy, bw, bh,
                m, sign, bipred);
+#if defined(THOR_ENC_TRACE)
+    if (size == 8 && split)
+      TE_TR(F.frame_num, 12, ypos, xpos, r | index << 4 | sign << 8 | bipred << 9 | bw << 12 | bh << 20,
+            (m.x & 0xffff) | (int)m.y << 16, (mv[index].x & 0xffff) | (int)mv[index].y << 16,
+            te_ld4(pb + idy * bh * size + idx * bw));
+#endif
     const int oc = idy * (bh / 2) * (size / 2) + idx * (bw / 2);
     const int orc = (ypos / 2 + idy * (bh / 2)) * F.rsc + xpos / 2 + idx * (bw / 2);
     te_mc_chroma(te_pu(pb, size) + oc, size / 2, F.refu[r] + orc, F.rsc, bw / 2, bh / 2, m, sign);
@@ -92,22 +165,38 @@ TE_FN void te_pred_yuv(const TeFrame &F, int r, uint8_t *pb, const TeBlockInfo &
 // over bwidth x bheight (chroma halves)
 TE_FN void te_avg_yuv(uint8_t *d, const uint8_t *a, const uint8_t *b, const TeBlockInfo &bi) {
   const int size = bi.size, bw = bi.bwidth, bh = bi.bheight;
-  for (int e = TE_LANE; e < bw * bh; e += TE_NL) {
-    const int i = te_dv(e, bw), j = e - te_dv(e, bw) * bw;
-    d[i * size + j] = (uint8_t)(((int)a[i * size + j] + (int)b[i * size + j]) >> 1);
-  }
+  te_avg_rect(d, size, a, size, b, size, bw, bh);
   const int cw = bw / 2, ch = bh / 2, cs = size / 2, co = size * size, cq = cs * cs;
-  for (int e = TE_LANE; e < cw * ch; e += TE_NL) {
-    const int i = te_dv(e, cw), j = e - te_dv(e, cw) * cw;
-    d[co + i * cs + j] = (uint8_t)(((int)a[co + i * cs + j] + (int)b[co + i * cs + j]) >> 1);
-    d[co + cq + i * cs + j] = (uint8_t)(((int)a[co + cq + i * cs + j] + (int)b[co + cq + i * cs + j]) >> 1);
-  }
+  te_avg_rect(d + co, cs, a + co, cs, b + co, cs, cw, ch);
+  te_avg_rect(d + co + cq, cs, a + co + cq, cs, b + co + cq, cs, cw, ch);
   te_sync();
 }
 
 TE_FN int te_sign_of(const TeFrame &F, int ref_idx, int bi) {
   // uni-pred: ref->frame_num > rec->frame_num; bi-pred legs: >= (encode_block.c:1694, :1707)
   return bi ? F.ref_fnum[ref_idx] >= F.frame_num : F.ref_fnum[ref_idx] > F.frame_num;
+}
+
+// rec[y * rs + x] = bit ? clip255(residual(y, x) + pb[y * ps + x]) : pb[..] (n x n)
+TE_FN void te_recon(uint8_t *rec, int rs, const uint8_t *pb, int ps, const TeTx &X, int n, int bit) {
+  if ((n & 3) == 0) {
+    const int w4 = n >> 2, n4 = w4 * n;
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      uint32_t v = te_ld4(pb + i * ps + j);
+      if (bit)
+        v = te_pack4(te_clip255(te_res_at(X, n, i, j) + te_b(v, 0)), te_clip255(te_res_at(X, n, i, j + 1) + te_b(v, 1)),
+                     te_clip255(te_res_at(X, n, i, j + 2) + te_b(v, 2)), te_clip255(te_res_at(X, n, i, j + 3) + te_b(v, 3)));
+      te_st4(rec + i * rs + j, v);
+    }
+  } else {
+    for (int e = TE_LANE; e < n * n; e += TE_NL) {
+      const int y = te_dv(e, n), x = e - te_dv(e, n) * n;
+      const int p = pb[y * ps + x];
+      rec[y * rs + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, n, y, x) + p) : p);
+    }
+  }
+  te_sync();
 }
 
 // ---- transform-block chains -------------------------------------------------
@@ -125,11 +214,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch S, const uint8_t *org
     // running copy of pred + residual (reconstruct_block after the loop, :1510)
     for (int t = 0; t < 4; t++) {
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
-      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
-        X.R[e] = (int16_t)((int)org[(i + y) * os + j + x] - (int)pb[(i + y) * size + j + x]);
-      }
-      te_sync();
+      te_residual(X.R, org + i * os + j, os, pb + i * size + j, size, s2);
       te_fwd_tx(X, s2, fast);
       const int bit = te_quant(X, qp, s2, type);
       const int q = TE_MIN(s2, 16);
@@ -138,22 +223,13 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch S, const uint8_t *org
         te_dequant(X, qp, s2);
         te_inv_tx(X, s2);
       }
-      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
-        const int p = pb[(i + y) * size + j + x];
-        rec[(i + y) * size + j + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, s2, y, x) + p) : p);
-      }
-      te_sync();
+      te_recon(rec + i * size + j, size, pb + i * size + j, size, X, s2, bit);
       cbp = (cbp << 1) + bit;
     }
     return cbp;
   }
   const int fast = (size == 64 && F.speed > 0) || F.speed > 1;
-  for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
-    X.R[e] = (int16_t)((int)org[y * os + x] - (int)pb[e]);
-  }
-  te_sync();
+  te_residual(X.R, org, os, pb, size, size);
   te_fwd_tx(X, size, fast);
   cbp = te_quant(X, qp, size, type);
   const int q = TE_MIN(size, 16);
@@ -162,11 +238,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch S, const uint8_t *org
     te_dequant(X, qp, size);
     te_inv_tx(X, size);
   }
-  for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
-    rec[e] = (uint8_t)(cbp ? te_clip255(te_res_at(X, size, y, x) + pb[e]) : pb[e]);
-  }
-  te_sync();
+  te_recon(rec, size, pb, size, X, size, cbp);
   return cbp;
 }
 
@@ -185,11 +257,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch S, const uint8_t *org
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
       te_make_top_and_left(*S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
       te_intra_pred(*S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
-      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
-        X.R[e] = (int16_t)((int)org[(i + y) * os + j + x] - (int)pb[e]);
-      }
-      te_sync();
+      te_residual(X.R, org + i * os + j, os, pb, s2, s2);
       te_fwd_tx(X, s2, fast);
       const int bit = te_quant(X, qp, s2, type);
       for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * 256 + e] = (int16_t)X.C[e];
@@ -197,22 +265,14 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch S, const uint8_t *org
         te_dequant(X, qp, s2);
         te_inv_tx(X, s2);
       }
-      for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-        const int y = te_dv(e, s2), x = e - te_dv(e, s2) * s2;
-        rec[(i + y) * size + j + x] = (uint8_t)(bit ? te_clip255(te_res_at(X, s2, y, x) + pb[e]) : pb[e]);
-      }
-      te_sync();
+      te_recon(rec + i * size + j, size, pb, s2, X, s2, bit);
       cbp = (cbp << 1) + bit;
     }
     return cbp;
   }
   te_make_top_and_left(*S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
   te_intra_pred(*S.nb, ypos, xpos, size, pb, mode, 0);
-  for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
-    X.R[e] = (int16_t)((int)org[y * os + x] - (int)pb[e]);
-  }
-  te_sync();
+  te_residual(X.R, org, os, pb, size, size);
   te_fwd_tx(X, size, fast);
   const int cbp = te_quant(X, qp, size, type);
   const int q = TE_MIN(size, 16);
@@ -221,11 +281,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch S, const uint8_t *org
     te_dequant(X, qp, size);
     te_inv_tx(X, size);
   }
-  for (int e = TE_LANE; e < size * size; e += TE_NL) {
-    const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
-    rec[e] = (uint8_t)(cbp ? te_clip255(te_res_at(X, size, y, x) + pb[e]) : pb[e]);
-  }
-  te_sync();
+  te_recon(rec, size, pb, size, X, size, cbp);
   return cbp;
 }
 
@@ -581,18 +637,11 @@ TE_FN void te_copy_best(TeBlockInfo &bi, TeParam &tmp) {
 TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
   TE_P(TP_COMMIT);
   const int size = bi.size, bw = bi.bwidth, bh = bi.bheight, sC = size / 2;
-  const uint8_t *r = bi.rec;
-  for (int e = TE_LANE; e < bw * bh; e += TE_NL) {
-    const int i = te_dv(e, bw), j = e - te_dv(e, bw) * bw;
-    F.ry[(bi.ypos + i) * F.rsy + bi.xpos + j] = r[i * size + j];
-  }
-  const int cw = bw / 2, ch = bh / 2;
-  for (int e = TE_LANE; e < cw * ch; e += TE_NL) {
-    const int i = te_dv(e, cw), j = e - te_dv(e, cw) * cw;
-    const int o = (bi.ypos / 2 + i) * F.rsc + bi.xpos / 2 + j;
-    F.ru[o] = te_pu((uint8_t *)r, size)[i * sC + j];
-    F.rv[o] = te_pv((uint8_t *)r, size)[i * sC + j];
-  }
+  uint8_t *r = bi.rec;
+  te_copy_rect(F.ry + bi.ypos * F.rsy + bi.xpos, F.rsy, r, size, bw, bh);
+  const int cw = bw / 2, ch = bh / 2, oc = (bi.ypos / 2) * F.rsc + bi.xpos / 2;
+  te_copy_rect(F.ru + oc, F.rsc, te_pu(r, size), sC, cw, ch);
+  te_copy_rect(F.rv + oc, F.rsc, te_pv(r, size), sC, cw, ch);
   const TeParam &p = bi.bp;
   const int div = size / 8, bs = F.W / 4;
   const int nw = bw / 4, nh = bh / 4;
@@ -895,14 +944,17 @@ TE_FN int te_es_luma(TeScratch S, const uint8_t *org, int os, int size, const ui
   TeTx &X = *S.tx;
   int n = size;
   if (size > 4) {
-    const int s2 = size / 2;
-    for (int e = TE_LANE; e < s2 * s2; e += TE_NL) {
-      const int i = te_dv(e, s2), j = e - te_dv(e, s2) * s2;
+    const int s2 = size / 2, h2 = s2 / 2;  // two outputs per lane: 4 columns x 2 rows
+    for (int g = TE_LANE; g < s2 * h2; g += TE_NL) {
+      const int i = te_dv(g, h2), j = (g - i * h2) * 2;
       const int i2 = 2 * i, j2 = 2 * j;
-      const int a = (int)org[i2 * os + j2] - pb[i2 * size + j2], b = (int)org[i2 * os + j2 + 1] - pb[i2 * size + j2 + 1];
-      const int c = (int)org[(i2 + 1) * os + j2] - pb[(i2 + 1) * size + j2],
-                d = (int)org[(i2 + 1) * os + j2 + 1] - pb[(i2 + 1) * size + j2 + 1];
-      X.R[e] = (int16_t)((a + b + c + d + 2) >> 2);
+      const uint32_t o0 = te_ld4(org + i2 * os + j2), o1 = te_ld4(org + (i2 + 1) * os + j2);
+      const uint32_t p0 = te_ld4(pb + i2 * size + j2), p1 = te_ld4(pb + (i2 + 1) * size + j2);
+      for (int k = 0; k < 2; k++) {
+        const int a = te_b(o0, 2 * k) - te_b(p0, 2 * k), b = te_b(o0, 2 * k + 1) - te_b(p0, 2 * k + 1);
+        const int c = te_b(o1, 2 * k) - te_b(p1, 2 * k), d = te_b(o1, 2 * k + 1) - te_b(p1, 2 * k + 1);
+        X.R[i * s2 + j + k] = (int16_t)((a + b + c + d + 2) >> 2);
+      }
     }
     n = s2;
   } else {
@@ -960,14 +1012,14 @@ TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch S, const TeBlockInf
         TeMv m1 = te_clip_mv(p.mv1[0], ypos, xpos, F.W, F.H, size0, sg1);
         te_mc_luma(pb0, size0, F.refy[p.ref_idx0] + ry, F.rsy, size0, size0, m0, sg0, bip);
         te_mc_luma(pb1, size0, F.refy[p.ref_idx1] + ry, F.rsy, size0, size0, m1, sg1, bip);
-        for (int e = TE_LANE; e < size0 * size0; e += TE_NL) pb[e] = (uint8_t)(((int)pb0[e] + (int)pb1[e]) >> 1);
+        te_avg_rect(pb, size0, pb0, size0, pb1, size0, size0, size0);
         te_sync();
         if (te_es_luma(S, oY, F.osy, size0, pb, thr_y)) return 0;
         // chroma legs use the unclipped vectors (:2680-2702)
         for (int c = 0; c < 2; c++) {
           te_mc_chroma(pb0, s0c, (c ? F.refv : F.refu)[p.ref_idx0] + rc, F.rsc, s0c, s0c, p.mv0[0], sg0);
           te_mc_chroma(pb1, s0c, (c ? F.refv : F.refu)[p.ref_idx1] + rc, F.rsc, s0c, s0c, p.mv1[0], sg1);
-          for (int e = TE_LANE; e < s0c * s0c; e += TE_NL) pb[e] = (uint8_t)(((int)pb0[e] + (int)pb1[e]) >> 1);
+          te_avg_rect(pb, s0c, pb0, s0c, pb1, s0c, s0c, s0c);
           te_sync();
           if (te_es_chroma(c ? oV : oU, F.osc, s0c, pb, thr_c)) return 0;
         }

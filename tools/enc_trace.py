@@ -20,7 +20,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "thor_amd", "libthor_amd_trace.so")
 KINDS = {1: "me", 2: "enc_block", 3: "cost", 4: "bipred", 5: "mode_dec", 6: "dqp", 7: "bip_org8", 8: "bip_mv",
-         9: "me_int", 10: "pb", 11: "ref"}
+         9: "me_int", 10: "pb", 11: "ref", 12: "pred_q"}
 
 
 def build():
@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--name", default="cif_high")
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--frame", type=int, default=3)
+    ap.add_argument("--sb-rows", type=int, default=1, help="keep the records of the first N SB rows (0: all)")
     a = ap.parse_args()
     if a.build:
         return build()
@@ -93,6 +94,8 @@ def main():
     m = min(int(cnt[0]), cap)
     recs = np.zeros((m, 8), np.int32)
     lib.thor_d2h(recs.ctypes.data, buf + 32, recs.nbytes)
+    keep = (recs[:, 2] < 64 * a.sb_rows) if a.sb_rows else np.ones(len(recs), bool)
+    recs = recs[keep]  # gpurun returns at most 64 MiB
     out = os.path.join(ROOT, "gpurun_out", "%s_f%d_dev.trc" % (a.name, a.frame))
     os.makedirs(os.path.dirname(out), exist_ok=True)
     recs.tofile(out)
