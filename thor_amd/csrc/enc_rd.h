@@ -686,7 +686,12 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
       const TeMv mv = list ? m0[0] : m1[0];
       ref_idx = list ? min_ref_idx0 : min_ref_idx1;
       const int sign = F.ref_fnum[ref_idx] > F.frame_num;
-      te_pred_yuv(F, ref_idx, S.pb, bi, list ? m0 : m1, sign, 1, 1);
+      // the leg's vectors copied by value: a pointer select between the two
+      // private arrays (list ? m0 : m1) is miscompiled by this hipcc for gfx950
+      // (the m1 array is read for list 1 in the second iteration)
+      TeMv leg[4];
+      for (int i = 0; i < 4; i++) leg[i] = list ? m0[i] : m1[i];
+      te_pred_yuv(F, ref_idx, S.pb, bi, leg, sign, 1, 1);
       for (int e = TE_LANE; e < size * size; e += TE_NL) {
         const int y = te_dv(e, size), x = e - te_dv(e, size) * size;
         S.org8[e] = (uint8_t)te_clip255(2 * (int)org[y * F.osy + x] - (int)S.pb[e]);

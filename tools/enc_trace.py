@@ -32,6 +32,8 @@ def build():
 def per_sb(recs):
     d = defaultdict(list)
     for r in recs:
+        if r[1] == 13:  # device-only (exec mask)
+            continue
         d[(int(r[2]) // 64, int(r[3]) // 64)].append(tuple(int(v) for v in r))
     return d
 
@@ -39,7 +41,7 @@ def per_sb(recs):
 def compare(a, b):
     A = per_sb(np.fromfile(a, np.int32).reshape(-1, 8))
     B = per_sb(np.fromfile(b, np.int32).reshape(-1, 8))
-    for key in sorted(set(A) | set(B)):
+    for key in sorted(set(A) & set(B)):
         x, y = A.get(key, []), B.get(key, [])
         for i, (p, q) in enumerate(zip(x, y)):
             if p != q:
