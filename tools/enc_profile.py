@@ -45,7 +45,7 @@ def main():
     lib.thor_enc_profile_buffer.argtypes = [C.c_void_p]
     meta = json.load(open(os.path.join(ROOT, "tests", "golden", "streams.json")))[a.name]
     w, h, n = meta["width"], meta["height"], a.frames
-    frames = np.stack([np.concatenate([p.reshape(-1) for p in synth.synth_frame(w, h, t, meta["seed"])]) for t in range(n)])
+    frames = synth.synth_frames(w, h, n, meta["seed"], workers=8)
     encs = [GpuEncoder(params_for(meta["config"], w, h, n, meta["extra"])) for _ in range(a.batch)]
     for e in encs:
         e.upload_sequence(frames)
