@@ -44,13 +44,21 @@ struct TeJob {
   int nsbh, nsbv, clpf;
 };
 
-__device__ __forceinline__ unsigned te_ld_acquire(const unsigned *p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+// Poll with a relaxed device-coherent load; the acquire fence follows once,
+// after the condition holds (an acquire load per poll would invalidate the
+// L2 on every iteration of every waiting wave).
+__device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // WPP worker: grid of persistent single-wave workgroups; ticket t -> stream
 // t % n, SB row t / n.
-__global__ __launch_bounds__(64) void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
+#if defined(THOR_ENC_WPE)  // experiments: minimum waves per SIMD the register budget must allow
+#define TE_WPE __attribute__((amdgpu_waves_per_eu(THOR_ENC_WPE)))
+#else
+#define TE_WPE
+#endif
+__global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
                                                  TeScratchMem *scratch, TeSB *sbs, unsigned *err) {
   __shared__ TeTx s_tx;
   __shared__ TeNbr s_nb;
@@ -67,13 +75,15 @@ __global__ __launch_bounds__(64) void k_enc_rows(const TeJob *__restrict__ jobs,
     const int s = (int)t % n, k = (int)t / n;
     const TeJob &J = jobs[s];
     if (k >= J.nsbv) continue;
+    unsigned seen = 0;  // progress of the row above observed (and acquired) so far
     for (int l = 0; l < J.nsbh; l++) {
-      if (k > 0) {  // SB (k-1, l+1) (or the whole row above) must be done
-        const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
+      const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
+      if (k > 0 && need > seen) {  // SB (k-1, l+1) (or the whole row above) must be done
         TE_P(TP_WAIT);
+        unsigned v = 0;
         if (lane == 0) {
           const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-          while (te_ld_acquire(&J.progress[k - 1]) < need) {
+          while ((v = te_ld_relaxed(&J.progress[k - 1])) < need) {
             __builtin_amdgcn_s_sleep(8);
             // a wedged dependency (5 minutes): give up, reported; never hang the GPU
             if (__builtin_amdgcn_s_memrealtime() - t0 > 30000000000ULL) {
@@ -82,6 +92,7 @@ __global__ __launch_bounds__(64) void k_enc_rows(const TeJob *__restrict__ jobs,
             }
           }
         }
+        seen = __builtin_amdgcn_readfirstlane(v);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }

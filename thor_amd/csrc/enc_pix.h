@@ -43,66 +43,93 @@ TE_FN void te_mc_luma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w, i
   const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
   const int fy = my & 3, fx = mx & 3;
   const uint8_t *r = ref + (my >> 2) * rs + (mx >> 2);
-  if ((w & 3) == 0) {  // four outputs per lane: dword loads, taps from registers
-    const int w4 = w >> 2, n4 = w4 * h;
-    if (!fx && !fy) {
-      for (int g = TE_LANE; g < n4; g += TE_NL) {
-        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
-        te_st4(dst + i * ds + j, te_ld4(r + i * rs + j));
-      }
-    } else if (fx == 2 && fy == 2) {  // rows -1..2, columns -1..6
-      for (int g = TE_LANE; g < n4; g += TE_NL) {
-        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
-        const uint8_t *p = r + (i - 1) * rs + j - 1;
-        int c[4][8];
-        for (int t = 0; t < 4; t++) {
-          const uint32_t lo = te_ld4(p + t * rs), hi = te_ld4(p + t * rs + 4);
+  if ((w & 3) == 0 && (h & 3) == 0) {
+    // 4 x 4 outputs per lane: every source row the unit needs is loaded up
+    // front (dwords, all in flight at once) and filtered horizontally once,
+    // then the vertical taps run from registers
+    const int w4 = w >> 2, nu = w4 * (h >> 2);
+    for (int u = TE_LANE; u < nu; u += TE_NL) {
+      const int rg = te_dv(u, w4), j = (u - rg * w4) * 4, i0 = rg * 4;
+      int o[4][4];
+      if (!fx && !fy) {
+        for (int y = 0; y < 4; y++) te_st4(dst + (i0 + y) * ds + j, te_ld4(r + (i0 + y) * rs + j));
+        continue;
+      } else if (fx == 2 && fy == 2) {  // rows -1..5, columns -1..6
+        uint32_t lo[7], hi[7];
+#pragma unroll
+        for (int t = 0; t < 7; t++) {
+          const uint8_t *p = r + (i0 - 1 + t) * rs + j - 1;
+          lo[t] = te_ld4(p);
+          hi[t] = te_ld4(p + 4);
+        }
+        int c[7][8];
+#pragma unroll
+        for (int t = 0; t < 7; t++)
           for (int k = 0; k < 4; k++) {
-            c[t][k] = te_b(lo, k);
-            c[t][k + 4] = te_b(hi, k);
+            c[t][k] = te_b(lo[t], k);
+            c[t][k + 4] = te_b(hi[t], k);
           }
-        }
-        int o[4];
-        for (int x = 0; x < 4; x++) {  // c[dy + 1][dx + 1]
-          const int k = x + 1;
-          const int v = c[0][k] + c[0][k + 1] + c[1][k - 1] + 2 * c[1][k] + 2 * c[1][k + 1] + c[1][k + 2] + c[2][k - 1] +
-                        2 * c[2][k] + 2 * c[2][k + 1] + c[2][k + 2] + c[3][k] + c[3][k + 1];
-          o[x] = te_clip255((v + 8) >> 4);
-        }
-        te_st4(dst + i * ds + j, te_pack4(o[0], o[1], o[2], o[3]));
-      }
-    } else {
-      const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
-      const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
-      const int k0 = fy ? 0 : 2, k1 = fy ? 6 : 3;  // fy == 0: the vertical taps are (0, 0, 64, 0, 0, 0)
-      for (int g = TE_LANE; g < n4; g += TE_NL) {
-        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
-        int s[4] = {0, 0, 0, 0};
-        for (int k = k0; k < k1; k++) {
-          const uint8_t *p = r + (i - 2 + k) * rs + j - 2;
-          int hk[4];
-          if (fx) {  // columns -2..9 of the row, 6 taps
-            const uint32_t d0 = te_ld4(p), d1 = te_ld4(p + 4), d2 = te_ld4(p + 8);
-            int c[12];
-            for (int b = 0; b < 4; b++) {
-              c[b] = te_b(d0, b);
-              c[b + 4] = te_b(d1, b);
-              c[b + 8] = te_b(d2, b);
-            }
-            for (int x = 0; x < 4; x++) {
-              int t = 0;
-              for (int m = 0; m < 6; m++) t += fh[m] * c[x + m];
-              hk[x] = t;
-            }
-          } else {  // horizontal taps (0, 0, 64, 0, 0, 0)
-            const uint32_t d = te_ld4(p + 2);
-            for (int x = 0; x < 4; x++) hk[x] = 64 * te_b(d, x);
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+          for (int x = 0; x < 4; x++) {  // c[y + dy + 1][x + dx + 1]
+            const int k = x + 1;
+            const int *a = c[y], *b = c[y + 1], *d = c[y + 2], *e = c[y + 3];
+            const int v = a[k] + a[k + 1] + b[k - 1] + 2 * b[k] + 2 * b[k + 1] + b[k + 2] + d[k - 1] + 2 * d[k] +
+                          2 * d[k + 1] + d[k + 2] + e[k] + e[k + 1];
+            o[y][x] = te_clip255((v + 8) >> 4);
           }
-          for (int x = 0; x < 4; x++) s[x] += fv[k] * hk[x];
+      } else {
+        const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
+        const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
+        int hk[9][4];  // horizontally filtered rows -2..6 (fy == 0: rows 0..3 at index 2..5)
+        if (fx) {
+          uint32_t d[9][3];
+          const int t0 = fy ? 0 : 2, t1 = fy ? 9 : 6;
+#pragma unroll
+          for (int t = 0; t < 9; t++)
+            if (t >= t0 && t < t1) {
+              const uint8_t *p = r + (i0 - 2 + t) * rs + j - 2;
+              d[t][0] = te_ld4(p);
+              d[t][1] = te_ld4(p + 4);
+              d[t][2] = te_ld4(p + 8);
+            }
+#pragma unroll
+          for (int t = 0; t < 9; t++)
+            if (t >= t0 && t < t1) {
+              int c[12];
+              for (int b = 0; b < 4; b++) {
+                c[b] = te_b(d[t][0], b);
+                c[b + 4] = te_b(d[t][1], b);
+                c[b + 8] = te_b(d[t][2], b);
+              }
+              for (int x = 0; x < 4; x++) {
+                int a = 0;
+                for (int m = 0; m < 6; m++) a += fh[m] * c[x + m];
+                hk[t][x] = a;
+              }
+            }
+        } else {  // horizontal taps (0, 0, 64, 0, 0, 0); fy != 0 here
+          uint32_t d[9];
+#pragma unroll
+          for (int t = 0; t < 9; t++) d[t] = te_ld4(r + (i0 - 2 + t) * rs + j);
+#pragma unroll
+          for (int t = 0; t < 9; t++)
+            for (int x = 0; x < 4; x++) hk[t][x] = 64 * te_b(d[t], x);
         }
-        te_st4(dst + i * ds + j, te_pack4(te_clip255((s[0] + 2048) >> 12), te_clip255((s[1] + 2048) >> 12),
-                                          te_clip255((s[2] + 2048) >> 12), te_clip255((s[3] + 2048) >> 12)));
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+          for (int x = 0; x < 4; x++) {
+            int a;
+            if (fy) {
+              a = 0;
+              for (int k = 0; k < 6; k++) a += fv[k] * hk[y + k][x];
+            } else {
+              a = 64 * hk[y + 2][x];
+            }
+            o[y][x] = te_clip255((a + 2048) >> 12);
+          }
       }
+      for (int y = 0; y < 4; y++) te_st4(dst + (i0 + y) * ds + j, te_pack4(o[y][0], o[y][1], o[y][2], o[y][3]));
     }
     te_sync();
     return;
@@ -146,6 +173,50 @@ TE_FN void te_mc_chroma(uint8_t *dst, int ds, const uint8_t *ref, int rs, int w,
   const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
   const int fy = my & 7, fx = mx & 7;
   const uint8_t *r = ref + (my >> 3) * rs + (mx >> 3);
+  if ((w & 3) == 0 && (h & 3) == 0) {  // 4 x 4 outputs per lane, rows -1..4 loaded up front
+    const int w4 = w >> 2, nu = w4 * (h >> 2);
+    const int8_t *fh = te_chroma_f[fx], *fv = te_chroma_f[fy];
+    for (int u = TE_LANE; u < nu; u += TE_NL) {
+      const int rg = te_dv(u, w4), j = (u - rg * w4) * 4, i0 = rg * 4;
+      if (!fx && !fy) {
+        for (int y = 0; y < 4; y++) te_st4(dst + (i0 + y) * ds + j, te_ld4(r + (i0 + y) * rs + j));
+        continue;
+      }
+      uint32_t lo[7], hi[7];
+#pragma unroll
+      for (int t = 0; t < 7; t++) {
+        const uint8_t *p = r + (i0 - 1 + t) * rs + j - 1;
+        lo[t] = te_ld4(p);
+        hi[t] = te_ld4(p + 4);
+      }
+      int hk[7][4];
+#pragma unroll
+      for (int t = 0; t < 7; t++) {
+        int c[8];
+        for (int b = 0; b < 4; b++) {
+          c[b] = te_b(lo[t], b);
+          c[b + 4] = te_b(hi[t], b);
+        }
+        for (int x = 0; x < 4; x++) {
+          int a = 0;
+          for (int k = 0; k < 4; k++) a += fh[k] * c[x + k];
+          hk[t][x] = a;
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < 4; y++) {
+        int o[4];
+        for (int x = 0; x < 4; x++) {
+          int a = 0;
+          for (int m = 0; m < 4; m++) a += fv[m] * hk[y + m][x];
+          o[x] = te_clip255((a + 2048) >> 12);
+        }
+        te_st4(dst + (i0 + y) * ds + j, te_pack4(o[0], o[1], o[2], o[3]));
+      }
+    }
+    te_sync();
+    return;
+  }
   if ((w & 3) == 0) {  // four outputs per lane
     const int w4 = w >> 2, n4 = w4 * h;
     if (!fx && !fy) {
