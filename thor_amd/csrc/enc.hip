@@ -94,7 +94,11 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
         }
         seen = __builtin_amdgcn_readfirstlane(v);
         __builtin_amdgcn_wave_barrier();
+#if defined(THOR_ENC_EXP_NOSYNC)  // experiment only: no L2 invalidate (incorrect across XCDs)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
       }
       const int sbi = k * J.nsbh + l;
       sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
@@ -104,7 +108,11 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
         J.sb_nbits[sbi] = sb.bits.pos;
         if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
       }
+#if defined(THOR_ENC_EXP_NOSYNC)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#else
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) __hip_atomic_store(&J.progress[k], (unsigned)(l + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }

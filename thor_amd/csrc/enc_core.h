@@ -366,6 +366,32 @@ TE_FN void te_rewind(TeBits &b, int p) {
   }
   b.pos = p;
 }
+// A register copy of a writer whose state is wave-uniform: the serial syntax
+// writers work on it (SGPRs, scalar branches) instead of going through the
+// caller's TeBits in memory on every put, and store it back once at the end.
+TE_FN int te_uni(int v) {
+#if !defined(TE_HOST)
+  return __builtin_amdgcn_readfirstlane(v);
+#else
+  return v;
+#endif
+}
+TE_FN TeBits te_bits_local(const TeBits &b) {
+  TeBits l;
+#if !defined(TE_HOST)
+  const uint64_t a = (uint64_t)b.w;
+  l.w = (uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+  l.cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)b.cur);
+#else
+  l.w = b.w;
+  l.cur = b.cur;
+#endif
+  l.pos = te_uni(b.pos);
+  l.cap = te_uni(b.cap);
+  return l;
+}
+
 // store the partial last word (end of a superblock)
 TE_FN void te_bits_flush(TeBits &b) {
   if ((b.pos & 31) && TE_LANE == 0 && b.pos <= b.cap) b.w[b.pos >> 5] = b.cur;
@@ -650,9 +676,12 @@ TE_FN void te_load_scan(TeScanRegs &R, const int16_t *c, int q) {
   R.nz[3] = __ballot(R.v3 != 0);
 #endif
 }
-TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, int16_t *scan /* unused */) {
+TE_NOINL void te_write_coeff(TeBits &bo, const int16_t *c, int size, int type, int16_t *scan /* unused */) {
   TE_P(TP_WCOEF);
   (void)scan;
+  TeBits b = te_bits_local(bo);
+  size = te_uni(size);
+  type = te_uni(type);
   const int q = TE_MIN(16, size), N = q * q;
   const int chroma = type & 1, intra = (type >> 1) & 1;
   int vlc_adaptive = intra && !chroma;
@@ -718,6 +747,7 @@ TE_NOINL void te_write_coeff(TeBits &b, const int16_t *c, int size, int type, in
       else te_put_vlc(b, 2, cn + 1);
     }
   }
+  bo = b;
 }
 
 // write_delta_qp, write_bits.c:255-265
@@ -780,8 +810,9 @@ TE_FN void te_write_super_mode(TeBits &b, const TeFrame &F, const TeBlockInfo &b
 TE_FN const int16_t *te_tile(const TeParam &p, int comp, int idx) { return p.coeff + comp * TE_COEF_COMP + idx * 256; }
 
 // write_block, write_bits.c:364-650.  Returns the number of bits written.
-TE_NOINL int te_write_block(TeBits &b, const TeFrame &F, const TeBlockInfo &bi, const TeParam &p, int16_t *scan) {
+TE_NOINL int te_write_block(TeBits &bo, const TeFrame &F, const TeBlockInfo &bi, const TeParam &p, int16_t *scan) {
   TE_P(TP_WBLOCK);
+  TeBits b = te_bits_local(bo);
   const int start = b.pos;
   const int size = bi.size, mode = p.mode, tb_split = p.tb_split;
   const int coeff_type = (mode == TE_INTRA) << 1;
@@ -935,5 +966,6 @@ TE_NOINL int te_write_block(TeBits &b, const TeFrame &F, const TeBlockInfo &bi, 
       if (p.cbp_v) te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1, scan);
     }
   }
+  bo = b;
   return b.pos - start;
 }

@@ -704,6 +704,33 @@ TE_FN int te_fwd8(const int16_t *s, int k, int shift) {
   return te_wrap16((v + (1 << (shift - 1))) >> shift);
 }
 
+// The two matrix passes of transform (common/transform.c:309-327) for an
+// N-point basis, N a compile-time constant so the inner products unroll and
+// their LDS reads issue back to back: in (N x N) -> X.T (q x N) -> X.C (q x q).
+template <int N>
+TE_FN void te_fwd_gen(TeTx &X, const int16_t *in, int sh1, int sh2) {
+  constexpr int q = N < 16 ? N : 16;
+  const int add1 = 1 << (sh1 - 1), add2 = 1 << (sh2 - 1);
+  for (int e = TE_LANE; e < q * N; e += TE_NL) {  // :309-316, int16 store
+    const int i = e / N, j = e % N;
+    const int16_t *x = &in[j * N];
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) s += TE_DCT(X, N, i, k) * (int)x[k];
+    X.T[i * N + j] = (int16_t)te_wrap16((s + add1) >> sh1);
+  }
+  te_sync();
+  for (int e = TE_LANE; e < q * q; e += TE_NL) {  // :319-327
+    const int i = e / q, j = e % q;
+    const int16_t *t = &X.T[j * N];
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) s += TE_DCT(X, N, i, k) * (int)t[k];
+    X.C[i * q + j] = (int16_t)te_wrap16((s + add2) >> sh2);
+  }
+  te_sync();
+}
+
 // transform, common/transform.c:249-330 (SIMD transform_simd for the 8x8
 // butterfly wrap): X.R (size x size, stride size) -> X.C (q x q raster).
 TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
@@ -749,24 +776,9 @@ TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
     in = X.A;
   }
   te_sync();
-  const int q = TE_MIN(size, 16);
-  const int add1 = 1 << (sh1 - 1), add2 = 1 << (sh2 - 1);
-  for (int e = TE_LANE; e < q * N; e += TE_NL) {  // :309-316, int16 store
-    const int i = te_dv(e, N), j = e - te_dv(e, N) * N;
-    const int16_t *x = &in[j * N];
-    int s = 0;
-    for (int k = 0; k < N; k++) s += TE_DCT(X, N, i, k) * (int)x[k];
-    X.T[i * N + j] = (int16_t)te_wrap16((s + add1) >> sh1);
-  }
-  te_sync();
-  for (int e = TE_LANE; e < q * q; e += TE_NL) {  // :319-327
-    const int i = te_dv(e, q), j = e - te_dv(e, q) * q;
-    const int16_t *t = &X.T[j * N];
-    int s = 0;
-    for (int k = 0; k < N; k++) s += TE_DCT(X, N, i, k) * (int)t[k];
-    X.C[i * q + j] = (int16_t)te_wrap16((s + add2) >> sh2);
-  }
-  te_sync();
+  if (N == 4) te_fwd_gen<4>(X, in, sh1, sh2);
+  else if (N == 16) te_fwd_gen<16>(X, in, sh1, sh2);
+  else te_fwd_gen<32>(X, in, sh1, sh2);
 }
 
 // quantize, enc/encode_block.c:75-172 (rdoq = 0): X.C -> levels (q x q
@@ -865,23 +877,34 @@ TE_FN void te_dequant(TeTx &X, int qp, int size) {
 
 // inverse_transform (common/transform.c:432-518): X.C (q x q) -> X.R
 // (n x n, n = min(size, 32); 64 = the 32-point output, replicated 2x2 by the reader).
-TE_FN void te_inv_tx(TeTx &X, int size) {
-  TE_P(TP_INV);
-  const int n = size == 64 ? 32 : size, q = TE_MIN(n, 16);
+template <int n>
+TE_FN void te_inv_gen(TeTx &X) {
+  constexpr int q = n < 16 ? n : 16;
   for (int e = TE_LANE; e < q * n; e += TE_NL) {
-    const int k = te_dv(e, n), yp = e - te_dv(e, n) * n;  // coefficient column k
+    const int k = e / n, yp = e % n;  // coefficient column k
     int s = 0;
+#pragma unroll
     for (int m = 0; m < q; m++) s += TE_DCT(X, n, m, yp) * X.C[m * q + k];
     X.T[k * n + yp] = (int16_t)te_clip16((s + 64) >> 7);
   }
   te_sync();
   for (int e = TE_LANE; e < n * n; e += TE_NL) {
-    const int yp = te_dv(e, n), xp = e - te_dv(e, n) * n;
+    const int yp = e / n, xp = e % n;
     int s = 0;
+#pragma unroll
     for (int k = 0; k < q; k++) s += TE_DCT(X, n, k, xp) * (int)X.T[k * n + yp];
     X.R[yp * n + xp] = (int16_t)te_clip16((s + 2048) >> 12);
   }
   te_sync();
+}
+TE_FN void te_inv_tx(TeTx &X, int size) {
+  TE_P(TP_INV);
+  switch (size) {
+    case 4: te_inv_gen<4>(X); break;
+    case 8: te_inv_gen<8>(X); break;
+    case 16: te_inv_gen<16>(X); break;
+    default: te_inv_gen<32>(X); break;  // 32, and 64 (the 32-point output, replicated 2x2 by the reader)
+  }
 }
 // residual value at (y, x) of an inverse-transformed N x N block in X.R
 TE_FN int te_res_at(const TeTx &X, int size, int y, int x) {
