@@ -599,6 +599,8 @@ struct TeBlockInfo {  // block_info_t, enc/mainenc.h:97-116
   int max_num_pb_part, max_num_tb_part, delta_qp, final_encode;
   TeCtx ctx;
   uint8_t *rec, *rec_best;  // compact Y (size^2) | U | V ((size/2)^2 each)
+  uint32_t *best_bits;      // the syntax bits the best candidate wrote (MSB first), or
+  int best_nbits;           // -1: not kept (the final write_block runs again)
 };
 
 // ---- block syntax (enc/write_bits.c) --------------------------------------

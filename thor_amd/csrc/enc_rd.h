@@ -7,9 +7,11 @@
 
 // Per-wave working memory (global memory on the device; one per SB-row worker).
 #define TE_BLK (64 * 64 * 3 / 2)
+#define TE_BEST_WORDS 1024
 struct TeLevel {             // one quadtree level (64, 32, 16, 8)
   uint8_t rbuf[2][TE_BLK];   // rec_block / rec_block_best (roles swap, see te_copy_best)
   int16_t cbuf[3][3 * TE_COEF_COMP];  // coefficient sets: best, tmp, spare
+  uint32_t bbits[TE_BEST_WORDS];      // the best candidate's syntax bits (TeBlockInfo::best_bits)
 };
 struct TeScratchMem {         // global memory, one per worker wave
   TeLevel lv[4];
@@ -285,6 +287,46 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch S, const uint8_t *org
   return cbp;
 }
 
+// The candidate just written (its nbits end at b.pos) became the best: keep
+// its syntax bits, so that the final encode of the block (re-use, the same
+// parameters and contexts) copies them instead of running write_block again.
+TE_FN void te_keep_best_bits(TeBits &b, TeBlockInfo &bi, int nbits) {
+  if (nbits > TE_BEST_WORDS * 32 || b.pos > b.cap) {
+    bi.best_nbits = -1;
+    return;
+  }
+  if ((b.pos & 31) && TE_LANE == 0) b.w[b.pos >> 5] = b.cur;  // the register word (stored again when complete)
+  te_sync();
+  const int start = b.pos - nbits, nw = (nbits + 31) >> 5, cw = b.cap >> 5;
+  for (int i = TE_LANE; i < nw; i += TE_NL) {
+    const int p = start + 32 * i, wi = p >> 5, sh = p & 31;
+    uint32_t v = b.w[wi] << sh;
+    if (sh && wi + 1 < cw) v |= b.w[wi + 1] >> (32 - sh);
+    bi.best_bits[i] = v;
+  }
+  te_sync();
+  bi.best_nbits = nbits;
+}
+// put nbits kept by te_keep_best_bits
+TE_FN void te_put_kept(TeBits &b, const uint32_t *w, int nbits) {
+#if !defined(TE_HOST)
+  for (int base = 0; base * 32 < nbits; base += 64) {
+    const int nw = TE_MIN(64, ((nbits + 31) >> 5) - base);
+    const uint32_t wl = TE_LANE < nw ? w[base + TE_LANE] : 0u;
+    for (int i = 0; i < nw; i++) {
+      const int n = TE_MIN(32, nbits - 32 * (base + i));
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)wl, i);
+      te_put(b, n, n == 32 ? v : v >> (32 - n));
+    }
+  }
+#else
+  for (int i = 0; 32 * i < nbits; i++) {
+    const int n = TE_MIN(32, nbits - 32 * i);
+    te_put(b, n, n == 32 ? w[i] : w[i] >> (32 - n));
+  }
+#endif
+}
+
 // encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
 // bi.rec, write the block's syntax.  Returns the bit count.
 TE_NOINL int te_encode_block(const TeFrame &F, TeScratch S, TeBits &b, TeBlockInfo &bi, TeParam &p) {
@@ -295,6 +337,10 @@ TE_NOINL int te_encode_block(const TeFrame &F, TeScratch S, TeBits &b, TeBlockIn
   const int re_use = (bi.final_encode & 1) && !F.enable_tb_split;
   if (re_use) {
     te_copy_bytes(bi.rec, bi.rec_best, size * size + 2 * sC * sC);
+    if (bi.best_nbits >= 0 && &p == &bi.bp) {  // the best candidate's own syntax bits
+      te_put_kept(b, bi.best_bits, bi.best_nbits);
+      return bi.best_nbits;
+    }
     return te_write_block(b, F, bi, p, S.tx->scan);
   }
   uint8_t *recY = bi.rec, *recU = te_pu(bi.rec, size), *recV = te_pv(bi.rec, size);
@@ -799,6 +845,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
       if (cost < min_cost) {
         min_cost = cost;
         te_copy_best(bi, tmp);
+        te_keep_best_bits(b, bi, nbits);
       }
     }
   }
@@ -818,6 +865,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
         if (cost < min_cost) {
           min_cost = cost;
           te_copy_best(bi, tmp);
+          te_keep_best_bits(b, bi, nbits);
         }
       }
       if (intra_inter_sad) {
@@ -872,6 +920,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
               if (cost < min_cost) {
                 min_cost = cost;
                 te_copy_best(bi, tmp);
+                te_keep_best_bits(b, bi, nbits);
               }
             }
           }
@@ -898,6 +947,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
         if (cost < min_cost) {
           min_cost = cost;
           te_copy_best(bi, tmp);
+          te_keep_best_bits(b, bi, nbits);
         }
         // B frames at speed 0 add a joint mv0 = -mv1 search (me_mode 1): rejected by the host
       }
@@ -933,6 +983,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
         if (cost < min_cost) {
           min_cost = cost;
           te_copy_best(bi, tmp);
+          te_keep_best_bits(b, bi, nbits);
         }
       }
     }
@@ -1067,6 +1118,7 @@ TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch S, TeSB &sb, TeBlo
       if (cost < min_cost) {
         min_cost = cost;
         te_copy_best(bi, tmp);
+        te_keep_best_bits(sb.bits, bi, nbits);
       }
     }
   }
@@ -1103,6 +1155,8 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch S, TeSB &sb, int 
   bi.delta_qp = qp - F.qp;
   bi.rec = lv.rbuf[0];
   bi.rec_best = lv.rbuf[1];
+  bi.best_bits = lv.bbits;
+  bi.best_nbits = -1;
   bi.bp.coeff = lv.cbuf[0];
   int16_t *tmp_coef = lv.cbuf[1];
   if (ft != TE_I) {
@@ -1115,6 +1169,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch S, TeSB &sb, int 
     te_rewind(b, pos_ref);
     if (early) {
       bi.final_encode = 3;
+      if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
       const int nbit = te_encode_block(F, S, b, bi, bi.bp);
@@ -1164,6 +1219,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch S, TeSB &sb, int 
     if (cost <= cost_small) {
       te_rewind(b, pos_ref);
       bi.final_encode = 1;
+      if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
       te_encode_block(F, S, b, bi, bi.bp);
