@@ -65,6 +65,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   __shared__ uint8_t s_pb[TE_BLK];
   const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb);
   te_load_basis(s_tx);
+  te_load_zig();
   TeSB &sb = sbs[blockIdx.x];
   const int lane = threadIdx.x;
   for (;;) {

@@ -317,14 +317,34 @@ static const TeZigzag &te_zig_h = te_zig;
 #else
 static const TeZigzag te_zig_h = TeZigzag();  // host copy (the parser)
 #endif
+#if !defined(TE_HOST)
+// LDS copy for the encoder worker (k_enc_rows loads it once: te_load_zig); the
+// per-lane lookups of quantize / write_coeff then cost an LDS read, not a
+// divergent global load
+__shared__ uint8_t te_zig_lds[2][3][256];
+__device__ __forceinline__ void te_load_zig() {
+  for (int e = threadIdx.x; e < 768; e += 64) {
+    te_zig_lds[0][e >> 8][e & 255] = te_zig.zz[e >> 8][e & 255];
+    te_zig_lds[1][e >> 8][e & 255] = te_zig.iz[e >> 8][e & 255];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+#endif
 TE_HD int te_zz(int q, int r) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return te_zig.zz[q == 4 ? 0 : (q == 8 ? 1 : 2)][r];
+  return te_zig_lds[0][q == 4 ? 0 : (q == 8 ? 1 : 2)][r];
 #else
   return te_zig_h.zz[q == 4 ? 0 : (q == 8 ? 1 : 2)][r];
 #endif
 }
-TE_FN int te_izz(int q, int pos) { return te_zig.iz[q == 4 ? 0 : (q == 8 ? 1 : 2)][pos]; }
+TE_FN int te_izz(int q, int pos) {
+#if defined(TE_HOST)
+  return te_zig.iz[q == 4 ? 0 : (q == 8 ? 1 : 2)][pos];
+#else
+  return te_zig_lds[1][q == 4 ? 0 : (q == 8 ? 1 : 2)][pos];
+#endif
+}
 
 // ---- bit writer (enc/putbits.c:112-146) -------------------------------------
 // One stream per superblock: MSB-first bits into 32-bit words.  The word being

@@ -789,19 +789,28 @@ TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
   const int lg = te_log2(size), q = TE_MIN(size, 16), nq = q * q;
   const int scale = te_gquant[qp % 6], shift2 = 21 - lg + qp / 6;
   const int offset = (intra ? 38 : -26) * (1 << (shift2 - 8));
+  // each lane's coefficients and scan positions stay in registers across the passes
+  constexpr int NS = (256 + TE_NL - 1) / TE_NL;
+  int posv[NS], cv[NS];
   int lp = -1;
-  for (int r = TE_LANE; r < nq; r += TE_NL) {
-    const int pos = te_zz(q, r), c = X.C[r];
-    if ((te_abs(te_abs(c) * scale + offset) >> shift2) != 0) lp = TE_MAX(lp, pos);
+#pragma unroll
+  for (int t = 0; t < NS; t++) {
+    const int r = TE_LANE + TE_NL * t;
+    posv[t] = r < nq ? te_zz(q, r) : 256;
+    cv[t] = r < nq ? X.C[r] : 0;
+    if (r < nq && (te_abs(te_abs(cv[t]) * scale + offset) >> shift2) != 0) lp = TE_MAX(lp, posv[t]);
   }
   const int last_pos = te_maxi(lp);  // -1: no level (the reference loop ends at pos = -1)
   const int off0 = (intra ? 102 : 51) * (1 << (shift2 - 8)), off1 = (intra ? 115 : 90) * (1 << (shift2 - 8));
   int any = 0;
-  for (int r = TE_LANE; r < nq; r += TE_NL) {
-    const int pos = te_zz(q, r);
+#pragma unroll
+  for (int t = 0; t < NS; t++) {
+    const int r = TE_LANE + TE_NL * t;
+    if (r >= nq) continue;
+    const int pos = posv[t];
     int lev = 0;
     if (pos <= last_pos) {
-      const int c = X.C[r];
+      const int c = cv[t];
       const int ac = scale * te_abs(c);
       const int l0 = ac >> shift2;
       const int l = (ac + ((l0 == 0 || chroma) ? off0 : off1)) >> shift2;
@@ -809,7 +818,7 @@ TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
       any |= l != 0;
     }
     X.S[pos] = (int16_t)lev;
-    X.O[pos] = X.C[r];
+    X.O[pos] = (int16_t)cv[t];
   }
   const int cbp = te_any(any);
   te_sync();
@@ -861,7 +870,11 @@ TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
     }
   }
   te_sync();
-  for (int r = TE_LANE; r < nq; r += TE_NL) X.C[r] = X.S[te_zz(q, r)];  // back to raster (:170-174)
+#pragma unroll
+  for (int t = 0; t < NS; t++) {  // back to raster (:170-174)
+    const int r = TE_LANE + TE_NL * t;
+    if (r < nq) X.C[r] = X.S[posv[t]];
+  }
   te_sync();
   return cbp;
 }

@@ -431,9 +431,34 @@ TE_NOINL int te_search_intra(const TeFrame &F, TeScratch S, const TeBlockInfo &b
   int min_sad = 1 << 30, best = TE_DC;
   const int n = num_modes == 4 ? 4 : 10;
   const uint8_t *o = F.oy + ypos * F.osy + xpos;
+#if !defined(TE_HOST)
+  // the original block in registers once (4-pixel chunks, up to 16 per lane), each
+  // mode's SAD against the compact prediction in LDS
+  const int w4 = size >> 2, n4 = w4 * size;
+  uint32_t org[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    const int g = TE_LANE + 64 * t;
+    org[t] = 0;
+    if (g < n4) {
+      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+      org[t] = te_ld4(o + i * F.osy + j);
+    }
+  }
+#endif
   for (int k = 0; k < n; k++) {
     te_intra_pred(*S.nb, ypos, xpos, size, S.pb, order[k], 1);
+#if !defined(TE_HOST)
+    uint32_t a = 0;
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      const int g = TE_LANE + 64 * t;
+      if (g < n4) a = te_sad4(org[t], te_ld4(S.pb + 4 * g), a);
+    }
+    const int sad = (int)te_sum(a);
+#else
     const int sad = (int)te_sad(o, F.osy, S.pb, size, size, size);
+#endif
     if (sad < min_sad) {
       best = order[k];
       min_sad = sad;
