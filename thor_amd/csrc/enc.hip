@@ -59,14 +59,18 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 #define TE_WPE
 #endif
 __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
-                                                 TeScratchMem *scratch, TeSB *sbs, unsigned *err) {
+                                                 TeScratchMem *scratch, unsigned *err) {
   __shared__ TeTx s_tx;
   __shared__ TeNbr s_nb;
   __shared__ uint8_t s_pb[TE_BLK];
-  const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb);
+  __shared__ TeBlockInfo s_bi[4];
+  __shared__ TeParam s_tmp;
+  __shared__ TeFrame s_F;  // the job's frame parameters, read all through the RD loop
+  __shared__ TeSB s_sb;    // the superblock's bit writer and ME candidate lists
+  const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb, s_bi, &s_tmp);
   te_load_basis(s_tx);
   te_load_zig();
-  TeSB &sb = sbs[blockIdx.x];
+  TeSB &sb = s_sb;
   const int lane = threadIdx.x;
   for (;;) {
     unsigned t = 0;
@@ -76,6 +80,12 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     const int s = (int)t % n, k = (int)t / n;
     const TeJob &J = jobs[s];
     if (k >= J.nsbv) continue;
+    {  // the job's frame parameters into LDS
+      const uint32_t *src = (const uint32_t *)&J.F;
+      uint32_t *dst = (uint32_t *)&s_F;
+      for (int e = lane; e < (int)(sizeof(TeFrame) / 4); e += 64) dst[e] = src[e];
+      te_sync();
+    }
     unsigned seen = 0;  // progress of the row above observed (and acquired) so far
     for (int l = 0; l < J.nsbh; l++) {
       const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
@@ -95,25 +105,17 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
         }
         seen = __builtin_amdgcn_readfirstlane(v);
         __builtin_amdgcn_wave_barrier();
-#if defined(THOR_ENC_EXP_NOSYNC)  // experiment only: no L2 invalidate (incorrect across XCDs)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
       }
       const int sbi = k * J.nsbh + l;
       sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
       sb.bits.cap = THOR_ENC_SB_WORDS * 32;
-      te_encode_sb(J.F, S, sb, k, l);
+      te_encode_sb(s_F, S, sb, k, l);
       if (lane == 0) {
         J.sb_nbits[sbi] = sb.bits.pos;
         if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
       }
-#if defined(THOR_ENC_EXP_NOSYNC)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#else
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) __hip_atomic_store(&J.progress[k], (unsigned)(l + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -290,7 +292,6 @@ struct EncPool {
   int device = -1;
   size_t nwork = 0;
   TeScratchMem *scratch = nullptr;
-  TeSB *sbs = nullptr;
   unsigned *ticket = nullptr, *err = nullptr;
   TeJob *jobs = nullptr;
   long long *scan = nullptr;
@@ -309,10 +310,7 @@ static int pool_reserve(int device, size_t nwork, size_t scan_n) {
   }
   if (nwork > g_pool.nwork) {
     if (g_pool.scratch) (void)hipFree(g_pool.scratch);
-    if (g_pool.sbs) (void)hipFree(g_pool.sbs);
     EHIP(hipMalloc(&g_pool.scratch, nwork * sizeof(TeScratchMem)));
-    EHIP(hipMalloc(&g_pool.sbs, nwork * sizeof(TeSB)));
-    EHIP(hipMemset(g_pool.sbs, 0, nwork * sizeof(TeSB)));
     g_pool.nwork = nwork;
   }
   if (scan_n > g_pool.scan_n) {
@@ -496,7 +494,7 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   }
   EHIP(hipMemcpyAsync(g_pool.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
   EHIP(hipMemsetAsync(g_pool.ticket, 0, 4, st));
-  k_enc_rows<<<nwork, 64, 0, st>>>(g_pool.jobs, n, g_pool.ticket, nrows, g_pool.scratch, g_pool.sbs, g_pool.err);
+  k_enc_rows<<<nwork, 64, 0, st>>>(g_pool.jobs, n, g_pool.ticket, nrows, g_pool.scratch, g_pool.err);
   EHIP(hipGetLastError());
   const int ncell = (W / 4) * (H / 4);
   k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(g_pool.jobs);

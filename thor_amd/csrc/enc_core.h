@@ -84,6 +84,28 @@ TE_FN int te_dv(int e, int w) {
 #endif
 }
 
+// te_lds(p): on the device, p is known to point into LDS (a worker's
+// __shared__ state handed down through a generic pointer or reference).  The
+// cast lets the compiler emit ds_* instead of flat_* accesses for it in the
+// (non-inlined) callee -- flat accesses wait on both memory counters and take
+// the vector-memory path.  Identity on the host.
+#if !defined(TE_HOST)
+template <typename T>
+__device__ __forceinline__ T *te_lds(T *p) {
+  return (T *)(__attribute__((address_space(3))) T *)p;
+}
+#else
+template <typename T>
+static inline T *te_lds(T *p) {
+  return p;
+}
+#endif
+// zero n bytes (n % 4 == 0, 4-byte aligned) with every lane
+TE_FN void te_zero_words(void *p, int n) {
+  uint32_t *w = (uint32_t *)p;
+  for (int e = TE_LANE; e < (n >> 2); e += TE_NL) w[e] = 0u;
+}
+
 // ---- 4-pixel (dword) helpers ----------------------------------------------------
 // Pixel loops that can take four horizontally adjacent pixels per lane do so:
 // one (possibly unaligned) dword load / store instead of four byte accesses,
@@ -698,10 +720,11 @@ TE_FN void te_load_scan(TeScanRegs &R, const int16_t *c, int q) {
   R.nz[3] = __ballot(R.v3 != 0);
 #endif
 }
-TE_NOINL void te_write_coeff(TeBits &bo, const int16_t *c, int size, int type, int16_t *scan /* unused */) {
+// The writer state travels by value (in registers) in and out: a reference
+// would pin the caller's register copy to the stack.
+TE_NOINL TeBits te_write_coeff(TeBits b_in, const int16_t *c, int size, int type) {
   TE_P(TP_WCOEF);
-  (void)scan;
-  TeBits b = te_bits_local(bo);
+  TeBits b = te_bits_local(b_in);
   size = te_uni(size);
   type = te_uni(type);
   const int q = TE_MIN(16, size), N = q * q;
@@ -769,8 +792,19 @@ TE_NOINL void te_write_coeff(TeBits &bo, const int16_t *c, int size, int type, i
       else te_put_vlc(b, 2, cn + 1);
     }
   }
-  bo = b;
+  return b;
 }
+
+// write_block's code tables (enc/write_bits.c:385 cbp codes, :401-413 intra mode codes),
+// constant memory: a local array indexed at run time would be built on the
+// stack on every call
+TE_CONST int8_t te_wb_cbp[8] = {1, 0, 5, 2, 6, 3, 7, 4};
+TE_CONST int8_t te_wb_map8[10] = {2, 8, 1, 0, 5, 9, 7, 6, 4, 3};
+TE_CONST int8_t te_wb_len8[8] = {2, 2, 2, 4, 4, 4, 5, 5};
+TE_CONST int8_t te_wb_cw8[8] = {0, 1, 2, 12, 13, 14, 30, 31};
+TE_CONST int8_t te_wb_map10[10] = {2, 3, 1, 0, 6, 9, 8, 7, 5, 4};
+TE_CONST int8_t te_wb_len10[10] = {2, 2, 3, 3, 4, 4, 5, 5, 5, 5};
+TE_CONST int8_t te_wb_cw10[10] = {2, 3, 2, 3, 2, 3, 0, 1, 2, 3};
 
 // write_delta_qp, write_bits.c:255-265
 TE_FN void te_write_delta_qp(TeBits &b, int dqp) {
@@ -832,13 +866,18 @@ TE_FN void te_write_super_mode(TeBits &b, const TeFrame &F, const TeBlockInfo &b
 TE_FN const int16_t *te_tile(const TeParam &p, int comp, int idx) { return p.coeff + comp * TE_COEF_COMP + idx * 256; }
 
 // write_block, write_bits.c:364-650.  Returns the number of bits written.
-TE_NOINL int te_write_block(TeBits &bo, const TeFrame &F, const TeBlockInfo &bi, const TeParam &p, int16_t *scan) {
+TE_NOINL int te_write_block(TeBits &bo_, const TeFrame &F_, const TeBlockInfo &bi_, const TeParam &p_, int16_t *scan_) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeBlockInfo &bi = *te_lds(&bi_);
+  TeBits &bo = *te_lds(&bo_);
+  const TeParam &p = *te_lds(&p_);
+  (void)scan_;  // (unused: the coefficient coder keeps its scan in registers)
   TE_P(TP_WBLOCK);
   TeBits b = te_bits_local(bo);
   const int start = b.pos;
   const int size = bi.size, mode = p.mode, tb_split = p.tb_split;
   const int coeff_type = (mode == TE_INTRA) << 1;
-  const int cbp_table[8] = {1, 0, 5, 2, 6, 3, 7, 4};
+  const int8_t *cbp_table = te_wb_cbp;
   te_write_super_mode(b, F, bi, mode, p.ref_idx0, 0);
   if (size == 64 && mode != TE_SKIP && F.max_delta_qp) te_write_delta_qp(b, bi.delta_qp);
   if (mode == TE_INTRA) {
@@ -846,15 +885,11 @@ TE_NOINL int te_write_block(TeBits &bo, const TeFrame &F, const TeBlockInfo &bi,
     if (F.num_intra_modes <= 4) {
       te_put(b, 2, im);
     } else if (F.num_intra_modes <= 8) {
-      const int map[10] = {2, 8, 1, 0, 5, 9, 7, 6, 4, 3};
-      const int len[8] = {2, 2, 2, 4, 4, 4, 5, 5}, cw[8] = {0, 1, 2, 12, 13, 14, 30, 31};
-      const int code = map[im];
-      te_put(b, len[code], cw[code]);
+      const int code = te_wb_map8[im];
+      te_put(b, te_wb_len8[code], te_wb_cw8[code]);
     } else {
-      const int map[10] = {2, 3, 1, 0, 6, 9, 8, 7, 5, 4};
-      const int len[10] = {2, 2, 3, 3, 4, 4, 5, 5, 5, 5}, cw[10] = {2, 3, 2, 3, 2, 3, 0, 1, 2, 3};
-      const int code = map[im];
-      te_put(b, len[code], cw[code]);
+      const int code = te_wb_map10[im];
+      te_put(b, te_wb_len10[code], te_wb_cw10[code]);
     }
   } else if (mode == TE_INTER) {
     if (bi.max_num_pb_part > 1) {
@@ -958,9 +993,9 @@ TE_NOINL int te_write_block(TeBits &bo, const TeFrame &F, const TeBlockInfo &bi,
     }
     te_put_vlc(b, 0, code);
     if (tb_split == 0) {
-      if (p.cbp_y) te_write_coeff(b, te_tile(p, 0, 0), size, coeff_type | 0, scan);
-      if (p.cbp_u) te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1, scan);
-      if (p.cbp_v) te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1, scan);
+      if (p.cbp_y) b = te_write_coeff(b, te_tile(p, 0, 0), size, coeff_type | 0);
+      if (p.cbp_u) b = te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1);
+      if (p.cbp_v) b = te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1);
     } else if (size > 8) {
       for (int index = 0; index < 4; index++) {
         const int cy = (p.cbp_y >> (3 - index)) & 1, cu = (p.cbp_u >> (3 - index)) & 1,
@@ -968,15 +1003,15 @@ TE_NOINL int te_write_block(TeBits &bo, const TeFrame &F, const TeBlockInfo &bi,
         code = cbp_table[cy + (cu << 1) + (cv << 2)];
         if (bi.ctx.cbp == 0 && code < 2) code = 1 - code;
         te_put_vlc(b, 0, code);
-        if (cy) te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0, scan);
-        if (cu) te_write_coeff(b, te_tile(p, 1, index), size / 4, coeff_type | 1, scan);
-        if (cv) te_write_coeff(b, te_tile(p, 2, index), size / 4, coeff_type | 1, scan);
+        if (cy) b = te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0);
+        if (cu) b = te_write_coeff(b, te_tile(p, 1, index), size / 4, coeff_type | 1);
+        if (cv) b = te_write_coeff(b, te_tile(p, 2, index), size / 4, coeff_type | 1);
       }
     } else {
       for (int index = 0; index < 4; index++) {
         const int cy = (p.cbp_y >> (3 - index)) & 1;
         te_put(b, 1, cy);
-        if (cy) te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0, scan);
+        if (cy) b = te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0);
       }
       // chroma of an 8x8 CU is not split: cbp_u / cbp_v are the block values here
       const int cbp = p.cbp_u + 2 * p.cbp_v;
@@ -984,8 +1019,8 @@ TE_NOINL int te_write_block(TeBits &bo, const TeFrame &F, const TeBlockInfo &bi,
       else if (cbp == 1) te_put(b, 2, 1);
       else if (cbp == 2) te_put(b, 3, 1);
       else te_put(b, 3, 0);
-      if (p.cbp_u) te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1, scan);
-      if (p.cbp_v) te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1, scan);
+      if (p.cbp_u) b = te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1);
+      if (p.cbp_v) b = te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1);
     }
   }
   bo = b;

@@ -312,11 +312,12 @@ TE_FN uint32_t te_ssd(const uint8_t *a, int as, const uint8_t *b, int bs, int w,
   return te_sum(s);
 }
 
+TE_CONST int8_t te_wide_off[5] = {-3, -1, 0, 1, 3};
 // widesad_calc, enc/encode_block.c:757-780 (its SIMD form widesad_calc_simd,
 // enc/enc_kernels.c:71-98, keeps the first minimum too): SAD at horizontal
 // offsets -3, -1, 0, 1, 3; returns the best, *x = its offset.
 TE_FN uint32_t te_widesad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h, int *x) {
-  const int off[5] = {-3, -1, 0, 1, 3};
+  const int8_t *off = te_wide_off;
   uint32_t s[5] = {0, 0, 0, 0, 0};
   if ((w & 3) == 0) {  // b columns j-4..j+7 as three dwords, the five offsets by byte alignment
     const int w4 = w >> 2, n4 = w4 * h;

@@ -15,6 +15,8 @@ struct TeLevel {             // one quadtree level (64, 32, 16, 8)
 };
 struct TeScratchMem {         // global memory, one per worker wave
   TeLevel lv[4];
+  TeBlockInfo bi[4];                 // (host build: the per-level block state; LDS on the device)
+  TeParam tmp;                       // (host build: the candidate parameters; LDS on the device)
   uint8_t pb0[TE_BLK], pb1[TE_BLK];  // bi-pred legs (Y | U | V, compact)
   uint8_t org8[64 * 64];             // bi-pred search target (search_bipred_prediction_params)
   uint8_t rf[64 * 64];               // exact sub-pel ME prediction
@@ -29,8 +31,10 @@ struct TeScratch {
   uint8_t *pb, *pb0, *pb1, *org8, *rf;
   TeTx *tx;
   TeNbr *nb;
+  TeBlockInfo *bi;  // [4], one per quadtree level (the recursion's block_info)
+  TeParam *tmp;     // the candidate of mode_decision / search_early_skip (never live at once)
 };
-TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb) {
+TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb, TeBlockInfo *bi, TeParam *tmp) {
   TeScratch S;
   S.lv = M.lv;
   S.pb = pb;
@@ -40,6 +44,17 @@ TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb) {
   S.rf = M.rf;
   S.tx = tx;
   S.nb = nb;
+  S.bi = bi;
+  S.tmp = tmp;
+  return S;
+}
+// a callee's view of the scratch: the LDS members re-declared as LDS
+TE_FN TeScratch te_local(TeScratch S) {
+  S.pb = te_lds(S.pb);
+  S.tx = te_lds(S.tx);
+  S.nb = te_lds(S.nb);
+  S.bi = te_lds(S.bi);
+  S.tmp = te_lds(S.tmp);
   return S;
 }
 // State of the superblock being encoded (frame_info mvcand / best_ref are
@@ -205,8 +220,11 @@ TE_FN void te_recon(uint8_t *rec, int rs, const uint8_t *pb, int ps, const TeTx 
 // encode_and_reconstruct_block_inter, enc/encode_block.c:1469-1532, one
 // component: orig (frame, stride os) - pred -> levels (tiles of `coef`) ->
 // rec (compact, stride size).  Returns cbp (4-bit mask when tb-split).
-TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch S, const uint8_t *org, int os, int size, int qp,
-                               const uint8_t *pb, int16_t *coef, uint8_t *rec, int type, int tb_split) {
+TE_NOINL int te_enc_inter_comp(const TeFrame &F_, TeScratch S_, const uint8_t *org, int os, int size, int qp,
+                               const uint8_t *pb_, int16_t *coef, uint8_t *rec, int type, int tb_split) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  const uint8_t *pb = te_lds(pb_);
   TE_P(TP_INTER_COMP);
   TeTx &X = *S.tx;
   int cbp = 0;
@@ -246,9 +264,12 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F, TeScratch S, const uint8_t *org
 
 // encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
 // component.  rf / fs: the frame being reconstructed at the CU origin.
-TE_NOINL int te_enc_intra_comp(const TeFrame &F, TeScratch S, const uint8_t *org, int os, const uint8_t *rf, int fs,
-                               int ypos, int xpos, int size, int qp, uint8_t *pb, int16_t *coef, uint8_t *rec, int type,
+TE_NOINL int te_enc_intra_comp(const TeFrame &F_, TeScratch S_, const uint8_t *org, int os, const uint8_t *rf, int fs,
+                               int ypos, int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
                                int tb_split, int mode, int ur, int dl) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  uint8_t *pb = te_lds(pb_);
   TE_P(TP_INTRA_COMP);
   TeTx &X = *S.tx;
   const int fast = F.speed > 1;
@@ -329,7 +350,12 @@ TE_FN void te_put_kept(TeBits &b, const uint32_t *w, int nbits) {
 
 // encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
 // bi.rec, write the block's syntax.  Returns the bit count.
-TE_NOINL int te_encode_block(const TeFrame &F, TeScratch S, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+TE_NOINL int te_encode_block(const TeFrame &F_, TeScratch S_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeBlockInfo &bi = *te_lds(&bi_);
+  TeBits &b = *te_lds(&b_);
+  TeParam &p = *te_lds(&p_);
   TE_P(TP_ENC_BLOCK);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, yC = ypos / 2, xC = xpos / 2, sC = size / 2;
   const int mode = p.mode;
@@ -419,15 +445,25 @@ TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *r
   return cost;
 }
 
+// search orders (constant memory: local arrays indexed at run time would be
+// built on the stack on every call)
+TE_CONST int8_t te_intra_order[10] = {TE_DC,      TE_HOR,       TE_VER,       TE_PLANAR,     TE_UPLEFT,
+                                      TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT, TE_UPLEFTLEFT, TE_DOWNLEFTLEFT};
+TE_CONST int8_t te_hex_dy[6] = {1, 2, 1, -1, -2, -1}, te_hex_dx[6] = {-1, 0, 1, 1, 0, -1};  // enc/encode_block.c:908-909
+TE_CONST int8_t te_hp_m[9] = {0, 0, -2, 2, 0, -2, -2, 2, 2}, te_hp_n[9] = {0, -2, 0, 0, 2, -2, 2, -2, 2};  // :942-943
+TE_CONST int8_t te_qp_m[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, te_qp_n[9] = {0, -1, 0, 0, 1, -1, 1, -1, 1};
+
 // search_intra_prediction_params, enc/encode_block.c:1230-1329: SAD over the
 // first `num_modes` modes in the order DC, HOR, VER, PLANAR, [UPLEFT ...].
-TE_NOINL int te_search_intra(const TeFrame &F, TeScratch S, const TeBlockInfo &bi, int num_modes, int *mode_out) {
+TE_NOINL int te_search_intra(const TeFrame &F_, TeScratch S_, const TeBlockInfo &bi_, int num_modes, int *mode_out) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  const TeBlockInfo &bi = *te_lds(&bi_);
   TE_P(TP_SEARCH_INTRA);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
   const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
   te_make_top_and_left(*S.nb, F.ry + ypos * F.rsy + xpos, F.rsy, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
-  const int order[10] = {TE_DC, TE_HOR, TE_VER, TE_PLANAR, TE_UPLEFT, TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT,
-                         TE_UPLEFTLEFT, TE_DOWNLEFTLEFT};
+  const int8_t *order = te_intra_order;
   int min_sad = 1 << 30, best = TE_DC;
   const int n = num_modes == 4 ? 4 : 10;
   const uint8_t *o = F.oy + ypos * F.osy + xpos;
@@ -473,9 +509,12 @@ TE_FN uint32_t te_lambda_bits(double lam, int bits) { return (uint32_t)(lam * (d
 // motion_estimate, enc/encode_block.c:830-1016 (params->sync = 0).  `org` /
 // `os`: the block (or partition) of the original; `ref`: the reference at the
 // block (partition) origin; size: the CU size (clip_mv, the size-16 rules).
-TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, int r, const uint8_t *org, int os,
+TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeScratch S_, TeSB &sb_, int r, const uint8_t *org, int os,
                                      const uint8_t *ref, int size, int width, int height, TeMv *mv, TeMv mvc, TeMv mvp,
                                      int sign, int xpos, int ypos, int enable_bipred) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeSB &sb = *te_lds(&sb_);
   TE_P(TP_ME);
   const int rs = F.rsy, s = sign ? -1 : 1;
   const double lam = F.sqrt_lambda;
@@ -532,7 +571,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, in
   const int maxsteps = size <= 16 || F.speed == 0 ? 6 : 0;
   int start = 0, end = 5;
   for (int step = 1; step < maxsteps; step++) {  // full-pel hexagon search
-    const int diy[6] = {1, 2, 1, -1, -2, -1}, dix[6] = {-1, 0, 1, 1, 0, -1};
+    const int8_t *diy = te_hex_dy, *dix = te_hex_dx;
     int dir = start - 1, best_dir = -1;
     do {
       dir++;
@@ -559,7 +598,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, in
   int ydelta_hp = 0, xdelta_hp = 0, ydelta_qp = 0, xdelta_qp = 0;
   uint32_t cmin = min_sad;
   if (F.speed == 0) {  // exact half- and quarter-pel search through the MC filters
-    const int hm[9] = {0, 0, -2, 2, 0, -2, -2, 2, 2}, hn[9] = {0, -2, 0, 0, 2, -2, 2, -2, 2};
+    const int8_t *hm = te_hp_m, *hn = te_hp_n;
     for (int i = 1; i <= 8; i++) {
       c.y = (int16_t)(mv_ref.y + hm[i]);
       c.x = (int16_t)(mv_ref.x + hn[i]);
@@ -574,7 +613,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F, TeScratch S, TeSB &sb, in
     }
     mv_opt.x = (int16_t)(mv_opt.x + xdelta_hp);
     mv_opt.y = (int16_t)(mv_opt.y + ydelta_hp);
-    const int qm[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, qn[9] = {0, -1, 0, 0, 1, -1, 1, -1, 1};
+    const int8_t *qm = te_qp_m, *qn = te_qp_n;
     for (int i = 1; i <= 8; i++) {
       c.y = (int16_t)(mv_opt.y + qm[i]);
       c.x = (int16_t)(mv_opt.x + qn[i]);
@@ -740,9 +779,13 @@ TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
 
 // search_bipred_prediction_params, enc/encode_block.c:2047-2202, me_mode 0
 // (the iterative uni-pred search on the modified target org8)
-TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch S, TeSB &sb, TeBlockInfo &bi, int part,
+TE_NOINL uint32_t te_search_bipred(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int part,
                                    TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_arr0,
                                    TeMv *mv_arr1) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeSB &sb = *te_lds(&sb_);
+  TeBlockInfo &bi = *te_lds(&bi_);
   const int size = bi.size;
   const int num_iter = F.speed == 0 ? 2 : 1;
   int ref_idx = (F.frame_type == TE_B && F.interp_ref == 1) ? 1 : 0;
@@ -840,7 +883,11 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
 }
 
 // mode_decision_rdo, enc/encode_block.c:2204-2479
-TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeSB &sb = *te_lds(&sb_);
+  TeBlockInfo &bi = *te_lds(&bi_);
   TE_P(TP_MODE);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
   TeBits &b = sb.bits;
@@ -851,8 +898,9 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F, TeScratch S, TeSB &sb, TeBl
   int do_inter = 1, do_intra = 1;
   int intra_mode = TE_DC;
   const int pos_ref = b.pos;
-  TeParam tmp;
-  memset(&tmp, 0, sizeof(tmp));
+  TeParam &tmp = *S.tmp;
+  te_zero_words(&tmp, sizeof(TeParam));
+  te_sync();
   tmp.coeff = tmp_coef;
   if (frame_type != TE_I) {  // skip candidates
     tmp.tb_param = 0;
@@ -1073,7 +1121,11 @@ TE_FN int te_es_chroma(const uint8_t *org, int os, int size, const uint8_t *pb, 
 }
 
 // check_early_skip_block, :2613-2741.  Returns 1 when every sub-block is insignificant.
-TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch S, const TeBlockInfo &bi, const TeParam &p) {
+TE_NOINL int te_check_early_skip(const TeFrame &F_, TeScratch S_, const TeBlockInfo &bi_, const TeParam &p_) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  const TeBlockInfo &bi = *te_lds(&bi_);
+  const TeParam &p = *te_lds(&p_);
   TE_P(TP_ES_CHECK);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, size0 = TE_MIN(size, 32);
   const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
@@ -1120,12 +1172,17 @@ TE_NOINL int te_check_early_skip(const TeFrame &F, TeScratch S, const TeBlockInf
 }
 
 // search_early_skip_candidates, :2743-2783
-TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch S, TeSB &sb, TeBlockInfo &bi, int16_t *tmp_coef) {
+TE_NOINL int te_search_early_skip(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeSB &sb = *te_lds(&sb_);
+  TeBlockInfo &bi = *te_lds(&bi_);
   TE_P(TP_ES_SEARCH);
   uint32_t min_cost = TE_MAX_UINT32;
   int early = 0;
-  TeParam tmp;
-  memset(&tmp, 0, sizeof(tmp));
+  TeParam &tmp = *S.tmp;
+  te_zero_words(&tmp, sizeof(TeParam));
+  te_sync();
   tmp.coeff = tmp_coef;
   for (int k = 0; k < bi.num_skip; k++) {
     tmp.tb_param = 0;
@@ -1154,7 +1211,10 @@ TE_NOINL int te_search_early_skip(const TeFrame &F, TeScratch S, TeSB &sb, TeBlo
 // Template over the CU size: the quadtree recursion unrolls at compile time
 // (64 -> 32 -> 16 -> 8); level L = log2(64 / SIZE) owns TeScratch::lv[L].
 template <int SIZE>
-TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch S, TeSB &sb, int ypos, int xpos, int qp) {
+TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, int ypos, int xpos, int qp) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeSB &sb = *te_lds(&sb_);
   constexpr int L = SIZE == 64 ? 0 : (SIZE == 32 ? 1 : (SIZE == 16 ? 2 : 3));
   const int W = F.W, H = F.H, ft = F.frame_type;
   if (ypos >= H || xpos >= W) return 0;
@@ -1167,8 +1227,9 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F, TeScratch S, TeSB &sb, int 
   TeBits &b = sb.bits;
   const int pos_ref = b.pos;
   TeLevel &lv = S.lv[L];
-  TeBlockInfo bi;
-  memset(&bi, 0, sizeof(bi));
+  TeBlockInfo &bi = S.bi[L];
+  te_zero_words(&bi, sizeof(TeBlockInfo));
+  te_sync();
   bi.ctx = te_block_ctx(ypos, xpos, H, W, SIZE, F.cells, F.use_block_contexts);
   bi.size = SIZE;
   bi.bwidth = TE_MIN(SIZE, W - xpos);
