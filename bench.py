@@ -430,7 +430,9 @@ def main():
             _, frames = parse_stream(bits[j])
             return [decs[k].upload(fr, pools[k][i]) for i, fr in enumerate(frames)]
 
+        t0 = time.perf_counter()
         devs = list(pool.map(host, range(len(ks))))
+        dec_host_s[0] += time.perf_counter() - t0
         gs = [[j for j, k in enumerate(ks) if k in gk] for gk in groups]
         for i in range(nf):
             for g in gs:
@@ -439,6 +441,8 @@ def main():
         for k in ks:
             decs[k].sync()
         return devs
+
+    dec_host_s = [0.0]  # parse + upload share of t_dec (timed steps)
 
     def step(ks):
         t0 = time.perf_counter()
@@ -461,6 +465,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(local)
     t_enc = t_dec = 0.0
+    dec_host_s[0] = 0.0
     enc_frame_ms = [0.0] * nf
     for _ in range(a.steps):
         te, td, bits, devs, fms = step(allk)
@@ -469,6 +474,7 @@ def main():
         enc_frame_ms = [x + y / a.steps for x, y in zip(enc_frame_ms, fms)]
         bit_exact &= all(b == want_bit for b in bits)
     torch.cuda.synchronize(local)
+    dec_host_ms = dec_host_s[0] / a.steps * 1e3
     elapsed = t_enc + t_dec
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda")
@@ -528,6 +534,9 @@ def main():
                 "streams_per_gpu": K,
                 "t_enc_ms_per_step": round(t_enc / a.steps * 1e3, 2),
                 "t_dec_ms_per_step": round(t_dec / a.steps * 1e3, 2),
+                "t_dec_host_ms_per_step": round(dec_host_ms, 2),
+                "t_dec_host_note": "host parse (thor_parse_frame) + upload of the parse output, %d threads; "
+                                   "the rest of t_dec is the GPU reconstruction" % HOST_THREADS,
                 "enc_mpx_s": round(K * px_stream * a.steps / t_enc / 1e6, 2),
                 "dec_mpx_s": round(K * px_stream * a.steps / t_dec / 1e6, 2),
                 "enc_batch_frame_ms": [round(x, 2) for x in enc_frame_ms],

@@ -119,12 +119,21 @@ class GpuDecoder:
         clist = np.zeros(max(n_clpf, 1), np.uint32)
         if flags.size:
             self.lib.thor_build_clpf_list(flags.ctypes.data, len(flags), clist.ctypes.data)
-        bb, cb, fb = self._buf(blocks, pool, 0), self._buf(coeffs, pool, 1), self._buf(flags, pool, 2)
-        ib, tb, lb = self._buf(ilist, pool, 3), self._buf(tlist, pool, 4), self._buf(clist, pool, 5)
+        # one host image, one device buffer, one copy (256-byte aligned parts)
+        parts = [blocks, coeffs, flags, ilist, tlist, clist]
+        offs, o = [], 0
+        for a in parts:
+            offs.append(o)
+            o += (a.nbytes + 255) & ~255
+        img = np.zeros(max(o, 256), np.uint8)
+        for a, off in zip(parts, offs):
+            img[off:off + a.nbytes] = a.view(np.uint8).reshape(-1)
+        base = self._buf(img, pool, 0).ptr
+        bp, cp, fp, ip, tp, lp = (base + off for off in offs)
         hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
         nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + TU_DTYPE.itemsize * n_tu
-        return DeviceFrame(hdr, bb.ptr, len(blocks), cb.ptr, fb.ptr if flags.size else 0, ib.ptr, n_intra, tb.ptr,
-                           n_tu, lb.ptr, n_clpf, nbytes)
+        return DeviceFrame(hdr, bp, len(blocks), cp, fp if flags.size else 0, ip, n_intra, tp, n_tu, lp, n_clpf,
+                           nbytes)
 
     def decode(self, d: DeviceFrame):
         fi = self.frame_in(d)
