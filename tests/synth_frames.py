@@ -6,7 +6,10 @@ every MC fraction, CU size 8..64, quadtree split pattern, mode (SKIP with
 rectangular frame-edge clipping, MERGE, INTER with four quarter MVs, BIPRED,
 bi-directional SKIP/MERGE), reference choice (past and future: the `sign`
 negation), tb_split and qp -- cases the reference-encoded streams hit only
-sparsely.  The descriptor semantics follow block_info_dec_t as read by
+sparsely.  With INTRA in `modes`, intra CUs of every mode (DC, HOR, VER,
+PLANAR and the six angular modes, common/intra_prediction.c:145-388) and size,
+with and without tb-split, anywhere in the frame (so at every availability
+pattern of the frame edges and of the quadtree).  The descriptor semantics follow block_info_dec_t as read by
 read_block (dec/read_bits.c:221); see thor_amd/trace.py for the layout."""
 from __future__ import annotations
 
@@ -45,7 +48,7 @@ def _leaves(rng, y, x, size, W, H, split_p):
 
 
 def synth_frame(rng, W, H, frame_num, ref_nums, coeff_p=0.0, split_p=0.35, mv_range=48,
-                modes=(SKIP, MERGE, INTER, BIPRED)):
+                modes=(SKIP, MERGE, INTER, BIPRED), frame_type=1):
     blocks = []
     pool = []
     pool_len = 0
@@ -58,16 +61,23 @@ def synth_frame(rng, W, H, frame_num, ref_nums, coeff_p=0.0, split_p=0.35, mv_ra
                 mode = SKIP if not inside else int(rng.choice(modes))
                 r["mode"] = mode
                 r["qp"] = int(rng.integers(18, 46))
+                if mode == INTRA:
+                    r["intra_mode"] = int(rng.integers(0, 10))
                 q_mvs = 4 if mode in (INTER, BIPRED) else 1
                 mv0 = rng.integers(-mv_range, mv_range + 1, (q_mvs, 2))
                 mv1 = rng.integers(-mv_range, mv_range + 1, (q_mvs, 2))
                 if q_mvs == 1:
                     mv0 = np.repeat(mv0, 4, 0)
                     mv1 = np.repeat(mv1, 4, 0)
+                if mode == INTRA:
+                    mv0[...] = 0
+                    mv1[...] = 0
                 r["mv0"] = mv0.reshape(-1)
                 r["mv1"] = mv1.reshape(-1)
                 r["ref0"] = int(rng.choice(ref_nums))
                 bi = mode == BIPRED or (mode in (SKIP, MERGE) and rng.random() < 0.3)
+                if mode == INTRA:
+                    r["ref0"] = ref_nums[0]
                 r["dir"] = 2 if (bi and mode != BIPRED) else 0
                 r["ref1"] = int(rng.choice(ref_nums)) if bi else r["ref0"]
                 cmask = 0
@@ -93,4 +103,4 @@ def synth_frame(rng, W, H, frame_num, ref_nums, coeff_p=0.0, split_p=0.35, mv_ra
                 blocks.append(r)
     coeffs = np.concatenate(pool).astype(np.int16) if pool else np.zeros(0, np.int16)
     b = np.array(blocks, dtype=BLOCK_DTYPE)
-    return Frame(0, frame_num, 1, int(rng.integers(22, 40)), len(ref_nums), 0, b, coeffs)
+    return Frame(0, frame_num, frame_type, int(rng.integers(22, 40)), len(ref_nums), 0, b, coeffs)

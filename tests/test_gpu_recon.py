@@ -60,3 +60,48 @@ def test_recon_matches_oracle_on_synthetic_frames(case, seed):
                 assert bad.size == 0, (CASES[case], seed, stage, name, len(bad), bad[:4].tolist())
     finally:
         gdec.close()
+
+
+INTRA_CASES = [
+    # W, H, frame_type, modes, coeff_p, split_p
+    (256, 128, 0, ("INTRA",), 0.7, 0.5),           # I frame: every CU intra, frame edges on all sides
+    (352, 136, 1, ("SKIP", "INTRA", "INTER"), 0.6, 0.5),  # intra CUs among inter ones, ragged right/bottom
+    (320, 192, 1, ("INTRA", "MERGE"), 0.3, 0.8),   # mostly 8x8 / 16x16 intra next to merges
+]
+
+
+@pytest.mark.parametrize("case", range(len(INTRA_CASES)))
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_intra_cus_match_oracle(case, seed):
+    """k_intra's WPP chains on synthetic intra CUs: all ten modes, sizes 8..64,
+    tb-split, every neighbour-availability pattern the quadtree and the frame
+    edges produce (common/intra_prediction.c:57-388, common/common_block.c:100-129)."""
+    import synth_frames as sf
+    from oracle import OracleDecoder
+    from thor_amd.decoder import GpuDecoder
+
+    W, H, ftype, mnames, coeff_p, split_p = INTRA_CASES[case]
+    modes = tuple(getattr(sf, m) for m in mnames)
+    rng = np.random.default_rng(7000 + 10 * case + seed)
+    seq = SeqParams(W, H, 0, 1, 2, 0, 0, 1, 0, 1, 0)
+    gdec, odec = GpuDecoder(seq), OracleDecoder(seq)
+    try:
+        refs = [0]
+        for r in refs:
+            planes = random_frame(rng, W, H)
+            gdec.write(r, *planes)
+            _oracle_ref(odec, r, planes)
+        fr = synth_frame(rng, W, H, 1, refs, coeff_p=coeff_p, split_p=split_p, modes=modes, frame_type=ftype)
+        assert (fr.blocks["mode"] == sf.INTRA).any()
+        dev = gdec.upload(fr)
+        for stage in (0, 1):
+            gdec.set_stop_stage(stage)
+            gdec.decode(dev)
+            gdec.sync()
+            got = gdec.read(1)
+            want = odec.decode(fr, stage).planes()
+            for name, g, o in zip("YUV", got, want):
+                bad = np.argwhere(g != o)
+                assert bad.size == 0, (INTRA_CASES[case], seed, stage, name, len(bad), bad[:4].tolist())
+    finally:
+        gdec.close()
