@@ -43,7 +43,9 @@ def load(build: bool = True):
     if _lib is not None:
         return _lib
     path = os.path.join(HERE, "liboracle.so")
-    if build and (not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(os.path.join(HERE, "thor_oracle.c"))):
+    srcs = ("thor_oracle.c", "thor_oracle_ti.c", "thor_oracle.h")
+    if build and (not os.path.exists(path) or
+                  os.path.getmtime(path) < max(os.path.getmtime(os.path.join(HERE, f)) for f in srcs)):
         subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
     _lib = C.CDLL(path)
     P = C.c_void_p
@@ -74,6 +76,11 @@ def load(build: bool = True):
     _lib.or_scale_down2x2.argtypes = [P, i, P, i, i, i]
     _lib.or_pad_plane.argtypes = [P, i, i, i, i]
     _lib.or_interp_comp.argtypes = [P, i, P, i, P, i, P, P] + [i] * 9
+    _lib.or_ti_levels.argtypes = [i, i]
+    _lib.or_ti_levels.restype = i
+    _lib.or_interpolate_frames.argtypes = [C.POINTER(OrFrame), C.POINTER(OrFrame), i, C.POINTER(OrFrame), i, i, i, i,
+                                           P, P]
+    _lib.or_interpolate_frames.restype = i
     return _lib
 
 
@@ -111,6 +118,47 @@ class PaddedFrame:
 
     def i420(self) -> bytes:
         return b"".join(np.ascontiguousarray(p).tobytes() for p in self.planes())
+
+
+def ti_block_grid(width: int, height: int, level: int):
+    """alloc_mv_data's (bw, bh) at a pyramid level (common/temporal_interp.c:97-99)."""
+    w, h = width >> level, height >> level
+    return 2 * ((w + 15) // 16), 2 * ((h + 15) // 16)
+
+
+def interpolate_frames(ref0: "PaddedFrame", ref1: "PaddedFrame", ratio: int, pos: int, levels: bool = False):
+    """The oracle's interpolate_frames (thor_oracle_ti.c): the interpolated frame,
+    padded (pad_yuv_frame, dec/decode_frame.c:107); with levels=True also the
+    final (mv0, mv1) block-vector fields of every level, level 0 first."""
+    L = load()
+    w, h = ref0.w, ref0.h
+    out = PaddedFrame(w, h)
+    nl = L.or_ti_levels(w, h)
+    fields = []
+    p0 = (C.c_void_p * 4)()
+    p1 = (C.c_void_p * 4)()
+    for lv in range(max(nl, 0)):
+        bw, bh = ti_block_grid(w, h, lv)
+        f0, f1 = np.zeros((bh, bw, 2), np.int16), np.zeros((bh, bw, 2), np.int16)
+        fields.append((f0, f1))
+        p0[lv], p1[lv] = ptr(f0), ptr(f1)
+    a, b, o = ref0.c(), ref1.c(), out.c()
+    rc = L.or_interpolate_frames(C.byref(a), C.byref(b), PAD_Y, C.byref(o), w, h, ratio, pos,
+                                 C.cast(p0, C.c_void_p), C.cast(p1, C.c_void_p))
+    if rc != 0:
+        raise RuntimeError("or_interpolate_frames failed: %d" % rc)
+    L.or_pad_frame(C.byref(o), w, h, PAD_Y, PAD_C)
+    return (out, fields) if levels else out
+
+
+def padded_from_planes(y, u, v, frame_num: int = -1) -> "PaddedFrame":
+    f = PaddedFrame(y.shape[1], y.shape[0])
+    fy, fu, fv = f.planes()
+    fy[:], fu[:], fv[:] = y, u, v
+    f.frame_num = frame_num
+    c = f.c()
+    load().or_pad_frame(C.byref(c), f.w, f.h, PAD_Y, PAD_C)
+    return f
 
 
 class OracleDecoder:

@@ -76,6 +76,15 @@ void or_pad_plane(uint8_t *p, int s, int w, int h, int pad);
 void or_interp_comp(const uint8_t *p0, int s0, const uint8_t *p1, int s1, uint8_t *out, int so, const int16_t *mv0,
                     const int16_t *mv1, int bw, int bh, int bs, int wP, int hP, int pad, int chroma, int wt0, int wt1);
 
+/* temporal-interpolated reference frame: interpolate_frames (common/temporal_interp.c:972-1053),
+ * thor_oracle_ti.c.  ref0/ref1: padded frames (luma pad pad_y); out: the interpolated frame's
+ * planes (written over 16*ceil(w/16) x 16*ceil(h/16), i.e. into out's padding).  lv_mv0/lv_mv1:
+ * optional per-level outputs of the final block-vector fields (bw*bh int16 pairs, level 0 first). */
+int or_ti_levels(int width, int height);
+void or_ti_weights(int ratio, int pos, int *wt0, int *wt1, int *reversed);
+int or_interpolate_frames(const or_frame_t *ref0, const or_frame_t *ref1, int pad_y, or_frame_t *out, int width,
+                          int height, int ratio, int pos, int16_t *const *lv_mv0, int16_t *const *lv_mv1);
+
 struct or_frame;
 void or_deblock_cells(struct or_frame *f, const or_cell_t *cells, int W, int H, int qp);
 void or_clpf_cells(struct or_frame *f, const or_cell_t *cells, int W, int H, const uint8_t *flags);
