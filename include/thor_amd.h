@@ -52,7 +52,9 @@ typedef struct thor_block {
   uint8_t rsv[3];
   int16_t mv0[8];           /* mv_arr0[4] as (x, y) pairs, quarter-pel luma    */
   int16_t mv1[8];           /* mv_arr1[4]                                      */
-  int32_t ref0, ref1;       /* display frame_num of the reference (-1 none)    */
+  int32_t ref0, ref1;       /* display frame_num of the reference (-1 none, -2 the
+                               frame's temporal-interpolated reference,
+                               dec/decode_block.c:249: interp_frames[0])     */
   uint32_t coeff_off[3];    /* int16 offset of each component in the frame's
                                compact coefficient pool                        */
 } thor_block_t;
@@ -70,6 +72,9 @@ typedef struct thor_seq {
   int32_t deblocking;  /* dec/maindec.c:144 */
   int32_t clpf;        /* dec/maindec.c:145 */
   int32_t tb_split_enable;
+  int32_t interp_ref;  /* sequence may use temporal-interpolated references
+                          (dec/maindec.c:140): the decoder then keeps an
+                          interpolation slot and its motion-search scratch  */
 } thor_seq_t;
 
 typedef struct thor_frame_hdr {
@@ -77,6 +82,13 @@ typedef struct thor_frame_hdr {
   int32_t frame_type;  /* 0 I, 1 P, 2 B */
   int32_t qp;          /* frame qp: drives deblocking (dec/decode_frame.c:124-128) */
   int32_t clpf_on;     /* CLPF signalled on for this frame (dec/decode_frame.c:130) */
+  /* temporal-interpolated reference (dec/decode_frame.c:91-109): when
+   * interp_ratio > 0 the frame's ref index 0 is interpolate_frames(ref_a,
+   * ref_b, interp_ratio, interp_pos) of the resident frames numbered
+   * interp_ref[0] (ref_array[1]) and interp_ref[1] (ref_array[2]); blocks name
+   * it as reference -2.  interp_ratio 0: no interpolated reference. */
+  int32_t interp_ref[2];
+  int32_t interp_ratio, interp_pos;
 } thor_frame_hdr_t;
 
 /* One coded transform block of a frame (thor_build_tu_list): everything the
@@ -358,6 +370,32 @@ typedef struct thor_interp_plane {
 } thor_interp_plane_t;
 int thor_interp_frame(const thor_interp_plane_t *planes, const int16_t *mv0, const int16_t *mv1, int bw, int bh,
                       int width, int height, int wt0, int wt1, void *stream);
+
+/* ---- temporal-interpolated reference frame (interpolate_frames) ----------- *
+ * The whole of interpolate_frames (common/temporal_interp.c:972-1053) on the
+ * GPU: both references' luma pyramids, motion_estimate_bi per level (:852-918;
+ * its raster-order search pass as a wavefront of step rows, then the merge
+ * pass) and interpolate_frame (:946-970).  A context holds the scratch for one
+ * frame size (pyramid levels, per-level vector fields).                       */
+typedef struct thor_ti thor_ti_t;
+typedef struct thor_yuv_planes {
+  uint8_t *y, *u, *v; /* interior (0,0) of each plane, DEVICE pointers */
+  int32_t stride_y, stride_c;
+} thor_yuv_planes_t;
+thor_ti_t *thor_ti_create(int width, int height, int device);
+void thor_ti_destroy(thor_ti_t *t);
+/* interpolate_frames(out, ref0, ref1, ratio, pos): ref0 / ref1 padded frames
+ * (luma padding pad_y >= 16, edge-replicated, as create_reference_frame leaves
+ * them; same strides); out's interior is written (and up to 15 columns / rows
+ * past the right and bottom edges), not padded.  Enqueued on `stream`. */
+int thor_interpolate_frames(thor_ti_t *t, const thor_yuv_planes_t *ref0, const thor_yuv_planes_t *ref1, int pad_y,
+                            const thor_yuv_planes_t *out, int ratio, int pos, void *stream);
+/* Host copies of the last call's final vector field of `level` (0 = full
+ * size): bw x bh (x, y) int16 pairs each, bw = 2 * ceil((W >> level) / 16),
+ * bh likewise (alloc_mv_data, :97-99).  Synchronises the device. */
+int thor_ti_read_fields(thor_ti_t *t, int level, int16_t *mv0, int16_t *mv1);
+/* THOR_OK, or THOR_ERR_HIP if a search wavefront wait gave up (then cleared). */
+int thor_ti_status(thor_ti_t *t);
 
 /* ---- device memory helpers (so the C-ABI is usable without torch) ------ */
 void *thor_dev_alloc(size_t bytes);

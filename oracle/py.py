@@ -26,11 +26,12 @@ def plane_stride(width: int, pad: int) -> int:
 
 class ThorSeq(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("bipred", C.c_int32), ("deblocking", C.c_int32),
-                ("clpf", C.c_int32), ("tb_split_enable", C.c_int32)]
+                ("clpf", C.c_int32), ("tb_split_enable", C.c_int32), ("interp_ref", C.c_int32)]
 
 
 class ThorFrameHdr(C.Structure):
-    _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32)]
+    _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32),
+                ("interp_ref", C.c_int32 * 2), ("interp_ratio", C.c_int32), ("interp_pos", C.c_int32)]
 
 
 class OrFrame(C.Structure):
@@ -167,15 +168,28 @@ class OracleDecoder:
     def __init__(self, seq):
         self.lib = load()
         self.seq = seq
-        self.cseq = ThorSeq(seq.width, seq.height, seq.bipred, seq.deblocking, seq.clpf, seq.tb_split_enable)
+        self.cseq = ThorSeq(seq.width, seq.height, seq.bipred, seq.deblocking, seq.clpf, seq.tb_split_enable,
+                            getattr(seq, "interp_ref", 0))
         self.refs: list[PaddedFrame] = []  # newest first, like decoder_info->ref[]
 
     def decode(self, fr, stop_stage: int = 2) -> PaddedFrame:
         cur = PaddedFrame(self.seq.width, self.seq.height)
         cur.frame_num = fr.frame_num
-        hdr = ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
-        nref = len(self.refs)
-        arr = (OrFrame * max(1, nref))(*[r.c() for r in self.refs])
+        ratio = getattr(fr, "interp_ratio", 0)
+        refs = list(self.refs)
+        if ratio > 0:  # the temporal-interpolated reference, named -2 by the blocks (dec/decode_frame.c:91-109)
+            ra = [r for r in self.refs if r.frame_num == fr.interp_refs[0]]
+            rb = [r for r in self.refs if r.frame_num == fr.interp_refs[1]]
+            if not ra or not rb:
+                raise RuntimeError("interpolated reference from a frame that is not resident")
+            it = interpolate_frames(ra[0], rb[0], ratio, fr.interp_pos)
+            it.frame_num = -2
+            refs.append(it)
+            self.last_interp = it
+        hdr = ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on,
+                           (C.c_int32 * 2)(*getattr(fr, "interp_refs", (-1, -1))), ratio, getattr(fr, "interp_pos", 0))
+        nref = len(refs)
+        arr = (OrFrame * max(1, nref))(*[r.c() for r in refs])
         blocks = np.ascontiguousarray(fr.blocks)
         coeffs = np.ascontiguousarray(fr.coeffs) if fr.coeffs.size else np.zeros(1, np.int16)
         flags = np.ascontiguousarray(fr.clpf_flags) if fr.clpf_flags.size else np.zeros(1, np.uint8)

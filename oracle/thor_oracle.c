@@ -797,8 +797,11 @@ int or_decode_frame(const thor_seq_t *seq, const thor_frame_hdr_t *hdr, or_frame
       int bi_dir = (b->mode == 3) || ((b->mode == 0 || b->mode == 4) && b->dir == 2);
       const or_frame_t *r1 = bi_dir ? find_ref(refs, nrefs, b->ref1) : NULL;
       if (!r0 || (bi_dir && !r1)) { err = THOR_ERR_REF; break; }
-      int sign0 = bi_dir ? (b->ref0 >= hdr->frame_num) : (b->ref0 > hdr->frame_num);
-      int sign1 = bi_dir ? (b->ref1 >= hdr->frame_num) : 0;
+      /* the interpolated reference (-2) carries the current frame's number
+       * (dec/decode_frame.c:108), so its `sign` compares equal */
+      const int fn0 = b->ref0 == -2 ? hdr->frame_num : b->ref0, fn1 = b->ref1 == -2 ? hdr->frame_num : b->ref1;
+      int sign0 = bi_dir ? (fn0 >= hdr->frame_num) : (fn0 > hdr->frame_num);
+      int sign1 = bi_dir ? (fn1 >= hdr->frame_num) : 0;
       int quarters = (b->mode == 2 || b->mode == 3);
       int pw = b->mode == 0 ? b->bwidth : S, ph = b->mode == 0 ? b->bheight : S;
       for (int leg = 0; leg < (bi_dir ? 2 : 1); leg++) {

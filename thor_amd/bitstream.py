@@ -57,7 +57,8 @@ class Parser:
             np.zeros(0, np.uint8)
         h = out.hdr
         return Frame(out.decode_order, h.frame_num, h.frame_type, h.qp, out.num_ref, h.clpf_on, blocks, coeffs,
-                     clpf if h.clpf_on else np.zeros(0, np.uint8))
+                     clpf if h.clpf_on else np.zeros(0, np.uint8), (h.interp_ref[0], h.interp_ref[1]),
+                     h.interp_ratio, h.interp_pos)
 
     def seq(self) -> L.ThorSeq:
         s = L.ThorSeq()
@@ -71,7 +72,7 @@ def parse_stream(data: bytes):
     try:
         frames = [p.parse(c) for c in split_chunks(data)]
         s = p.seq()
-        seq = SeqParams(s.width, s.height, 0, s.tb_split_enable, 0, 0, 0, s.deblocking, s.clpf, 0, s.bipred)
+        seq = SeqParams(s.width, s.height, 0, s.tb_split_enable, 0, s.interp_ref, 0, s.deblocking, s.clpf, 0, s.bipred)
         return seq, frames
     finally:
         p.close()

@@ -65,6 +65,10 @@ struct thor_dec {
   hipEvent_t xev[2];  // cross-stream ordering when a batch mixes contexts on different streams
   int band0, band1;    // SB rows k_recon reconstructs (row sharding); band1 0 = all
   void *pending;       // Batch of a thor_dec_frame_begin awaiting its _end
+  // temporal-interpolated references (seq.interp_ref): slot `islot` after the
+  // ring holds the current frame's interpolated reference; `ti` its scratch
+  int islot;
+  thor_ti_t *ti;
   // optional per-stage timing (hipEvents on the decode stream)
   int timing;
   std::vector<hipEvent_t> ev_pool;
@@ -145,11 +149,14 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->offu = ybytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
   d->offv = ybytes + cbytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
   d->slot_bytes = ybytes + 2 * cbytes + 256;
-  if (d->slot_bytes * num_slots >= (1LL << 31)) {  // k_recon addresses the ring with 32-bit buffer offsets
+  if (d->slot_bytes * (num_slots + (seq->interp_ref ? 1 : 0)) >= (1LL << 31)) {  // k_recon addresses the ring with 32-bit buffer offsets
     delete d;
     return nullptr;
   }
   d->nslots = num_slots;
+  d->islot = seq->interp_ref ? num_slots : -1;
+  d->ti = nullptr;
+  const int alloc_slots = num_slots + (seq->interp_ref ? 1 : 0);
   d->slot_fnum.assign(num_slots, -1);
   d->slot_age.assign(num_slots, -1);
   d->decode_count = 0;
@@ -167,8 +174,9 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
   d->stream = d->own_stream;
-  ok = ok && hipMalloc(&d->slots, d->slot_bytes * num_slots) == hipSuccess;
-  ok = ok && hipMemset(d->slots, 0, d->slot_bytes * num_slots) == hipSuccess;
+  ok = ok && hipMalloc(&d->slots, d->slot_bytes * alloc_slots) == hipSuccess;
+  ok = ok && hipMemset(d->slots, 0, d->slot_bytes * alloc_slots) == hipSuccess;
+  if (ok && seq->interp_ref) ok = (d->ti = thor_ti_create(W, H, device)) != nullptr;
   size_t ncell = (size_t)(W / 4) * (H / 4);
   ok = ok && hipMalloc(&d->cellinfo, ncell * sizeof(uint16_t)) == hipSuccess;
   ok = ok && hipMalloc(&d->cellmc, ncell * sizeof(uint2)) == hipSuccess;
@@ -210,6 +218,7 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->progress) (void)hipFree(d->progress);
   if (d->resid) (void)hipFree(d->resid);
   if (d->edge) (void)hipFree(d->edge);
+  if (d->ti) thor_ti_destroy(d->ti);
   for (int i = 0; i < 2; i++)
     if (d->xev[i]) (void)hipEventDestroy(d->xev[i]);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
@@ -245,6 +254,10 @@ static int check_timeout(thor_dec *d) {
   }
   if (fl[0]) {
     fprintf(stderr, "thor_amd: intra dependency wait timed out\n");
+    return THOR_ERR_HIP;
+  }
+  if (d->ti && thor_ti_status(d->ti) != THOR_OK) {
+    fprintf(stderr, "thor_amd: interpolation search wait timed out\n");
     return THOR_ERR_HIP;
   }
   return THOR_OK;
@@ -286,7 +299,8 @@ static bool make_ctx(const thor_dec *d, int cur_slot, int frame_num, FrameCtx &f
   f.cv = cur + d->offv;
   f.slots = d->slots;
   f.slot_bytes = d->slot_bytes;
-  f.ring_bytes = d->slot_bytes * d->nslots;
+  f.ring_bytes = d->slot_bytes * (d->nslots + (d->islot >= 0 ? 1 : 0));
+  f.islot = -1;
   f.offy = d->offy;
   f.offu = d->offu;
   f.offv = d->offv;
@@ -339,6 +353,8 @@ int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, 
 struct Batch {
   FrameBatch fb;
   int n, cur[THOR_MAX_BATCH], frame_num[THOR_MAX_BATCH];
+  // interpolated reference per frame: source slots (-1: none) and interpolate_frames' (ratio, pos)
+  int ia[THOR_MAX_BATCH], ib[THOR_MAX_BATCH], iratio[THOR_MAX_BATCH], ipos[THOR_MAX_BATCH];
   int max_prep, any_intra, any_clpf, any_deblock, clpf_grid, max_intra;
 };
 
@@ -369,6 +385,17 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     b.frame_num[i] = hdrs[i].frame_num;
     FrameCtx &f = b.fb.f[i];
     if (!make_ctx(d, b.cur[i], hdrs[i].frame_num, f)) return THOR_ERR_REF;
+    b.ia[i] = b.ib[i] = -1;
+    b.iratio[i] = b.ipos[i] = 0;
+    if (hdrs[i].interp_ratio > 0) {  // dec/decode_frame.c:91-109
+      if (!d->ti || hdrs[i].interp_pos < 0) return THOR_ERR_ARG;
+      b.ia[i] = find_slot_host(d, hdrs[i].interp_ref[0]);
+      b.ib[i] = find_slot_host(d, hdrs[i].interp_ref[1]);
+      if (b.ia[i] < 0 || b.ib[i] < 0 || b.ia[i] == b.cur[i] || b.ib[i] == b.cur[i]) return THOR_ERR_REF;
+      b.iratio[i] = hdrs[i].interp_ratio;
+      b.ipos[i] = hdrs[i].interp_pos;
+      f.islot = d->islot;
+    }
     f.blk = in.blocks;
     f.coeffs = in.coeffs;
     f.tus = in.tu_list;
@@ -409,6 +436,37 @@ static int recon_lds_pad() {
     return e ? atoi(e) : 0;
   }();
   return v;
+}
+
+static thor_yuv_planes_t slot_planes(const thor_dec *d, int s) {
+  uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  return thor_yuv_planes_t{base + d->offy, base + d->offu, base + d->offv, d->sy, d->sc};
+}
+
+// The frames' temporal-interpolated references (interpolate_frames + pad_yuv_frame,
+// dec/decode_frame.c:106-107) into their contexts' interpolation slots.
+static int batch_interp(thor_dec_t *const *ds, const Batch &b) {
+  hipStream_t st = ds[0]->stream;
+  for (int i = 0; i < b.n; i++) {
+    if (b.iratio[i] <= 0) continue;
+    thor_dec *d = ds[i];
+    StageMark m(ds[0], ST_PREP);
+    const thor_yuv_planes_t ra = slot_planes(d, b.ia[i]), rb = slot_planes(d, b.ib[i]), o = slot_planes(d, d->islot);
+    const int rc = thor_interpolate_frames(d->ti, &ra, &rb, THOR_PAD_Y, &o, b.iratio[i], b.ipos[i], st);
+    if (rc != THOR_OK) return rc;
+    FrameBatch fb;
+    memset(&fb, 0, sizeof(fb));
+    fb.f[0].cy = o.y;
+    fb.f[0].cu = o.u;
+    fb.f[0].cv = o.v;
+    fb.f[0].sy = d->sy;
+    fb.f[0].sc = d->sc;
+    fb.f[0].W = d->seq.width;
+    fb.f[0].H = d->seq.height;
+    k_pad<<<dim3((pad_chunks(d->seq.width, d->seq.height) + 255) / 256, 1), 256, 0, st>>>(fb);
+    HIPCHK(hipGetLastError());
+  }
+  return THOR_OK;
 }
 
 // Phase A: side info, residuals, intra setup, inter reconstruction (the SB
@@ -490,6 +548,7 @@ static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t
       HIPCHK(hipEventRecord(lead->xev[0], ds[i]->stream));
       HIPCHK(hipStreamWaitEvent(st, lead->xev[0], 0));
     }
+  if ((rc = batch_interp(ds, b)) != THOR_OK) return rc;
   if ((rc = batch_phase_a(lead, b)) != THOR_OK) return rc;
   if ((rc = batch_phase_b(lead, b)) != THOR_OK) return rc;
   // later work a member context enqueues on its own stream follows this batch
@@ -521,7 +580,7 @@ int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_
   int rc = batch_prepare(ds, 1, hdr, in, *b);
   if (rc == THOR_OK) {
     if (hipSetDevice(d->device) != hipSuccess) rc = THOR_ERR_HIP;
-    else rc = batch_phase_a(d, *b);
+    else if ((rc = batch_interp(ds, *b)) == THOR_OK) rc = batch_phase_a(d, *b);
   }
   if (rc != THOR_OK) {
     delete b;

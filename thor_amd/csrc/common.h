@@ -51,6 +51,7 @@ struct FrameCtx {
   int nblocks, ntus, nintra, nprep, nres, full_sb;
   int qp, qpc, deblock, clpf_on;
   int band0, band1;  // SB rows k_recon reconstructs (row-band sharding); all by default
+  int islot;         // slot of the frame's temporal-interpolated reference (blocks' ref -2), -1 none
 };
 // A batch of frames travels in the kernel argument segment (8 x 384 B, under
 // the 4 KB kernarg limit): the host fills it per call, no upload copy.  Every

@@ -564,6 +564,7 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
     P->seq.tb_split_enable = (int)b.get(1);
     P->max_num_ref = (int)b.get(2) + 1;
     P->interp_ref = (int)b.get(1);
+    P->seq.interp_ref = P->interp_ref;
     P->max_delta_qp = (int)b.get(3);
     P->seq.deblocking = (int)b.get(1);
     P->seq.clpf = (int)b.get(1);
@@ -591,9 +592,29 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
     P->num_ref = 0;
   }
   P->frame_num = (int)b.get(16);
-  if (P->fr_interp) return THOR_ERR_ARG;  // interpolated references: not supported by this build
-  for (int r = 0; r < P->num_ref; r++)
+  for (int r = 0; r < P->num_ref; r++) {
+    if (P->ref_array[r] == -1) continue;  // the interpolated reference
     if (P->ref_array[r] < 0 || P->ref_array[r] > 32 || P->window[P->ref_array[r]] < 0) return THOR_ERR_REF;
+  }
+  // the interpolated reference is built only for num_ref > 2 with ref_array[0] == -1
+  // (decode_frame.c:91-109); any other use of index -1 would read a stale frame
+  int interp_a = -1, interp_b = -1, interp_ratio = 0, interp_pos = 0;
+  if (P->fr_interp) {
+    if (!(P->num_ref > 2 && P->ref_array[0] == -1) || P->ref_array[1] < 0 || P->ref_array[2] < 0) return THOR_ERR_REF;
+    for (int r = 1; r < P->num_ref; r++)
+      if (P->ref_array[r] == -1) return THOR_ERR_REF;
+    interp_a = P->window[P->ref_array[1]];
+    interp_b = P->window[P->ref_array[2]];
+    int off1 = interp_b - P->frame_num, off2 = P->frame_num - interp_a;
+    if (off1 < 0 && off2 < 0) {
+      off1 = -off1;
+      off2 = -off2;
+    }
+    if (off1 == off2) off1 = off2 = 1;
+    interp_ratio = off1 + off2;
+    interp_pos = off2;
+    if (interp_ratio <= 0) return THOR_ERR_REF;  // the one-sided case the reference leaves unhandled (:105)
+  }
   P->qpb = P->qp;
   P->blocks.clear();
   P->coeffs.clear();
@@ -631,6 +652,10 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
   out->hdr.frame_type = P->frame_type;
   out->hdr.qp = P->qp;
   out->hdr.clpf_on = P->clpf_on;
+  out->hdr.interp_ref[0] = interp_a;
+  out->hdr.interp_ref[1] = interp_b;
+  out->hdr.interp_ratio = interp_ratio;
+  out->hdr.interp_pos = interp_pos;
   out->num_ref = P->num_ref;
   out->decode_order = P->decode_order++;
   out->blocks = P->blocks.data();

@@ -33,11 +33,14 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   // (uni-pred: >, each bi-pred leg: >=, :259-260, :291, :328-329, :358, :377,
   // :416-417); reference slot by frame number
   const bool bi = mode == M_BIPRED || ((mode == M_SKIP || mode == M_MERGE) && B.dir == 2);
-  const int ref0 = B.ref0, ref1 = B.ref1;
+  // the temporal-interpolated reference (-2) carries the current frame's
+  // number (dec/decode_frame.c:108) and lives in its own slot
+  const int ref0 = B.ref0 == -2 ? f.frame_num : B.ref0, ref1 = B.ref1 == -2 ? f.frame_num : B.ref1;
   const int sg0 = bi ? (ref0 >= f.frame_num) : (ref0 > f.frame_num);
   const int sg1 = ref1 >= f.frame_num;
   const int8_t *lut = (const int8_t *)f.slot_lut;
-  const int s0 = lut[ref0 & 127], s1 = bi ? lut[ref1 & 127] : 0;
+  const int s0 = B.ref0 == -2 ? f.islot : lut[ref0 & 127];
+  const int s1 = bi ? (B.ref1 == -2 ? f.islot : lut[ref1 & 127]) : 0;
   // an inter CU naming a reference that is not resident: flag it (ctl[2] ->
   // THOR_ERR_REF from thor_dec_sync / thor_dec_read_frame) instead of leaving
   // stale slot pixels behind silently

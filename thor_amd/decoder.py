@@ -66,7 +66,8 @@ class GpuDecoder:
         if self.lib.thor_device_count() <= 0:
             raise RuntimeError("no HIP device visible: the GPU decode path has no CPU fallback")
         self.seq = seq
-        cs = L.ThorSeq(seq.width, seq.height, seq.bipred, seq.deblocking, seq.clpf, seq.tb_split_enable)
+        cs = L.ThorSeq(seq.width, seq.height, seq.bipred, seq.deblocking, seq.clpf, seq.tb_split_enable,
+                       getattr(seq, "interp_ref", 0))
         self.h = self.lib.thor_dec_create(C.byref(cs), device, slots)
         if not self.h:
             raise RuntimeError("thor_dec_create failed")
@@ -130,7 +131,8 @@ class GpuDecoder:
             img[off:off + a.nbytes] = a.view(np.uint8).reshape(-1)
         base = self._buf(img, pool, 0).ptr
         bp, cp, fp, ip, tp, lp = (base + off for off in offs)
-        hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on)
+        hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on,
+                             (C.c_int32 * 2)(*fr.interp_refs), fr.interp_ratio, fr.interp_pos)
         nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + TU_DTYPE.itemsize * n_tu
         return DeviceFrame(hdr, bp, len(blocks), cp, fp if flags.size else 0, ip, n_intra, tp, n_tu, lp, n_clpf,
                            nbytes)

@@ -14,11 +14,17 @@ _lib = None
 
 class ThorSeq(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("bipred", C.c_int32), ("deblocking", C.c_int32),
-                ("clpf", C.c_int32), ("tb_split_enable", C.c_int32)]
+                ("clpf", C.c_int32), ("tb_split_enable", C.c_int32), ("interp_ref", C.c_int32)]
 
 
 class ThorFrameHdr(C.Structure):
-    _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32)]
+    _fields_ = [("frame_num", C.c_int32), ("frame_type", C.c_int32), ("qp", C.c_int32), ("clpf_on", C.c_int32),
+                ("interp_ref", C.c_int32 * 2), ("interp_ratio", C.c_int32), ("interp_pos", C.c_int32)]
+
+
+class ThorYuvPlanes(C.Structure):
+    _fields_ = [("y", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p), ("stride_y", C.c_int32),
+                ("stride_c", C.c_int32)]
 
 
 class ThorEncParams(C.Structure):
@@ -57,6 +63,7 @@ BATCHED_SYMBOLS = [
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_frames", "thor_enc_frame", "thor_enc_frame_bytes",
     "thor_enc_read_recon", "thor_enc_reset",
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
+    "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
 SIMD_SURFACE_SYMBOLS = [
@@ -164,6 +171,16 @@ def load(path: str = LIB_PATH):
     L.thor_interp_comp.restype = i
     L.thor_interp_frame.argtypes = [P, P, P, i, i, i, i, i, i, P]
     L.thor_interp_frame.restype = i
+    L.thor_ti_create.argtypes = [i, i, i]
+    L.thor_ti_create.restype = P
+    L.thor_ti_destroy.argtypes = [P]
+    L.thor_interpolate_frames.argtypes = [P, C.POINTER(ThorYuvPlanes), C.POINTER(ThorYuvPlanes), i,
+                                          C.POINTER(ThorYuvPlanes), i, i, P]
+    L.thor_interpolate_frames.restype = i
+    L.thor_ti_read_fields.argtypes = [P, i, P, P]
+    L.thor_ti_read_fields.restype = i
+    L.thor_ti_status.argtypes = [P]
+    L.thor_ti_status.restype = i
     # the reference's SIMD kernel surface (include/thor_kernels.h)
     u8p = P
     L.transform_simd.argtypes = [P, P, i, i]

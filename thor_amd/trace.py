@@ -72,6 +72,16 @@ class Frame:
     blocks: np.ndarray  # BLOCK_DTYPE
     coeffs: np.ndarray  # int16 compact coefficient pool
     clpf_flags: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint8))
+    # temporal-interpolated reference (dec/decode_frame.c:91-109): the frame numbers of the
+    # two interpolated references and interpolate_frames' (ratio, pos); ratio 0 = none
+    interp_refs: tuple = (-1, -1)
+    interp_ratio: int = 0
+    interp_pos: int = 0
+
+    def hdr_fields(self):
+        """thor_frame_hdr_t's fields in order."""
+        return (self.frame_num, self.frame_type, self.qp, self.clpf_on, self.interp_refs, self.interp_ratio,
+                self.interp_pos)
 
 
 def tu_layout(size: int, tb_split: int):

@@ -50,6 +50,10 @@ STREAMS = [
     ("w8_low", 360, 288, 6, "config_LDB_low_complexity.txt", [], 8),
     # BASELINE config 3 operating point at 1080p (3 frames: the reference needs ~75 s)
     ("hd_high", 1920, 1080, 3, "config_LDB_high_efficiency.txt", [], 9),
+    # temporal-interpolated references (-interp_ref 1, the HDB16 configs' default): BASELINE config 5
+    ("cif_hdbi", 352, 288, 17, "config_HDB16_low_complexity.txt", [], 10),
+    ("cif_hdbi_high", 352, 288, 17, "config_HDB16_high_efficiency.txt", [], 11),
+    ("k4_hdbi", 3840, 2160, 17, "config_HDB16_low_complexity.txt", [], 12),
 ]
 
 
