@@ -188,7 +188,7 @@ int thor_dec_sync(thor_dec_t *d);
  * thor_dec_frame brackets each stage; thor_dec_stage_ms waits for the stream
  * and returns the milliseconds accumulated per stage since the last call:
  * [0] side info + residuals (k_prep, k_resid), [1] inter recon (k_recon), [2] intra,
- * [3] deblock, [4] CLPF, [5] pad. */
+ * [3] deblock, [4] CLPF, [5] pad, [6] temporal-interpolated reference. */
 int thor_dec_set_timing(thor_dec_t *d, int on);
 int thor_dec_stage_ms(thor_dec_t *d, double *ms, int nstages);
 /* The same marks one by one in enqueue order (stage index, milliseconds), so

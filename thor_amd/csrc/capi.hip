@@ -76,7 +76,7 @@ struct thor_dec {
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_marks;
 };
 
-enum { ST_PREP = 0, ST_INTER, ST_INTRA, ST_DEBLOCK, ST_CLPF, ST_PAD, ST_COUNT };
+enum { ST_PREP = 0, ST_INTER, ST_INTRA, ST_DEBLOCK, ST_CLPF, ST_PAD, ST_INTERP, ST_COUNT };
 
 static hipEvent_t ev_next(thor_dec *d) {
   if (d->ev_used == d->ev_pool.size()) {
@@ -450,7 +450,7 @@ static int batch_interp(thor_dec_t *const *ds, const Batch &b) {
   for (int i = 0; i < b.n; i++) {
     if (b.iratio[i] <= 0) continue;
     thor_dec *d = ds[i];
-    StageMark m(ds[0], ST_PREP);
+    StageMark m(ds[0], ST_INTERP);
     const thor_yuv_planes_t ra = slot_planes(d, b.ia[i]), rb = slot_planes(d, b.ib[i]), o = slot_planes(d, d->islot);
     const int rc = thor_interpolate_frames(d->ti, &ra, &rb, THOR_PAD_Y, &o, b.iratio[i], b.ipos[i], st);
     if (rc != THOR_OK) return rc;

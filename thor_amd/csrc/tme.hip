@@ -35,8 +35,11 @@ struct TiLevel {
   uint32_t *f0, *f1;       // final field after the merge pass
   const uint32_t *guide;   // final f1 of the coarser level (up-scaled on read), nullptr at the top
   int gbw;
-  unsigned *prog;          // per step-row progress words, ticket at prog[bh / 2]
+  unsigned long long *pub; // per step: (generation << 32) | mv1, the wavefront's ready flags
+  unsigned *ticket;
+  unsigned gen;            // this launch's generation tag
   unsigned *err;
+  unsigned long long *dbg; // optional (diagnostics): per step (ready, done) s_memrealtime stamps
 };
 
 __device__ __forceinline__ int ti_x(uint32_t v) { return (int)(int16_t)(v & 0xffff); }
@@ -102,9 +105,20 @@ __device__ __forceinline__ uint32_t ti_sad_part(const TiLevel &L, int x0, int y0
   return s;
 }
 
-__device__ __forceinline__ uint32_t ti_wave_sum(uint32_t v) {
-  for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+// Sum over each 16-lane DPP row, in every lane of the row: quad butterflies,
+// then the half-row and row mirrors (4 VALU ops, no LDS-pipe permutes).
+__device__ __forceinline__ uint32_t ti_row_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);  // row_mirror
   return v;
+}
+// Wave total, uniform: the four row sums read out and added on the scalar unit.
+__device__ __forceinline__ uint32_t ti_wave_sum(uint32_t v) {
+  const uint32_t r = ti_row_sum(v);
+  return __builtin_amdgcn_readlane(r, 0) + __builtin_amdgcn_readlane(r, 16) + __builtin_amdgcn_readlane(r, 32) +
+         __builtin_amdgcn_readlane(r, 48);
 }
 
 // get_mv_cost (:366-385) from the step's neighbour vectors (already loaded)
@@ -142,52 +156,155 @@ __device__ __forceinline__ uint32_t ti_median(const uint32_t *l, int n) {
   return l[best];
 }
 
+// Sliding LDS window of both pictures around the current step: a ring of
+// 16-px column tiles (T_k covers x in [16k, 16k + 16)), TI_WH rows from y0 -
+// TI_WR.  Step c reads T_{c-2} .. T_{c+2} while T_{c+3} is being loaded.
+#define TI_WR 32
+#define TI_WH (16 + 2 * TI_WR)
+#define TI_TILES 6
+struct TiWin {
+  uint8_t t[2][TI_TILES][TI_WH][16];
+};
+
+__device__ __forceinline__ int ti_slot(int k) { return (k + 6 * TI_TILES) % TI_TILES; }  // k >= -2
+
+// Stage tile T_k (rows y0 - TI_WR ..) of both pictures: 2 x TI_WH 16-byte rows,
+// row coordinates clamped into the plane's allocation (clamped rows lie outside
+// [-pad, h + pad), so no in-frame SAD ever reads them).
+// Every lane issues its three loads unconditionally (surplus lanes re-load the
+// last row): a load skipped under an exec mask would leave its register
+// "pending" across the loop back-edge and cost a vmcnt(0) every step.
+struct TiTile {
+  uint4 v0, v1, v2;  // this lane's rows idx = lane, lane + 64, lane + 128 (named: kept in registers)
+};
+__device__ __forceinline__ uint4 ti_tile_row(const TiLevel &L, int k, int y0, int idx) {
+  idx = min(idx, 2 * TI_WH - 1);
+  const int pic = idx >= TI_WH, r = idx - pic * TI_WH;
+  const int y = min(L.h + L.pad - 1, max(-L.pad, y0 - TI_WR + r));
+  const uint8_t *p = pic ? L.p1 : L.p0;
+  const int s = pic ? L.s1 : L.s0;
+  return *(const uint4 *)(p + (long long)y * s + 16 * k);
+}
+__device__ __forceinline__ TiTile ti_tile_load(const TiLevel &L, int k, int y0) {
+  const int lane = threadIdx.x;
+  return TiTile{ti_tile_row(L, k, y0, lane), ti_tile_row(L, k, y0, lane + 64), ti_tile_row(L, k, y0, lane + 128)};
+}
+__device__ __forceinline__ void ti_tile_put(TiWin &W, int sl, int idx, uint4 v) {
+  if (idx < 2 * TI_WH) {
+    const int pic = idx >= TI_WH, r = idx - pic * TI_WH;
+    *(uint4 *)&W.t[pic][sl][r][0] = v;
+  }
+}
+__device__ __forceinline__ void ti_tile_store(TiWin &W, int k, const TiTile &t) {
+  const int lane = threadIdx.x, sl = ti_slot(k);
+  ti_tile_put(W, sl, lane, t.v0);
+  ti_tile_put(W, sl, lane + 64, t.v1);
+  ti_tile_put(W, sl, lane + 128, t.v2);
+}
+
+// 4 pixels of picture `pic` at window row wr, level column x = u + 4q + sh
+// (u: uniform, dword aligned; sh: uniform byte shift)
+__device__ __forceinline__ uint32_t ti_win4(const TiWin &W, int pic, int u, int sh, int q, int wr) {
+  const int ta = (u & 15) + 4 * q, tb = ta + 4;
+  const int k0 = u >> 4;
+  const uint32_t A = *(const uint32_t *)&W.t[pic][ti_slot(k0 + (ta >> 4))][wr][ta & 15];
+  const uint32_t B = *(const uint32_t *)&W.t[pic][ti_slot(k0 + (tb >> 4))][wr][tb & 15];
+  return __builtin_amdgcn_alignbyte(B, A, (uint32_t)sh);
+}
+
+// Spin (uniformly) until the published word of a step of the row above carries
+// this launch's generation.
+__device__ __forceinline__ unsigned long long ti_spin(const unsigned long long *p, unsigned gen, unsigned *err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long w;
+  while (__builtin_amdgcn_readfirstlane(
+             (uint32_t)((w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32)) != gen) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ULL) {  // 60 s: report, never hang the GPU
+      if (threadIdx.x == 0) atomicOr(err, 1u);
+      break;
+    }
+  }
+  return w;
+}
+
+// This lane's share of a 16x16 sad_cost at step origin (x0, y0): from the LDS
+// window when both displaced blocks lie in it (and in the padded frame), else
+// from the planes (ti_sad_part).
+// Vectors and the path choice are made explicitly uniform (SGPRs, scalar
+// branch): a VALU-computed condition would be treated as divergent, the
+// if / else linearised, and the window path would then wait (vmcnt(0)) on the
+// fallback path's loads -- and with them on the tile prefetch -- every step.
+__device__ __forceinline__ uint32_t ti_sad16(const TiLevel &L, const TiWin &W, int x0, int y0, uint32_t a, uint32_t b,
+                                             int r, int q) {
+  a = __builtin_amdgcn_readfirstlane(a);
+  b = __builtin_amdgcn_readfirstlane(b);
+  const int dxa = ti_round(ti_x(a)), dya = ti_round(ti_y(a)), dxb = ti_round(ti_x(b)), dyb = ti_round(ti_y(b));
+  const int xa = x0 + dxa, ya = y0 + dya, xb = x0 + dxb, yb = y0 + dyb;
+  const int pad = L.pad, wP = L.w + pad, hP = L.h + pad;
+  const bool inside = xa >= -pad && xa + 16 <= wP && ya >= -pad && ya + 16 <= hP && xb >= -pad && xb + 16 <= wP &&
+                      yb >= -pad && yb + 16 <= hP;
+  const bool inwin = abs(dxa) <= TI_WR && abs(dya) <= TI_WR && abs(dxb) <= TI_WR && abs(dyb) <= TI_WR;
+  if (__builtin_amdgcn_readfirstlane((int)(inside && inwin))) {
+    const uint32_t va = ti_win4(W, 0, xa & ~3, xa & 3, q, dya + TI_WR + r);
+    const uint32_t vb = ti_win4(W, 1, xb & ~3, xb & 3, q, dyb + TI_WR + r);
+    return __builtin_amdgcn_sad_u8(va, vb, 0u);
+  }
+  return ti_sad_part(L, x0, y0, a, b, 16, r, q);
+}
+
+__device__ __forceinline__ unsigned long long ti_ld64(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The search pass of motion_estimate_bi (:874-896): one wave per step row.
+// A step publishes its vector as a 64-bit (generation, mv1) word; the row
+// below spins on exactly the word it needs (its above-right step), so the
+// wavefront needs no progress counters and no fences: the vector travels with
+// its own ready flag.
 __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
+  __shared__ TiWin W;
   const int lane = threadIdx.x, r16 = lane >> 2, q = lane & 3;
   const int nrows = L.bh >> 1, ncols = L.bw >> 1, bw = L.bw;
   unsigned t = 0;
-  if (lane == 0) t = atomicAdd(&L.prog[nrows], 1u);
+  if (lane == 0) t = atomicAdd(L.ticket, 1u);
   const int row = (int)__builtin_amdgcn_readfirstlane(t);
   if (row >= nrows) return;
-  const int yp = 2 * row;
+  const int yp = 2 * row, y0 = yp * 8;
   const bool guided = L.guide != nullptr;
   const int lambda = guided ? 3000 / 4 : 3000;
   const int wt0 = L.wt0, wt1 = L.wt1;
-  unsigned seen = 0;
-  uint32_t left = 0;           // this row's previous step (written by this wave)
-  uint32_t up_l = 0, up = 0;   // row above: steps c-1 and c (rolled forward)
+  const unsigned long long tag = (unsigned long long)L.gen << 32;
+  const unsigned long long *above = L.pub + (long long)(row - 1) * ncols;
+  unsigned long long *mine = L.pub + (long long)row * ncols;
+  // the window for step 0: tiles -2 .. 2
+  for (int k = -2; k <= 2; k++) ti_tile_store(W, k, ti_tile_load(L, k, y0));
+  uint32_t left = 0;          // this row's previous step (written by this wave)
+  uint32_t up_l = 0, up = 0;  // row above: steps c-1 and c (rolled forward)
   uint32_t up_r = 0;
+  unsigned long long next = 0;  // prefetched published word of the row above
+  if (row > 0) next = ti_ld64(above + (ncols > 1 ? 1 : 0));
   for (int c = 0; c < ncols; c++) {
-    const int xp = 2 * c;
+    const int xp = 2 * c, x0 = xp * 8;
+    const TiTile pf = ti_tile_load(L, c + 3, y0);  // next step's new tile, in flight during this step
     if (row > 0) {
-      const unsigned need = (unsigned)(c + 2 < ncols ? c + 2 : ncols);
-      if (need > seen) {
-        unsigned v = 0;
-        if (lane == 0) {
-          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-          while ((v = ti_ld_relaxed(&L.prog[row - 1])) < need) {
-            __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ULL) {  // 60 s: report, never hang the GPU
-              atomicOr(L.err, 1u);
-              break;
-            }
-          }
-        }
-        seen = __builtin_amdgcn_readfirstlane(v);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-      const uint32_t *above = L.m1 + (long long)(yp - 2) * bw;
+      // above-right (or, at the last column, nothing new: its vectors are already held)
       if (c == 0) {
-        up = ti_ld_field(above);
+        up = __builtin_amdgcn_readfirstlane((uint32_t)ti_spin(above, L.gen, L.err));
         up_l = 0;
       } else {
         up_l = up;
         up = up_r;
       }
-      up_r = xp + 2 < bw ? ti_ld_field(above + xp + 2) : 0;
+      if (c + 1 < ncols) {
+        unsigned long long w = next;
+        if (__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) != L.gen) w = ti_spin(above + c + 1, L.gen, L.err);
+        up_r = __builtin_amdgcn_readfirstlane((uint32_t)w);
+        if (c + 2 < ncols) next = ti_ld64(above + c + 2);  // the next step's, early
+      }
     }
+    unsigned long long t_ready = 0;
+    if (L.dbg) t_ready = __builtin_amdgcn_s_memrealtime();
     // skip vector (:820-832) and its pic[0] companion
     uint32_t nb[3];
     int n = 0;
@@ -196,7 +313,6 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
     if (yp > 0) nb[n++] = up;
     const uint32_t skip1 = n ? ti_median(nb, n) : 0u;
     const uint32_t skip0 = ti_scale(skip1, -wt1, wt0);
-    const int x0 = xp * 8, y0 = yp * 8;
     // skip_test (:525-647): each 8x8 quarter of the 16x16 within 8 * 64 and inside the padded frame
     bool skip;
     {
@@ -206,16 +322,14 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
       skip = xa >= -pad && xa + 16 <= wP && ya >= -pad && ya + 16 <= hP && xb >= -pad && xb + 16 <= wP &&
              yb >= -pad && yb + 16 <= hP;
       if (skip) {
-        const uint32_t va = ti_load4(L.p0 + (long long)(ya + r16) * L.s0 + xa + 4 * q);
-        const uint32_t vb = ti_load4(L.p1 + (long long)(yb + r16) * L.s1 + xb + 4 * q);
-        uint32_t s = __builtin_amdgcn_sad_u8(va, vb, 0u);
-        // quarter sums: reduce over column bit 0 and row bits 0-2 (lanes keep q bit 1 and row bit 3)
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        s += __shfl_xor(s, 16);
-        const bool over = s > 8u * 64u;
-        skip = __ballot(over && (lane == 0 || lane == 2 || lane == 32 || lane == 34)) == 0;
+        const uint32_t s = ti_sad16(L, W, x0, y0, skip0, skip1, r16, q);
+        // quarter sums: left / right column half packed (16 bits each), rows of 16 lanes =
+        // 4 image rows, rows 0-1 the top quarters, 2-3 the bottom ones
+        const uint32_t r = ti_row_sum(q < 2 ? s : s << 16);
+        const uint32_t top = __builtin_amdgcn_readlane(r, 0) + __builtin_amdgcn_readlane(r, 16);
+        const uint32_t bot = __builtin_amdgcn_readlane(r, 32) + __builtin_amdgcn_readlane(r, 48);
+        const uint32_t thr = 8u * 64u;
+        skip = (top & 0xffff) <= thr && (top >> 16) <= thr && (bot & 0xffff) <= thr && (bot >> 16) <= thr;
       }
     }
     uint32_t r0, r1;
@@ -228,7 +342,7 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
       int nc = 0;
       cand[nc++] = 0u;
       if (guided) {
-        const uint32_t g = ti_ld_field(L.guide + (long long)(yp >> 1) * L.gbw + (xp >> 1));
+        const uint32_t g = L.guide[(long long)(yp >> 1) * L.gbw + (xp >> 1)];
         nc = ti_add(cand, nc, ti_mv(ti_x(g) << 1, ti_y(g) << 1));  // upscale_mv_data_2x2 (:266-267); scale by wt0/wt0 = identity
       }
       if (yp > 0 && xp < bw - 2) nc = ti_add(cand, nc, up_r);
@@ -237,9 +351,9 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
       // every candidate's cost at once (adaptive_search_v2 :674-683), two SADs per reduction
       uint32_t cost[5];
       for (int k = 0; k < nc; k += 2) {
-        uint32_t s = ti_sad_part(L, x0, y0, ti_scale(cand[k], -wt1, wt0), cand[k], 16, r16, q);
-        if (k + 1 < nc) s |= ti_sad_part(L, x0, y0, ti_scale(cand[k + 1], -wt1, wt0), cand[k + 1], 16, r16, q) << 16;
-        s = __builtin_amdgcn_readfirstlane(ti_wave_sum(s));
+        uint32_t s = ti_sad16(L, W, x0, y0, ti_scale(cand[k], -wt1, wt0), cand[k], r16, q);
+        if (k + 1 < nc) s |= ti_sad16(L, W, x0, y0, ti_scale(cand[k + 1], -wt1, wt0), cand[k + 1], r16, q) << 16;
+        s = ti_wave_sum(s);
         cost[k] = (s & 0xffff) + (uint32_t)ti_mv_cost(cand[k], xp, yp, bw, up_r, up, up_l, left, lambda);
         if (k + 1 < nc) cost[k + 1] = (s >> 16) + (uint32_t)ti_mv_cost(cand[k + 1], xp, yp, bw, up_r, up, up_l, left, lambda);
       }
@@ -252,12 +366,12 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
           while (shift >= 3 && count > 0) {
             const int o = 1 << shift, cx = ti_x(cm), cy = ti_y(cm);
             const uint32_t p[4] = {ti_mv(cx - o, cy), ti_mv(cx + o, cy), ti_mv(cx, cy - o), ti_mv(cx, cy + o)};
-            uint32_t s01 = ti_sad_part(L, x0, y0, ti_scale(p[0], -wt1, wt0), p[0], 16, r16, q) |
-                           (ti_sad_part(L, x0, y0, ti_scale(p[1], -wt1, wt0), p[1], 16, r16, q) << 16);
-            uint32_t s23 = ti_sad_part(L, x0, y0, ti_scale(p[2], -wt1, wt0), p[2], 16, r16, q) |
-                           (ti_sad_part(L, x0, y0, ti_scale(p[3], -wt1, wt0), p[3], 16, r16, q) << 16);
-            s01 = __builtin_amdgcn_readfirstlane(ti_wave_sum(s01));
-            s23 = __builtin_amdgcn_readfirstlane(ti_wave_sum(s23));
+            uint32_t s01 = ti_sad16(L, W, x0, y0, ti_scale(p[0], -wt1, wt0), p[0], r16, q) |
+                           (ti_sad16(L, W, x0, y0, ti_scale(p[1], -wt1, wt0), p[1], r16, q) << 16);
+            uint32_t s23 = ti_sad16(L, W, x0, y0, ti_scale(p[2], -wt1, wt0), p[2], r16, q) |
+                           (ti_sad16(L, W, x0, y0, ti_scale(p[3], -wt1, wt0), p[3], r16, q) << 16);
+            s01 = ti_wave_sum(s01);
+            s23 = ti_wave_sum(s23);
             const uint32_t sads[4] = {s01 & 0xffff, s01 >> 16, s23 & 0xffff, s23 >> 16};
             bool better = false;
             for (int i = 0; i < 4; i++) {
@@ -280,16 +394,22 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
       r1 = best;
       r0 = ti_scale(best, -wt1, wt0);
     }
-    // propagate over the 2x2 blocks of the step (:884-894)
+    // publish (the row below waits on exactly this word), then the 2x2 blocks of the step (:884-894)
+    if (lane == 0) __hip_atomic_store(mine + c, tag | r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (L.dbg && lane == 0) {
+      L.dbg[2 * ((long long)row * ncols + c)] = t_ready;
+      L.dbg[2 * ((long long)row * ncols + c) + 1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (lane < 4) {
       const long long o = (long long)(yp + (lane >> 1)) * bw + xp + (lane & 1);
       L.m0[o] = r0;
       L.m1[o] = r1;
     }
     left = r1;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) __hip_atomic_store(&L.prog[row], (unsigned)(c + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // slide the window: T_{c+3} replaces T_{c-3} (no longer read)
+    wave_lds_sync();
+    ti_tile_store(W, c + 3, pf);
+    wave_lds_sync();
   }
 }
 
@@ -315,11 +435,7 @@ __global__ __launch_bounds__(256) void k_ti_merge(const TiLevel L) {
     b0 = b1 = 0;
     for (int k = 0; k < nc; k++) {
       const uint32_t q0 = ti_scale(cand[k], -L.wt1, L.wt0);
-      uint32_t s = ti_sad_part(L, j * 8, i * 8, q0, cand[k], 8, l16 >> 1, l16 & 1);
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      s += __shfl_xor(s, 4);
-      s += __shfl_xor(s, 8);
+      const uint32_t s = ti_row_sum(ti_sad_part(L, j * 8, i * 8, q0, cand[k], 8, l16 >> 1, l16 & 1));
       if (s < bc) {
         bc = s;
         b1 = cand[k];
@@ -342,8 +458,11 @@ struct thor_ti {
   uint32_t *fields;               // per level: m0, m1, f0, f1
   long long foff[TI_MAXL];
   int bw[TI_MAXL], bh[TI_MAXL];
-  unsigned *prog;                 // per level: step-row progress + ticket
+  unsigned long long *pub;        // per level: published step vectors (k_ti_search)
   long long poff[TI_MAXL];
+  unsigned *tickets;              // one per level
+  unsigned gen;                   // last generation tag used
+  unsigned long long *dbg;        // diagnostics: level-0 step stamps (thor_ti_debug)
   unsigned *err;
 };
 
@@ -380,12 +499,14 @@ thor_ti_t *thor_ti_create(int width, int height, int device) {
     t->foff[l] = (long long)fwords;
     fwords += 4 * (size_t)t->bw[l] * t->bh[l];
     t->poff[l] = (long long)pwords;
-    pwords += (size_t)t->bh[l] / 2 + 1;
+    pwords += (size_t)(t->bh[l] / 2) * (t->bw[l] / 2);
   }
   bool ok = true;
-  if (pbytes) ok = hipMalloc(&t->pyr, pbytes) == hipSuccess;
+  // + 256: the search window's last 16-byte tile of a row may run past the last plane's end
+  if (pbytes) ok = hipMalloc(&t->pyr, pbytes + 256) == hipSuccess;
   ok = ok && hipMalloc(&t->fields, fwords * 4) == hipSuccess;
-  ok = ok && hipMalloc(&t->prog, pwords * 4) == hipSuccess;
+  ok = ok && hipMalloc(&t->pub, pwords * 8) == hipSuccess && hipMemset(t->pub, 0, pwords * 8) == hipSuccess;
+  ok = ok && hipMalloc(&t->tickets, 64) == hipSuccess;
   ok = ok && hipMalloc(&t->err, 64) == hipSuccess && hipMemset(t->err, 0, 64) == hipSuccess;
   if (!ok) {
     thor_ti_destroy(t);
@@ -408,7 +529,8 @@ void thor_ti_destroy(thor_ti_t *t) {
   (void)hipSetDevice(t->device);
   if (t->pyr) (void)hipFree(t->pyr);
   if (t->fields) (void)hipFree(t->fields);
-  if (t->prog) (void)hipFree(t->prog);
+  if (t->pub) (void)hipFree(t->pub);
+  if (t->tickets) (void)hipFree(t->tickets);
   if (t->err) (void)hipFree(t->err);
   delete t;
 }
@@ -426,9 +548,7 @@ int thor_interpolate_frames(thor_ti_t *t, const thor_yuv_planes_t *ref0, const t
     const int rc = thor_scale_pyramid2(ref0->y, ref1->y, ref0->stride_y, W, H, t->lv[0], t->lv[1], t->ls, nl - 1, stream);
     if (rc != THOR_OK) return rc;
   }
-  long long pw = 0;
-  for (int l = 0; l < nl; l++) pw += t->bh[l] / 2 + 1;
-  if (hipMemsetAsync(t->prog, 0, pw * 4, st) != hipSuccess) return THOR_ERR_HIP;
+  if (hipMemsetAsync(t->tickets, 0, 4 * TI_MAXL, st) != hipSuccess) return THOR_ERR_HIP;
   for (int l = nl - 1; l >= 0; l--) {
     TiLevel L;
     const uint8_t *a = l ? t->lv[0][l - 1] : ref0->y, *b = l ? t->lv[1][l - 1] : ref1->y;
@@ -450,8 +570,12 @@ int thor_interpolate_frames(thor_ti_t *t, const thor_yuv_planes_t *ref0, const t
     L.f1 = F + 3 * area;
     L.guide = l + 1 < nl ? t->fields + t->foff[l + 1] + 3 * (size_t)t->bw[l + 1] * t->bh[l + 1] : nullptr;
     L.gbw = l + 1 < nl ? t->bw[l + 1] : 0;
-    L.prog = t->prog + t->poff[l];
+    L.pub = t->pub + t->poff[l];
+    L.ticket = t->tickets + l;
+    L.gen = ++t->gen;  // a fresh tag: words of earlier launches never read as ready
+    if (L.gen == 0) L.gen = ++t->gen;
     L.err = t->err;
+    L.dbg = l == 0 ? t->dbg : nullptr;
     k_ti_search<<<L.bh / 2, 64, 0, st>>>(L);
     if (hipGetLastError() != hipSuccess) return THOR_ERR_HIP;
     k_ti_merge<<<(unsigned)((area * 16 + 255) / 256), 256, 0, st>>>(L);
@@ -479,6 +603,14 @@ int thor_ti_read_fields(thor_ti_t *t, int level, int16_t *mv0, int16_t *mv1) {
   const uint32_t *F = t->fields + t->foff[level];
   if (mv0 && hipMemcpy(mv0, F + 2 * area, area * 4, hipMemcpyDeviceToHost) != hipSuccess) return THOR_ERR_HIP;
   if (mv1 && hipMemcpy(mv1, F + 3 * area, area * 4, hipMemcpyDeviceToHost) != hipSuccess) return THOR_ERR_HIP;
+  return THOR_OK;
+}
+
+// Diagnostics (not in the public header): record (ready, done) s_memrealtime
+// stamps of every level-0 search step into dev_buf (2 x u64 per step).
+int thor_ti_debug(thor_ti_t *t, void *dev_buf) {
+  if (!t) return THOR_ERR_ARG;
+  t->dbg = (unsigned long long *)dev_buf;
   return THOR_OK;
 }
 
