@@ -28,7 +28,32 @@ def test_library_loads_and_exports_batched_api():
     assert set(declared) == set(L.SIMD_SURFACE_SYMBOLS)
     for name in declared:
         assert hasattr(lib, name), name
+    # the reference's block / frame reconstruction entry points
+    declared = _declared("thor_l2.h")
+    assert set(declared) == set(L.L2_SURFACE_SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), name
     assert b"gfx950" in lib.thor_version()
+
+
+def test_l2_struct_layouts_match_reference():
+    """thor_ref_yuv_frame_t / thor_ref_deblock_data_t mirror yuv_frame_t and
+    deblock_data_t (common/types.h:41-59, :127-135; 44-byte deblock_data_t,
+    SURVEY.md sec. 8(a) a16)."""
+    import ctypes as C
+
+    class Mv(C.Structure):
+        _fields_ = [("x", C.c_int16), ("y", C.c_int16)]
+
+    class Ip(C.Structure):
+        _fields_ = [("mv0", Mv), ("mv1", Mv), ("ref_idx0", C.c_uint32), ("ref_idx1", C.c_uint32),
+                    ("bipred_flag", C.c_uint32)]
+
+    class Dd(C.Structure):
+        _fields_ = [("mode", C.c_int32), ("cbp_y", C.c_int32), ("cbp_u", C.c_int32), ("cbp_v", C.c_int32),
+                    ("size", C.c_uint8), ("tb_split", C.c_uint8), ("pb_part", C.c_int32), ("inter_pred", Ip)]
+
+    assert C.sizeof(Dd) == 44 and Dd.pb_part.offset == 20 and Dd.inter_pred.offset == 24
 
 
 def test_block_descriptor_layout_matches_header():

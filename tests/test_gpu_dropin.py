@@ -1,9 +1,11 @@
 """Drop-in boundary, end to end: the reference's own host C (Thorenc /
 Thordec, compiled from the reference sources into oracle/_ref by
 oracle/Makefile `dropin`) with common/common_kernels.c and
-enc/enc_kernels.c replaced by libthor_amd.so.  Every SIMD-surface call --
-MC, forward/inverse transforms, SAD/SSD, fast sub-pel search, CLPF --
-executes on the GPU.  The encoder must produce the reference's bitstream
+enc/enc_kernels.c replaced by libthor_amd.so, and the L2 entry points
+(deblock_frame_y/uv, make_top_and_left, get_intra_prediction, dequantize,
+reconstruct_block; include/thor_l2.h) bound to the library too.  Every
+SIMD-surface call -- MC, forward/inverse transforms, SAD/SSD, fast sub-pel
+search, CLPF -- and every one of those L2 calls executes on the GPU.  The encoder must produce the reference's bitstream
 bit for bit (every RD decision, hence every RD cost, identical) and the
 decoder the reference's output."""
 import hashlib

@@ -10,6 +10,8 @@
 // CLPF flags (include/thor_amd.h).  MV prediction and skip / merge candidates
 // come from the same neighbour logic the device encoder uses (enc_core.h).
 // Serial bit parsing is host work by design.
+#include <string.h>
+
 #include <vector>
 
 #include "common.h"
@@ -18,22 +20,37 @@
 namespace {
 
 // getbits / getbits1 / showbits / flushbits over one frame's payload; bits
-// past the end read as zero (fillbfr, dec/getbits.c:71-106).
+// past the end read as zero (fillbfr, dec/getbits.c:71-106).  The payload is
+// copied once into a zero-padded buffer, so a read of up to 32 bits is one
+// unaligned big-endian 64-bit load and two shifts.
 struct TpBits {
-  const uint8_t *p = nullptr;
+  std::vector<uint8_t> buf;
   size_t nbits = 0, pos = 0;
-  uint32_t bit(size_t i) const { return i < nbits ? (p[i >> 3] >> (7 - (i & 7))) & 1 : 0; }
-  uint32_t show(int n) const {
-    uint32_t v = 0;
-    for (int k = 0; k < n; k++) v = (v << 1) | bit(pos + k);
-    return v;
+  void set(const uint8_t *p, size_t nbytes) {
+    buf.assign(nbytes + 16, 0);
+    if (nbytes) memcpy(buf.data(), p, nbytes);
+    nbits = nbytes * 8;
+    pos = 0;
+  }
+  uint32_t show(int n) const {  // n <= 32
+    if (n <= 0) return 0;
+    const size_t byte = pos >> 3;
+    if (byte + 8 > buf.size()) return 0;  // far past the end (corrupt input): zeros
+    uint64_t w;
+    memcpy(&w, buf.data() + byte, 8);
+    w = __builtin_bswap64(w) << (pos & 7);
+    return (uint32_t)(w >> (64 - n));
   }
   uint32_t get(int n) {
     const uint32_t v = show(n);
     pos += n;
     return v;
   }
-  uint32_t get1() { return bit(pos++); }
+  uint32_t get1() {
+    const uint32_t v = show(1);
+    pos++;
+    return v;
+  }
   void flush(int n) { pos += n; }
 };
 
@@ -190,7 +207,7 @@ struct thor_parser {
   int ref_array[8];
   std::vector<thor_block_t> blocks;
   std::vector<int16_t> coeffs;
-  std::vector<uint8_t> clpf;
+  std::vector<uint8_t> clpf, clpf_cand;
   int clpf_on = 0;
   int error = 0;
 };
@@ -482,10 +499,15 @@ void read_block(thor_parser *P, int size, int ypos, int xpos, int mode, int ref_
   B.ref1 = mode == TE_INTRA ? -1 : ref_frame_num(P, ref_idx1);
   for (int c = 0; c < 3; c++) B.coeff_off[c] = off[c];
   P->blocks.push_back(B);
-  // copy_deblock_data (dec/decode_block.c:122-156)
-  const int bs = W / 4, div = size / 8;
-  for (int m = 0; m < B.bheight / 4; m++)
-    for (int n = 0; n < B.bwidth / 4; n++) {
+  // copy_deblock_data (dec/decode_block.c:122-156), boundary cells only: later
+  // CUs read a neighbour's cells only along its bottom row and right column
+  // (te_mv_pred / te_mv_skip / te_block_ctx), so the interior is never read and
+  // the per-frame memset of the reference (decode_frame.c:53) is not needed
+  // either -- every cell read in a frame was written earlier in that frame.
+  const int bs = W / 4, div = size / 8, bh4 = B.bheight / 4, bw4 = B.bwidth / 4;
+  for (int e = 0; e < bh4 + bw4 - 1; e++) {
+    const int m = e < bw4 ? bh4 - 1 : e - bw4, n = e < bw4 ? e : bw4 - 1;
+    {
       const int m0i = div > 0 ? m / div : 0, n0i = div > 0 ? n / div : 0, index = 2 * m0i + n0i;
       TeCell &c = P->cells[(ypos / 4 + m) * bs + xpos / 4 + n];
       c.cbp_y = (uint8_t)cbp_y;
@@ -501,6 +523,7 @@ void read_block(thor_parser *P, int size, int ypos, int xpos, int mode, int ref_
       c.ip.ref_idx1 = ref_idx1;
       c.ip.bipred_flag = dir;
     }
+  }
 }
 
 // process_block_dec, dec/decode_block.c:625-669
@@ -554,9 +577,7 @@ int thor_parser_seq(const thor_parser_t *P, thor_seq_t *seq) {
 int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, thor_parsed_frame_t *out) {
   if (!P || !payload || !out) return THOR_ERR_ARG;
   TpBits &b = P->b;
-  b.p = payload;
-  b.nbits = nbytes * 8;
-  b.pos = 0;
+  b.set(payload, nbytes);
   if (!P->have_seq) {  // sequence header, dec/maindec.c:124-147
     P->seq.width = (int)b.get(16);
     P->seq.height = (int)b.get(16);
@@ -575,7 +596,6 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
     P->cells.assign((size_t)(P->seq.width / 4) * (P->seq.height / 4), TeCell());
   }
   const int W = P->seq.width, H = P->seq.height;
-  memset(&P->cells[0], 0, P->cells.size() * sizeof(TeCell));  // memset deblock_data (decode_frame.c:53)
   // frame header, dec/decode_frame.c:58-78
   P->frame_type = (int)b.get(1);
   P->qp = (int)b.get(8);
@@ -630,17 +650,18 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
   if (P->seq.clpf && b.get(1)) {
     P->clpf_on = 1;
     const int all = (int)b.get(1);
-    const int bs = W / 4;
+    // an SB is a candidate when a cell on its 8x8 grid belongs to a non-BIPRED CU
+    // with coded residual; every CU of a full SB covers a grid cell, so this is
+    // the OR over the SB's CUs
+    std::vector<uint8_t> &cand = P->clpf_cand;
+    cand.assign((size_t)nh * nv, 0);
+    for (const thor_block_t &B : P->blocks) {
+      const int k = B.ypos / 64, l = B.xpos / 64;
+      if (k < nv && l < nh && B.mode != TE_BIPRED && (B.cbp_y || B.cbp_u || B.cbp_v)) cand[k * nh + l] = 1;
+    }
     for (int k = 0; k < nv; k++)
-      for (int l = 0; l < nh; l++) {
-        int cand = 0;
-        for (int m = 0; m < 8; m++)
-          for (int n = 0; n < 8; n++) {
-            const TeCell &c = P->cells[((k * 64 + m * 8) / 4) * bs + (l * 64 + n * 8) / 4];
-            cand |= c.mode != TE_BIPRED && (c.cbp_y || c.cbp_u || c.cbp_v);
-          }
-        if (cand) P->clpf[k * nh + l] = all ? 1 : (uint8_t)b.get(1);
-      }
+      for (int l = 0; l < nh; l++)
+        if (cand[k * nh + l]) P->clpf[k * nh + l] = all ? 1 : (uint8_t)b.get(1);
   }
   if (b.pos > b.nbits) return THOR_ERR_ARG;  // read past the payload: truncated or corrupt
   // slide the window (decode_frame.c:135-147)

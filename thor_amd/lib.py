@@ -66,6 +66,8 @@ BATCHED_SYMBOLS = [
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
 ]
+L2_SURFACE_SYMBOLS = ["deblock_frame_y", "deblock_frame_uv", "make_top_and_left", "get_intra_prediction", "dequantize",
+                      "reconstruct_block", "quantize"]
 SIMD_SURFACE_SYMBOLS = [
     "block_avg_simd", "sad_calc_simd_unaligned", "get_inter_prediction_luma_simd", "get_inter_prediction_chroma_simd",
     "transform_simd", "inverse_transform_simd", "clpf_block4", "clpf_block8",
