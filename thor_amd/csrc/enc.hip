@@ -67,7 +67,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   __shared__ TeParam s_tmp;
   __shared__ TeFrame s_F;  // the job's frame parameters, read all through the RD loop
   __shared__ TeSB s_sb;    // the superblock's bit writer and ME candidate lists
-  const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb, s_bi, &s_tmp);
+  __shared__ TeSmallLv s_sl;  // the small quadtree levels' buffers
+  const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb, s_bi, &s_tmp, &s_sl);
   te_load_basis(s_tx);
   te_load_zig();
   TeSB &sb = s_sb;

@@ -623,13 +623,19 @@ TE_FN void te_add_mvcand(TeMvCand &mc, int r, TeMv mv) {
 // order), row-major.  Only that low-frequency corner can be non-zero
 // (common/transform.c:309-327; quantize writes nothing else, enc/encode_block.c:170-174).
 #define TE_COEF_COMP 1024
+// Per-level strides of that layout: component stride cs (the 64 / 32 levels'
+// 1024, the 16 / 8 levels' own size^2) and tb-split tile stride ts
+// (min(N/2, 16)^2), so the small levels' coefficient sets are small enough for LDS.
+#define TE_CS(S) ((S) <= 16 ? (S) * (S) : TE_COEF_COMP)
+#define TE_TS(S) ((S) <= 32 ? ((S) / 2) * ((S) / 2) : 256)
 struct TeParam {
   int mode, intra_mode, skip_idx, pb_part;
   TeMv mv0[4], mv1[4];
   int ref_idx0, ref_idx1, dir;
   int cbp_y, cbp_u, cbp_v;
   int tb_param, tb_split;
-  int16_t *coeff;  // 3 x TE_COEF_COMP (Y, U, V)
+  int16_t *coeff;  // 3 components (Y, U, V) at stride cs, tb-split tiles at stride ts
+  int cs, ts;
 };
 
 struct TeBlockInfo {  // block_info_t, enc/mainenc.h:97-116
@@ -643,6 +649,7 @@ struct TeBlockInfo {  // block_info_t, enc/mainenc.h:97-116
   uint8_t *rec, *rec_best;  // compact Y (size^2) | U | V ((size/2)^2 each)
   uint32_t *best_bits;      // the syntax bits the best candidate wrote (MSB first), or
   int best_nbits;           // -1: not kept (the final write_block runs again)
+  int best_cap;             // capacity of best_bits in words
 };
 
 // ---- block syntax (enc/write_bits.c) --------------------------------------
@@ -863,7 +870,7 @@ TE_FN void te_write_super_mode(TeBits &b, const TeFrame &F, const TeBlockInfo &b
   }
 }
 
-TE_FN const int16_t *te_tile(const TeParam &p, int comp, int idx) { return p.coeff + comp * TE_COEF_COMP + idx * 256; }
+TE_FN const int16_t *te_tile(const TeParam &p, int comp, int idx) { return p.coeff + comp * p.cs + idx * p.ts; }
 
 // write_block, write_bits.c:364-650.  Returns the number of bits written.
 TE_NOINL int te_write_block(TeBits &bo_, const TeFrame &F_, const TeBlockInfo &bi_, const TeParam &p_, int16_t *scan_) {

@@ -13,8 +13,19 @@ struct TeLevel {             // one quadtree level (64, 32, 16, 8)
   int16_t cbuf[3][3 * TE_COEF_COMP];  // coefficient sets: best, tmp, spare
   uint32_t bbits[TE_BEST_WORDS];      // the best candidate's syntax bits (TeBlockInfo::best_bits)
 };
+// The 32 / 16 / 8 levels' reconstruction buffers and the 16 / 8 levels'
+// coefficient sets and kept syntax bits (80 of an SB's 85 CUs): LDS on the
+// device (k_enc_rows), so a candidate's levels and pixels make no global
+// memory round trips.  Capacity of the kept bits: overflow falls back to
+// running write_block again (te_keep_best_bits).
+struct TeSmallLv {
+  uint8_t rec1[2][32 * 32 * 3 / 2], rec2[2][16 * 16 * 3 / 2], rec3[2][8 * 8 * 3 / 2];
+  int16_t cf2[2][3 * 256], cf3[2][3 * 64];
+  uint32_t bb2[128], bb3[64];
+};
 struct TeScratchMem {         // global memory, one per worker wave
   TeLevel lv[4];
+  TeSmallLv sl;                      // (host build; LDS on the device)
   TeBlockInfo bi[4];                 // (host build: the per-level block state; LDS on the device)
   TeParam tmp;                       // (host build: the candidate parameters; LDS on the device)
   uint8_t pb0[TE_BLK], pb1[TE_BLK];  // bi-pred legs (Y | U | V, compact)
@@ -33,8 +44,10 @@ struct TeScratch {
   TeNbr *nb;
   TeBlockInfo *bi;  // [4], one per quadtree level (the recursion's block_info)
   TeParam *tmp;     // the candidate of mode_decision / search_early_skip (never live at once)
+  TeSmallLv *sl;
 };
-TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb, TeBlockInfo *bi, TeParam *tmp) {
+TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb, TeBlockInfo *bi, TeParam *tmp,
+                           TeSmallLv *sl) {
   TeScratch S;
   S.lv = M.lv;
   S.pb = pb;
@@ -46,6 +59,7 @@ TE_FN TeScratch te_scratch(TeScratchMem &M, TeTx *tx, TeNbr *nb, uint8_t *pb, Te
   S.nb = nb;
   S.bi = bi;
   S.tmp = tmp;
+  S.sl = sl;
   return S;
 }
 // a callee's view of the scratch: the LDS members re-declared as LDS
@@ -55,6 +69,7 @@ TE_FN TeScratch te_local(TeScratch S) {
   S.nb = te_lds(S.nb);
   S.bi = te_lds(S.bi);
   S.tmp = te_lds(S.tmp);
+  S.sl = te_lds(S.sl);
   return S;
 }
 // State of the superblock being encoded (frame_info mvcand / best_ref are
@@ -221,7 +236,7 @@ TE_FN void te_recon(uint8_t *rec, int rs, const uint8_t *pb, int ps, const TeTx 
 // component: orig (frame, stride os) - pred -> levels (tiles of `coef`) ->
 // rec (compact, stride size).  Returns cbp (4-bit mask when tb-split).
 TE_NOINL int te_enc_inter_comp(const TeFrame &F_, TeScratch S_, const uint8_t *org, int os, int size, int qp,
-                               const uint8_t *pb_, int16_t *coef, uint8_t *rec, int type, int tb_split) {
+                               const uint8_t *pb_, int16_t *coef, uint8_t *rec, int type, int tb_split, int ts) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_local(S_);
   const uint8_t *pb = te_lds(pb_);
@@ -238,7 +253,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, TeScratch S_, const uint8_t *o
       te_fwd_tx(X, s2, fast);
       const int bit = te_quant(X, qp, s2, type);
       const int q = TE_MIN(s2, 16);
-      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * 256 + e] = (int16_t)X.C[e];
+      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * ts + e] = (int16_t)X.C[e];
       if (bit) {
         te_dequant(X, qp, s2);
         te_inv_tx(X, s2);
@@ -266,7 +281,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, TeScratch S_, const uint8_t *o
 // component.  rf / fs: the frame being reconstructed at the CU origin.
 TE_NOINL int te_enc_intra_comp(const TeFrame &F_, TeScratch S_, const uint8_t *org, int os, const uint8_t *rf, int fs,
                                int ypos, int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
-                               int tb_split, int mode, int ur, int dl) {
+                               int tb_split, int mode, int ur, int dl, int ts) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_local(S_);
   uint8_t *pb = te_lds(pb_);
@@ -283,7 +298,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F_, TeScratch S_, const uint8_t *o
       te_residual(X.R, org + i * os + j, os, pb, s2, s2);
       te_fwd_tx(X, s2, fast);
       const int bit = te_quant(X, qp, s2, type);
-      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * 256 + e] = (int16_t)X.C[e];
+      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * ts + e] = (int16_t)X.C[e];
       if (bit) {
         te_dequant(X, qp, s2);
         te_inv_tx(X, s2);
@@ -312,7 +327,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F_, TeScratch S_, const uint8_t *o
 // its syntax bits, so that the final encode of the block (re-use, the same
 // parameters and contexts) copies them instead of running write_block again.
 TE_FN void te_keep_best_bits(TeBits &b, TeBlockInfo &bi, int nbits) {
-  if (nbits > TE_BEST_WORDS * 32 || b.pos > b.cap) {
+  if (nbits > bi.best_cap * 32 || b.pos > b.cap) {
     bi.best_nbits = -1;
     return;
   }
@@ -378,11 +393,11 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeScratch S_, TeBits &b_, TeBloc
   if (mode == TE_INTRA) {
     const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
     cy = te_enc_intra_comp(F, S, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb,
-                           p.coeff, recY, itype | 0, tb_split, p.intra_mode, ur, dl);
+                           p.coeff, recY, itype | 0, tb_split, p.intra_mode, ur, dl, p.ts);
     cu = te_enc_intra_comp(F, S, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
-                           p.coeff + TE_COEF_COMP, recU, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl);
+                           p.coeff + p.cs, recU, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
     cv = te_enc_intra_comp(F, S, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
-                           p.coeff + 2 * TE_COEF_COMP, recV, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl);
+                           p.coeff + 2 * p.cs, recV, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
   } else {
     const int bip = F.enable_bipred;
     if (mode == TE_SKIP) {
@@ -412,11 +427,11 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeScratch S_, TeBits &b_, TeBloc
       if (zero_block) {
         te_copy_bytes(bi.rec, S.pb, size * size + 2 * sC * sC);
       } else {
-        cy = te_enc_inter_comp(F, S, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split);
-        cu = te_enc_inter_comp(F, S, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + TE_COEF_COMP, recU, itype | 1,
-                               tb_split && size > 8);
-        cv = te_enc_inter_comp(F, S, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * TE_COEF_COMP, recV,
-                               itype | 1, tb_split && size > 8);
+        cy = te_enc_inter_comp(F, S, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
+        cu = te_enc_inter_comp(F, S, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1,
+                               tb_split && size > 8, p.ts);
+        cv = te_enc_inter_comp(F, S, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV,
+                               itype | 1, tb_split && size > 8, p.ts);
       }
     }
   }
@@ -902,6 +917,8 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
   te_zero_words(&tmp, sizeof(TeParam));
   te_sync();
   tmp.coeff = tmp_coef;
+  tmp.cs = bi.bp.cs;
+  tmp.ts = bi.bp.ts;
   if (frame_type != TE_I) {  // skip candidates
     tmp.tb_param = 0;
     tmp.pb_part = 0;
@@ -1184,6 +1201,8 @@ TE_NOINL int te_search_early_skip(const TeFrame &F_, TeScratch S_, TeSB &sb_, Te
   te_zero_words(&tmp, sizeof(TeParam));
   te_sync();
   tmp.coeff = tmp_coef;
+  tmp.cs = bi.bp.cs;
+  tmp.ts = bi.bp.ts;
   for (int k = 0; k < bi.num_skip; k++) {
     tmp.tb_param = 0;
     tmp.skip_idx = k;
@@ -1239,12 +1258,19 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, i
   bi.max_num_tb_part = F.enable_tb_split == 1 ? 2 : 1;
   bi.max_num_pb_part = F.enable_pb_split ? 4 : 1;
   bi.delta_qp = qp - F.qp;
-  bi.rec = lv.rbuf[0];
-  bi.rec_best = lv.rbuf[1];
-  bi.best_bits = lv.bbits;
+  // this level's buffers: LDS for the small levels (TeSmallLv), the worker's global scratch otherwise
+  TeSmallLv &sl = *S.sl;
+  int16_t *const cb0 = SIZE == 16 ? sl.cf2[0] : (SIZE == 8 ? sl.cf3[0] : lv.cbuf[0]);
+  int16_t *const cb1 = SIZE == 16 ? sl.cf2[1] : (SIZE == 8 ? sl.cf3[1] : lv.cbuf[1]);
+  bi.rec = SIZE == 32 ? sl.rec1[0] : (SIZE == 16 ? sl.rec2[0] : (SIZE == 8 ? sl.rec3[0] : lv.rbuf[0]));
+  bi.rec_best = SIZE == 32 ? sl.rec1[1] : (SIZE == 16 ? sl.rec2[1] : (SIZE == 8 ? sl.rec3[1] : lv.rbuf[1]));
+  bi.best_bits = SIZE == 16 ? sl.bb2 : (SIZE == 8 ? sl.bb3 : lv.bbits);
+  bi.best_cap = SIZE == 16 ? 128 : (SIZE == 8 ? 64 : TE_BEST_WORDS);
   bi.best_nbits = -1;
-  bi.bp.coeff = lv.cbuf[0];
-  int16_t *tmp_coef = lv.cbuf[1];
+  bi.bp.coeff = cb0;
+  bi.bp.cs = TE_CS(SIZE);
+  bi.bp.ts = TE_TS(SIZE);
+  int16_t *tmp_coef = cb1;
   if (ft != TE_I) {
     bi.num_skip = te_mv_skip(ypos, xpos, W, H, SIZE, F.cells, bi.skip_c);
     bi.num_merge = te_mv_skip(ypos, xpos, W, H, SIZE, F.cells, bi.merge_c);
@@ -1280,7 +1306,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, i
   if (encode_this) {
     bi.final_encode = 0;
     // the tmp coefficient set: whichever of cbuf[0..1] the best does not hold
-    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == lv.cbuf[0] ? lv.cbuf[1] : lv.cbuf[0]);
+    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
     const int me_threshold = SIZE * SIZE * te_iq8[qp] / 8;
     if constexpr (SIZE > 8) {
       if (top_down && cost > (uint32_t)me_threshold) {
@@ -1301,7 +1327,7 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, i
     }
   } else if (encode_rect) {
     bi.final_encode = 0;
-    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == lv.cbuf[0] ? lv.cbuf[1] : lv.cbuf[0]);
+    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
     if (cost <= cost_small) {
       te_rewind(b, pos_ref);
       bi.final_encode = 1;

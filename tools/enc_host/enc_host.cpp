@@ -75,7 +75,7 @@ int main(int argc, char **argv) {
   std::vector<TeCell> cells((size_t)(W / 4) * (H / 4));
   std::vector<or_cell_t> ocells(cells.size());
   TeScratchMem *SM = (TeScratchMem *)calloc(1, sizeof(TeScratchMem));
-  const TeScratch S = te_scratch(*SM, &SM->tx, &SM->nb, SM->pb, SM->bi, &SM->tmp);
+  const TeScratch S = te_scratch(*SM, &SM->tx, &SM->nb, SM->pb, SM->bi, &SM->tmp, &SM->sl);
   te_load_basis(SM->tx);
   TeSB sb;
   std::vector<uint32_t> sbw(1 << 17);
