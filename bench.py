@@ -266,6 +266,61 @@ def interp_leg(torch, lib, reps: int = 50):
             "note": "hipEvents on torch's current stream (the launches' stream); not part of `value`"}
 
 
+def interp_frames_leg(torch, lib, clip: np.ndarray, reps: int = 10):
+    """The whole temporal-interpolated reference of BASELINE config 5
+    (thor_interpolate_frames: both luma pyramids, motion_estimate_bi on every
+    level, interpolate_frame; common/temporal_interp.c:972-1053) from frames 0
+    and 2 of the 4K clip (ratio 2, pos 1: dec/decode_frame.c's symmetric B
+    case), on torch's current stream.  Not part of `value`; the reference's own
+    interpolate_frames takes 33.6 ms for the same pair on one core of the build
+    container (profiles/r02c_interp_speed.json)."""
+    W, H = 3840, 2160
+    dev = torch.device("cuda", torch.cuda.current_device())
+    keep = []
+
+    def padded(fr):
+        y = fr[:W * H].reshape(H, W)
+        u = fr[W * H:W * H * 5 // 4].reshape(H // 2, W // 2)
+        v = fr[W * H * 5 // 4:].reshape(H // 2, W // 2)
+        ptrs, strides = [], []
+        for p, pad in ((y, 96), (u, 48), (v, 48)):
+            s = (p.shape[1] + 2 * pad + 15) & ~15
+            full = np.zeros((p.shape[0] + 2 * pad, s), np.uint8)
+            full[:, :p.shape[1] + 2 * pad] = np.pad(p, pad, mode="edge")
+            t = torch.from_numpy(full).to(dev)
+            keep.append(t)
+            ptrs.append(t.data_ptr() + pad * s + pad)
+            strides.append(s)
+        return L_planes(ptrs[0], ptrs[1], ptrs[2], strides[0], strides[1])
+
+    from thor_amd.lib import ThorYuvPlanes as L_planes
+
+    ra, rb = padded(clip[0]), padded(clip[2])
+    ro = padded(np.zeros_like(clip[0]))
+    st = torch.cuda.current_stream().cuda_stream
+    t = lib.thor_ti_create(W, H, torch.cuda.current_device())
+    try:
+        def run():
+            assert lib.thor_interpolate_frames(t, C.byref(ra), C.byref(rb), 96, C.byref(ro), 2, 1, st) == 0
+
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        assert lib.thor_ti_status(t) == 0
+        ms = e0.elapsed_time(e1) / reps
+    finally:
+        lib.thor_ti_destroy(t)
+    return {"workload": "4K interpolated reference from frames 0 and 2 of the clip (pyramid + motion search on "
+                        "4 levels + compensation)", "ms_per_frame": round(ms, 3),
+            "reference_cpu_ms_per_frame_1core": 33.6,
+            "note": "hipEvents on torch's current stream; latency-bound (the search is a wavefront of step rows)"}
+
+
 def cpu_baseline(meta, clip: np.ndarray, procs: int = HOST_THREADS, budget_s: float = 8.0):
     """The reference encoder + decoder (oracle/_ref/Thorenc, Thordec: SIMD
     build, -O3) on the same clip and configuration: `procs` concurrent
@@ -632,6 +687,7 @@ def main():
             out["encoder_tu_chain"] = encoder_leg(torch, lib)
             out["temporal_pyramid"] = pyramid_leg(torch, lib)
             out["temporal_interp_comp"] = interp_leg(torch, lib)
+            out["temporal_interp_frame"] = interp_frames_leg(torch, lib, clip)
         if not a.no_cpu_baseline and world == 1:
             cb = cpu_baseline(meta, clip)
             if cb is not None:

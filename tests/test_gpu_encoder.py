@@ -162,3 +162,28 @@ def test_enc_cost_batch(L):
         v = s + int(np.int32(np.float64(lam) * np.float64(nbits[c]) + 0.5))
         v = min(v & 0xFFFFFFFF, 1 << 30) if v <= (1 << 30) else (1 << 30)
         assert cost[c] == v, c
+
+
+def test_enc_cost_batch_vs_reference_cost_calc(L):
+    """k_enc_cost against the reference's own cost_calc (tests/golden/cost.npz,
+    tools/make_cost_goldens.py: ssd_calc + cost_calc of libthor_ref.so on
+    random blocks of every CU size, the encoder's lambda range and the 2^30
+    clamp): the three SSDs of each case as three TUs of one candidate."""
+    import os
+
+    from conftest import GOLD
+
+    z = np.load(os.path.join(GOLD, "cost.npz"))
+    ssd, nbits, lam, want = z["ssd"], z["nbits"], z["lam"], z["cost"]
+    D = Dev(L)
+    try:
+        first, counts = np.zeros(1, np.int32), np.full(1, 3, np.int32)
+        p_first, p_counts = D.put(first), D.put(counts)
+        d_cost = D.empty(4)
+        for i in range(len(want)):
+            p_ssd, p_nb = D.put(np.ascontiguousarray(ssd[i])), D.put(nbits[i:i + 1])
+            assert L.thor_enc_cost_batch(p_ssd, p_first, p_counts, p_nb, float(lam[i]), d_cost, 1, None) == 0
+            got = D.get(d_cost, (1,), np.uint32)[0]
+            assert got == want[i], (i, int(got), int(want[i]))
+    finally:
+        D.free()
