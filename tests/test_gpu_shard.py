@@ -67,3 +67,19 @@ def test_row_sharded_decode_matches_reference(name, nframes, world):
     for p in procs:
         p.join(timeout=30)
     assert res == [(r, []) for r in range(world)], res
+
+
+def test_row_shard_device_exchange_rccl():
+    """The RCCL branch (device buffers, decoder on its own stream, events
+    between it and the collective's stream): bench.py --shard rows on one rank,
+    4K stream md5 vs the reference decoder."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29531")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--shard", "rows", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=110, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["bit_exact"] is True, line

@@ -20,7 +20,7 @@
 #include "enc_gop.h"
 #include "enc_rd.h"
 
-#define THOR_ENC_MAX_BATCH 64
+#define THOR_ENC_MAX_BATCH 256
 #define THOR_ENC_SB_WORDS 4096  // 131072 bits of one SB's stream (trial writes included)
 
 __global__ void k_deblock_v(const FrameBatch, int, int);

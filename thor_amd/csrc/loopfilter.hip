@@ -69,9 +69,12 @@ __device__ __forceinline__ void luma_v_items(int t0, int tstep, uint8_t *Y, int 
     if (on0[r] || on1[r]) {
       const uint8_t *base = Y + (long long)ii[r] * sy + jj[r] - 4;
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        A[r][k] = *(const uint32_t *)(base + (long long)k * sy);
-        Bv[r][k] = *(const uint32_t *)(base + (long long)k * sy + 4);
+      for (int k = 0; k < 8; k++) {  // rows 2 and 5 feed the activity test; the rest only where filtered
+        A[r][k] = Bv[r][k] = 0;
+        if (k == 2 || k == 5 || (k < 4 ? on0[r] : on1[r])) {
+          A[r][k] = *(const uint32_t *)(base + (long long)k * sy);
+          Bv[r][k] = *(const uint32_t *)(base + (long long)k * sy + 4);
+        }
       }
     }
   }
@@ -99,7 +102,8 @@ __device__ __forceinline__ void luma_v_items(int t0, int tstep, uint8_t *Y, int 
 #undef Q1
     uint8_t *base = Y + (long long)ii[r] * sy + jj[r] - 4;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < 8; k++) {  // only the filtered half's rows go back
+      if (!(k < 4 ? on0[r] : on1[r])) continue;
       *(uint32_t *)(base + (long long)k * sy) = A[r][k];
       *(uint32_t *)(base + (long long)k * sy + 4) = Bv[r][k];
     }

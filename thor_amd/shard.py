@@ -55,12 +55,13 @@ class RowShard:
         dec.set_band(b0, b1)
         import torch
 
+        self.dstream = None
         if device_exchange:
             dev = torch.device("cuda", torch.cuda.current_device())
-            # the band copies (decoder stream) and the collective (torch's current
-            # stream) must be ordered: run the decoder on torch's current stream
-            if hasattr(dec, "set_stream"):
-                dec.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            # the band copies run on the decoder's stream, the collective on
+            # torch's current stream: events order them both ways (decode())
+            if hasattr(dec, "stream"):
+                self.dstream = torch.cuda.ExternalStream(dec.stream(), device=dev)
             self.send = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
             self.recv = torch.empty(self.world * self.nbytes, dtype=torch.uint8, device=dev)
         else:
@@ -73,8 +74,19 @@ class RowShard:
         d.begin(devframe)
         y0 = self.rank * self.rows
         if self.device_exchange:
+            import torch
+
             d.get_rows(frame_num, y0, self.rows, self.send.data_ptr())
+            cur = torch.cuda.current_stream()
+            if self.dstream is not None:  # the band rows are in `send` before the all-gather reads them
+                ev = torch.cuda.Event()
+                ev.record(self.dstream)
+                cur.wait_event(ev)
             self.dist.all_gather_into_tensor(self.recv, self.send)
+            if self.dstream is not None:  # put_rows (and the next frame's get_rows) after the all-gather
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                self.dstream.wait_event(ev)
             for r in range(self.world):
                 if r != self.rank:
                     d.put_rows(frame_num, r * self.rows, self.rows, self.recv.data_ptr() + r * self.nbytes)
