@@ -416,7 +416,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the kernel legs reported beside `value`")
-    ap.add_argument("--streams", type=int, default=64, help="independent streams (encoder + decoder) per GPU")
+    ap.add_argument("--streams", type=int, default=192, help="independent streams (encoder + decoder) per GPU")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
                     help="streams: independent enc+dec streams per GPU (default); rows: decode-only, ONE "
                          "stream's SB rows split across the ranks with an RCCL all-gather before intra/deblock")
