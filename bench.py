@@ -503,6 +503,7 @@ def main():
         return devs
 
     dec_host_s = [0.0]  # parse + upload share of t_dec (serial steps)
+    pipe_tl = {}  # the last pipelined step's timeline (ms from its start)
 
     def step_pipe(ks):
         """Frame-pipelined encode + decode: while the GPU codes frame i + 1 of
@@ -512,6 +513,7 @@ def main():
         of both legs complete, the .bit files and the device frames."""
         for k in ks:
             encs[k].reset()
+        pipe_tl.update(enc_done_ms=[0.0] * nf, dec_enq_ms=[0.0] * nf)
         parsers = [Parser() for _ in ks]
         bits = [[] for _ in ks]
         devs = [[None] * nf for _ in ks]
@@ -533,6 +535,7 @@ def main():
                             decode_batch([decs[ks[j]] for j in g], [ds[j] for j in g])
                     for j in range(len(ks)):
                         devs[j][i] = ds[j]
+                    pipe_tl["dec_enq_ms"][i] = round((time.perf_counter() - t0) * 1e3, 1)
             except BaseException as e:  # re-raised by the caller
                 err.append(e)
 
@@ -545,8 +548,10 @@ def main():
                 for j, ch in enumerate(chunks):
                     bits[j].append(ch)
                 q.put([ch[4:] for ch in chunks])  # payload after the 4-byte chunk length (dec/getbits.c:48-69)
+                pipe_tl["enc_done_ms"][i] = round((time.perf_counter() - t0) * 1e3, 1)
         finally:
             th.join()
+        pipe_tl["consumer_done_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         for k in ks:
             decs[k].sync()
         t = time.perf_counter() - t0
@@ -653,6 +658,7 @@ def main():
                 "streams_per_gpu": K,
                 "pipelining": "frame-pipelined: the host parse + upload + GPU reconstruction of frame i "
                               "run while the GPU encodes frame i + 1 (value = wall time of both legs complete)",
+                "pipe_timeline_last_step": pipe_tl,
                 "serial_t_enc_ms": round(t_enc * 1e3, 2),
                 "serial_t_dec_ms": round(t_dec * 1e3, 2),
                 "serial_mpx_s": round(K * px_stream / (t_enc + t_dec) / 1e6, 2),
