@@ -417,6 +417,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the kernel legs reported beside `value`")
     ap.add_argument("--streams", type=int, default=192, help="independent streams (encoder + decoder) per GPU")
+    ap.add_argument("--band-local", action="store_true",
+                    help="--shard rows: each rank deblocks / CLPFs only its band, then a second all-gather of final rows")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
                     help="streams: independent enc+dec streams per GPU (default); rows: decode-only, ONE "
                          "stream's SB rows split across the ranks with an RCCL all-gather before intra/deblock")
@@ -730,7 +732,7 @@ def rows_mode(a, torch, dist, rank, world, local):
     seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
     dec = GpuDecoder(seq, device=local)
     devs = [dec.upload(fr) for fr in frames]
-    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True)
+    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=a.band_local)
 
     def step():
         for d, fr in zip(devs, frames):
@@ -762,7 +764,9 @@ def rows_mode(a, torch, dist, rank, world, local):
             "vs_baseline": None, "dtype": "u8/i16", "data": "synthetic (seeded clip) encoded by the reference Thorenc",
             "bit_exact": ok,
             "config": {"workload": "ONE 4K 8-frame LDB-low stream, SB rows sharded across %d GPU(s): band k_recon, "
-                                   "RCCL all-gather of pre-deblock bands, whole-frame intra/deblock/CLPF/pad" % world,
+                                   "RCCL all-gather of pre-deblock bands, whole-frame intra, %s" % (
+                                   world, "band-local deblock/CLPF + all-gather of final bands, pad" if a.band_local
+                                   else "whole-frame deblock/CLPF/pad"),
                        "parallelism": "rows%d" % world, "frames": len(frames)},
         }), flush=True)
     dec.close()

@@ -162,6 +162,15 @@ int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_
 int thor_dec_frame_end(thor_dec_t *d);
 int thor_dec_get_rows(thor_dec_t *d, int frame_num, int y0, int nrows, void *dst);
 int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const void *src);
+/* Band-local phase B (on = 1, with a band set): thor_dec_frame_end then
+ * enqueues intra for the whole frame (its chains cross bands) but deblocking
+ * and CLPF only for the band's rows (the deblocking reads a 2-row halo the
+ * first exchange already carries), and no padding; the caller exchanges the
+ * bands' final rows (get_rows / put_rows again, same packing) and calls
+ * thor_dec_frame_finish, which pads the frame and makes it a reference.  Each
+ * rank's loop filters then cover 1/N of the frame instead of all of it. */
+int thor_dec_set_band_local(thor_dec_t *d, int on);
+int thor_dec_frame_finish(thor_dec_t *d);
 
 /* Host helper: write the decode-order indices of the intra CUs of a frame
  * (host descriptors) to `out` (may be NULL to count); returns the count. */

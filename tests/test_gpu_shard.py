@@ -14,7 +14,7 @@ from conftest import GOLD
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, name, nframes, q):
+def _worker(rank, world, port, name, nframes, q, local=False):
     import hashlib
 
     import torch.distributed as dist
@@ -29,10 +29,16 @@ def _worker(rank, world, port, name, nframes, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         meta = json.load(open(os.path.join(GOLD, "streams.json")))[name]
-        seq, frames = load_trace(trace_path(name))
+        bit = os.path.join(GOLD, name + ".bit")
+        if os.path.exists(bit):  # the host parser's output (carries the interpolated-reference headers)
+            from thor_amd.bitstream import parse_stream
+
+            seq, frames = parse_stream(open(bit, "rb").read())
+        else:
+            seq, frames = load_trace(trace_path(name))
         frames = frames[:nframes]
         dec = GpuDecoder(seq)
-        sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=False)
+        sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=False, band_local=local)
         bad = []
         for fr in frames:
             sh.decode(dec.upload(fr), fr.frame_num)
@@ -49,8 +55,12 @@ def _worker(rank, world, port, name, nframes, q):
             dec.close()
 
 
-@pytest.mark.parametrize("name,nframes,world", [("cif_high", 10, 2), ("hd_low", 6, 2), ("cif_med", 10, 3), ("k4_med", 8, 2)])
-def test_row_sharded_decode_matches_reference(name, nframes, world):
+@pytest.mark.parametrize("name,nframes,world,local", [
+    ("cif_high", 10, 2, False), ("hd_low", 6, 2, False), ("cif_med", 10, 3, False), ("k4_med", 8, 2, False),
+    # band-local phase B: each rank deblocks / CLPFs its own band, second exchange of final rows
+    ("cif_high", 10, 2, True), ("cif_med", 10, 3, True), ("hd_low", 6, 3, True), ("k4_med", 8, 2, True),
+    ("cif_hdbi", 9, 2, True)])
+def test_row_sharded_decode_matches_reference(name, nframes, world, local):
     import random
     import sys
 
@@ -60,7 +70,7 @@ def test_row_sharded_decode_matches_reference(name, nframes, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, nframes, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, nframes, q, local)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=110) for _ in procs)
@@ -69,7 +79,8 @@ def test_row_sharded_decode_matches_reference(name, nframes, world):
     assert res == [(r, []) for r in range(world)], res
 
 
-def test_row_shard_device_exchange_rccl():
+@pytest.mark.parametrize("local", [False, True])
+def test_row_shard_device_exchange_rccl(local):
     """The RCCL branch (device buffers, decoder on its own stream, events
     between it and the collective's stream): bench.py --shard rows on one rank,
     4K stream md5 vs the reference decoder."""
@@ -79,7 +90,7 @@ def test_row_shard_device_exchange_rccl():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29531")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--shard", "rows", "--steps", "2",
-                        "--warmup", "1"], capture_output=True, text=True, timeout=110, env=env, cwd=root)
+                        "--warmup", "1"] + (["--band-local"] if local else []), capture_output=True, text=True, timeout=110, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["bit_exact"] is True, line

@@ -31,11 +31,15 @@ class NumpyContext:
     def __init__(self, W, H, truth):
         self.W, self.H, self.truth = W, H, truth
         self.band = None
+        self.local = False
         self.cur = None
         self.bufs = {}
 
     def set_band(self, b0, b1):
         self.band = (b0, b1)
+
+    def set_band_local(self, on):
+        self.local = on
 
     def begin(self, fnum):  # the "device frame" is the frame number here
         y, u, v = (np.zeros_like(p) for p in self.truth[fnum])
@@ -82,9 +86,21 @@ class NumpyContext:
         fnum, planes = self.cur
         for got, want in zip(planes, self.truth[fnum]):
             assert np.array_equal(got, want), fnum
+        if self.local:  # band-local phase B: only the band's rows are final, model the rest as stale
+            r0, r1 = 64 * self.band[0], min(64 * self.band[1], self.H)
+            for k, p in enumerate(planes):
+                a, b = (r0, r1) if k == 0 else (r0 // 2, r1 // 2)
+                p[:a] ^= 0x5A
+                p[b:] ^= 0x5A
+
+    def finish(self):
+        assert self.local
+        fnum, planes = self.cur
+        for got, want in zip(planes, self.truth[fnum]):
+            assert np.array_equal(got, want), fnum
 
 
-def _worker(rank, world, port, W, H, q):
+def _worker(rank, world, port, W, H, q, local=False):
     import torch.distributed as dist
 
     from thor_amd.shard import RowShard
@@ -96,7 +112,7 @@ def _worker(rank, world, port, W, H, q):
         truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
                      rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(3)}
         ctx = NumpyContext(W, H, truth)
-        sh = RowShard(ctx, dist, W, H, device_exchange=False)
+        sh = RowShard(ctx, dist, W, H, device_exchange=False, band_local=local)
         for f in range(3):
             sh.decode(f, f)
         dist.barrier()
@@ -106,8 +122,9 @@ def _worker(rank, world, port, W, H, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 352, 288), (3, 256, 200), (2, 128, 64)])
-def test_row_shard_exchange_gloo(world, W, H):
+@pytest.mark.parametrize("world,W,H,local", [(2, 352, 288, False), (3, 256, 200, False), (2, 128, 64, False),
+                                             (2, 352, 288, True), (3, 256, 200, True)])
+def test_row_shard_exchange_gloo(world, W, H, local):
     import random
 
     import torch.multiprocessing as mp
@@ -115,7 +132,7 @@ def test_row_shard_exchange_gloo(world, W, H):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q, local)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -64,7 +64,9 @@ struct thor_dec {
   int stop_stage;
   hipEvent_t xev[2];  // cross-stream ordering when a batch mixes contexts on different streams
   int band0, band1;    // SB rows k_recon reconstructs (row sharding); band1 0 = all
-  void *pending;       // Batch of a thor_dec_frame_begin awaiting its _end
+  int band_local;      // phase B filters only the band's rows (thor_dec_set_band_local)
+  void *pending;       // Batch of a thor_dec_frame_begin awaiting its _end (or, band-local, its _finish)
+  int pending_ended;   // band-local: _end done, _finish (pad + commit) due
   // temporal-interpolated references (seq.interp_ref): slot `islot` after the
   // ring holds the current frame's interpolated reference; `ti` its scratch
   int islot;
@@ -170,6 +172,8 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->timing = 0;
   d->xev[0] = d->xev[1] = nullptr;
   d->band0 = d->band1 = 0;
+  d->band_local = 0;
+  d->pending_ended = 0;
   d->pending = nullptr;
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
@@ -415,6 +419,12 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.clpf_on = d->stop_stage >= 2 && d->seq.clpf && hdrs[i].clpf_on && in.clpf_flags;
     f.band0 = d->band0;
     f.band1 = d->band1 > 0 ? d->band1 : f.nsbrows;
+    f.pb0 = f.pb1 = 0;
+    if (d->band_local && d->band1 > 0) {
+      f.pb0 = d->band0 * 64;
+      f.pb1 = d->band1 * 64 < H ? d->band1 * 64 : H;
+      if (f.pb1 <= f.pb0) f.pb0 = f.pb1 = H;  // an empty band: nothing to filter (pb1 > 0 keeps it band-local)
+    }
     b.max_prep = b.max_prep > f.nprep + f.nres + 1 ? b.max_prep : f.nprep + f.nres + 1;
     b.any_intra |= in.n_intra > 0;
     b.max_intra = b.max_intra > in.n_intra ? b.max_intra : in.n_intra;
@@ -489,8 +499,9 @@ static int batch_phase_a(thor_dec *lead, const Batch &b) {
   return THOR_OK;
 }
 
-// Phase B: intra, deblock, CLPF, reference padding.
-static int batch_phase_b(thor_dec *lead, const Batch &b) {
+// Phase B: intra, deblock, CLPF, reference padding (pad = 0: the band-local
+// form, padded by thor_dec_frame_finish after the final-rows exchange).
+static int batch_phase_b(thor_dec *lead, const Batch &b, int pad = 1) {
   const int W = lead->seq.width, H = lead->seq.height, n = b.n;
   hipStream_t st = lead->stream;
   const int nrows = (H + 63) / 64;
@@ -520,7 +531,7 @@ static int batch_phase_b(thor_dec *lead, const Batch &b) {
     k_clpf<<<dim3(b.clpf_grid, n), 256, 0, st>>>(b.fb);
     HIPCHK(hipGetLastError());
   }
-  {
+  if (pad) {
     StageMark m(lead, ST_PAD);
     k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(b.fb);
     HIPCHK(hipGetLastError());
@@ -537,6 +548,8 @@ static void batch_commit(thor_dec_t *const *ds, const Batch &b) {
 
 static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins) {
   thor_dec *lead = ds[0];
+  for (int i = 0; i < n; i++)  // band-local phase B needs the begin / end / finish protocol
+    if (ds[i]->band_local && ds[i]->band1 > 0) return THOR_ERR_ARG;
   Batch b;
   int rc = batch_prepare(ds, n, hdrs, ins, b);
   if (rc != THOR_OK) return rc;
@@ -573,8 +586,14 @@ int thor_dec_set_band(thor_dec_t *d, int sb_row0, int sb_row1) {
   return THOR_OK;
 }
 
+int thor_dec_set_band_local(thor_dec_t *d, int on) {
+  if (!d || d->pending) return THOR_ERR_ARG;
+  d->band_local = on != 0;
+  return THOR_OK;
+}
+
 int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_frame_in_t *in) {
-  if (!d || !hdr || !in) return THOR_ERR_ARG;
+  if (!d || !hdr || !in || d->pending) return THOR_ERR_ARG;
   Batch *b = new Batch();
   thor_dec_t *ds[1] = {d};
   int rc = batch_prepare(ds, 1, hdr, in, *b);
@@ -591,13 +610,37 @@ int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_
 }
 
 int thor_dec_frame_end(thor_dec_t *d) {
-  if (!d || !d->pending) return THOR_ERR_ARG;
+  if (!d || !d->pending || d->pending_ended) return THOR_ERR_ARG;
   Batch *b = (Batch *)d->pending;
   HIPCHK(hipSetDevice(d->device));
-  int rc = batch_phase_b(d, *b);
+  const int local = b->fb.f[0].pb1 > 0;
+  int rc = batch_phase_b(d, *b, !local);
+  if (rc == THOR_OK && local) {  // the final-rows exchange, then thor_dec_frame_finish
+    d->pending_ended = 1;
+    return THOR_OK;
+  }
   thor_dec_t *ds[1] = {d};
   if (rc == THOR_OK) batch_commit(ds, *b);
   d->pending = nullptr;
+  delete b;
+  return rc;
+}
+
+int thor_dec_frame_finish(thor_dec_t *d) {
+  if (!d || !d->pending || !d->pending_ended) return THOR_ERR_ARG;
+  Batch *b = (Batch *)d->pending;
+  HIPCHK(hipSetDevice(d->device));
+  const int W = d->seq.width, H = d->seq.height;
+  int rc = THOR_OK;
+  {
+    StageMark m(d, ST_PAD);
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(b->fb);
+    if (hipGetLastError() != hipSuccess) rc = THOR_ERR_HIP;
+  }
+  thor_dec_t *ds[1] = {d};
+  if (rc == THOR_OK) batch_commit(ds, *b);
+  d->pending = nullptr;
+  d->pending_ended = 0;
   delete b;
   return rc;
 }

@@ -52,6 +52,7 @@ struct FrameCtx {
   int qp, qpc, deblock, clpf_on;
   int band0, band1;  // SB rows k_recon reconstructs (row-band sharding); all by default
   int islot;         // slot of the frame's temporal-interpolated reference (blocks' ref -2), -1 none
+  int pb0, pb1;      // band-local phase B: luma rows [pb0, pb1) deblocked / CLPF'd here; pb1 = 0: whole frame
 };
 // A batch of frames travels in the kernel argument segment (8 x 384 B, under
 // the 4 KB kernarg limit): the host fills it per call, no upload copy.  Every

@@ -41,7 +41,7 @@ __device__ __forceinline__ void filt4(int &p1, int &p0, int &q0, int &q1, int tc
 // (2) the pixels of the items that are on, (3) activity test, filter, store.
 template <int R>
 __device__ __forceinline__ void luma_v_items(int t0, int tstep, uint8_t *Y, int sy, int W, int H,
-                                             const uint16_t *cell, int qp) {
+                                             const uint16_t *cell, int qp, int g0 = 0, int g1 = 1 << 30) {
   const int ne = (W >> 3) - 1, cs = W >> 2;
   const int beta = beta_of(qp), tc = tc_of(qp);
   int ii[R], jj[R];
@@ -52,7 +52,7 @@ __device__ __forceinline__ void luma_v_items(int t0, int tstep, uint8_t *Y, int 
     ii[r] = g * 8;
     jj[r] = e * 8;
     cq[r][0] = cq[r][1] = cq[r][2] = cq[r][3] = 0;
-    if (g < (H >> 3)) {
+    if (g < (H >> 3) && g >= g0 && g < g1) {  // [g0, g1): 8-row groups of a row band (phase_b_rows)
       const int qa = (ii[r] >> 2) * cs + (jj[r] >> 2);
       cq[r][0] = cell[qa - 1];
       cq[r][1] = cell[qa];
@@ -112,7 +112,7 @@ __device__ __forceinline__ void luma_v_items(int t0, int tstep, uint8_t *Y, int 
 
 template <int R>
 __device__ __forceinline__ void luma_h_items(int t0, int tstep, uint8_t *Y, int sy, int W, int H,
-                                             const uint16_t *cell, int qp) {
+                                             const uint16_t *cell, int qp, int i0 = 0, int i1 = 1 << 30) {
   const int ng = W >> 3, cs = W >> 2;
   const int beta = beta_of(qp), tc = tc_of(qp);
   int ii[R], jj[R];
@@ -123,7 +123,7 @@ __device__ __forceinline__ void luma_h_items(int t0, int tstep, uint8_t *Y, int 
     ii[r] = (k + 1) * 8;
     jj[r] = gcol * 8;
     cq[r][0] = cq[r][1] = cq[r][2] = cq[r][3] = 0;
-    if (ii[r] < H) {
+    if (ii[r] < H && ii[r] >= i0 && ii[r] <= i1) {  // [i0, i1]: edges of a row band (phase_b_rows)
       const int qa = (ii[r] >> 2) * cs + (jj[r] >> 2);
       cq[r][0] = cell[qa - cs];
       cq[r][1] = cell[qa];
@@ -177,11 +177,11 @@ __device__ __forceinline__ void luma_h_items(int t0, int tstep, uint8_t *Y, int 
 // Chroma (deblock_frame_uv): intra-only edges, p0/q0 modified.  One thread
 // per (edge, 8-luma-row/column group) per plane (blockIdx.y = plane).
 __device__ __forceinline__ void k_deblock_chroma_v_body(int t, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
-                                                          const uint16_t *cell, int qpc) {
+                                                          const uint16_t *cell, int qpc, int g0 = 0, int g1 = 1 << 30) {
   uint8_t *C = by ? V : U;
   int ne = (W >> 3) - 1;
   int g = t / ne, e = t - g * ne + 1;
-  if (g >= (H >> 3)) return;
+  if (g >= (H >> 3) || g < g0 || g >= g1) return;
   int i = g * 8, j = e * 8;
   int cs = W >> 2;
   int qi = (i >> 2) * cs + (j >> 2);
@@ -202,12 +202,12 @@ __device__ __forceinline__ void k_deblock_chroma_v_body(int t, int by, uint8_t *
 }
 
 __device__ __forceinline__ void k_deblock_chroma_h_body(int t, int by, uint8_t *U, uint8_t *V, int sc, int W, int H,
-                                                          const uint16_t *cell, int qpc) {
+                                                          const uint16_t *cell, int qpc, int i0 = 0, int i1 = 1 << 30) {
   uint8_t *C = by ? V : U;
   int ng = W >> 3;
   int k = t / ng, gcol = t - k * ng;
   int i = (k + 1) * 8, j = gcol * 8;
-  if (i >= H) return;
+  if (i >= H || i < i0 || i > i1) return;
   int cs = W >> 2;
   int qi = (i >> 2) * cs + (j >> 2);
   uint16_t P = cell[qi - cs], Q = cell[qi];
@@ -243,6 +243,26 @@ __device__ __forceinline__ void k_deblock_chroma_h_body(int t, int by, uint8_t *
 // segment of its left / right (vertical pass) or top / bottom (horizontal
 // pass) boundary.  An edge between two intra CUs is filtered once, by the CU
 // on its Q side.
+// Row band of a band-local phase B (row sharding, FrameCtx.pb0/pb1 luma rows;
+// pb1 = 0: the whole frame).  For every pixel of rows [y0, y1) to come out
+// final: horizontal edges at rows i in [y0, y1] (the edge at y1 writes rows
+// y1 - 2, y1 - 1) and vertical edges on the 8-row groups covering rows
+// [y0 - 2, y1 + 2) that those read, i.e. groups [y0/8 - 1, y1/8 + 1).
+struct DbRows {
+  int g0, g1, i0, i1;
+  __device__ __forceinline__ explicit DbRows(const FrameCtx &f) {
+    if (f.pb1 > 0) {
+      g0 = (f.pb0 >> 3) - 1;
+      g1 = (f.pb1 >> 3) + 1;
+      i0 = f.pb0;
+      i1 = f.pb1;
+    } else {
+      g0 = 0;
+      g1 = i1 = 1 << 30;
+      i0 = 0;
+    }
+  }
+};
 __device__ __forceinline__ void chroma_intra_edges(const FrameCtx &f, int item, bool vertical) {
   const int lane = threadIdx.x & 63;
   if (item >= 2 * f.nintra) return;
@@ -256,12 +276,13 @@ __device__ __forceinline__ void chroma_intra_edges(const FrameCtx &f, int item, 
   const int j = vertical ? (side ? x + S : x) : x + 8 * k;
   if (i >= f.H || j >= f.W || (vertical ? j : i) < 8) return;
   if (side && CI_MODE(f.cellinfo[(i >> 2) * cs + (j >> 2)]) == M_INTRA) return;  // the intra Q CU owns it
+  const DbRows rb(f);
   if (vertical)
     k_deblock_chroma_v_body((i >> 3) * ((f.W >> 3) - 1) + (j >> 3) - 1, plane, f.cu, f.cv, f.sc, f.W, f.H,
-                            f.cellinfo, f.qpc);
+                            f.cellinfo, f.qpc, rb.g0, rb.g1);
   else
     k_deblock_chroma_h_body(((i >> 3) - 1) * (f.W >> 3) + (j >> 3), plane, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo,
-                            f.qpc);
+                            f.qpc, rb.i0, rb.i1);
 }
 
 // DB_ITEMS luma edge segments per lane (grid-stride): a quarter as many
@@ -281,10 +302,12 @@ __global__ __launch_bounds__(256) void k_deblock_v(const FrameBatch fb_, int nbl
     }
     const int c = (b - nbl) >= nbl, bb = b - nbl - c * nbl;  // every chroma edge segment, per plane
     for (int r = 0; r < DB_ITEMS; r++)
-      k_deblock_chroma_v_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+      k_deblock_chroma_v_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc,
+                              DbRows(f).g0, DbRows(f).g1);
     return;
   }
-  luma_v_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+  const DbRows rb(f);
+  luma_v_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp, rb.g0, rb.g1);
 }
 __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl, int clist) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
@@ -298,10 +321,12 @@ __global__ __launch_bounds__(256) void k_deblock_h(const FrameBatch fb_, int nbl
     }
     const int c = (b - nbl) >= nbl, bb = b - nbl - c * nbl;  // every chroma edge segment, per plane
     for (int r = 0; r < DB_ITEMS; r++)
-      k_deblock_chroma_h_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc);
+      k_deblock_chroma_h_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, f.cu, f.cv, f.sc, f.W, f.H, f.cellinfo, f.qpc,
+                              DbRows(f).i0, DbRows(f).i1);
     return;
   }
-  luma_h_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp);
+  const DbRows rb(f);
+  luma_h_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, f.cy, f.sy, f.W, f.H, f.cellinfo, f.qp, rb.i0, rb.i1);
 }
 
 // One flagged SB per workgroup.  The SB's pixels and its 64 8x8-block side
@@ -403,6 +428,10 @@ __global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
   if ((int)blockIdx.x >= nwork) return;
   const int sb = f.n_clpf >= 0 ? (int)f.clpf_list[blockIdx.x] : (int)blockIdx.x;
   if (sb >= (f.W >> 6) * (f.H >> 6)) return;
+  if (f.pb1 > 0) {  // band-local phase B: the band's SB rows only (CLPF reads nothing outside its SB)
+    const int r = sb / (f.W >> 6);
+    if (r < (f.pb0 >> 6) || r >= ((f.pb1 + 63) >> 6)) return;
+  }
   k_clpf_body(sb, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, f.cellinfo, f.clpf_flags, sY, sU, sV, sC);
 }
 

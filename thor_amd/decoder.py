@@ -157,6 +157,12 @@ class GpuDecoder:
     def end(self):
         L.check(self.lib.thor_dec_frame_end(self.h), "thor_dec_frame_end")
 
+    def set_band_local(self, on: bool):
+        L.check(self.lib.thor_dec_set_band_local(self.h, 1 if on else 0), "thor_dec_set_band_local")
+
+    def finish(self):
+        L.check(self.lib.thor_dec_frame_finish(self.h), "thor_dec_frame_finish")
+
     def get_rows(self, frame_num: int, y0: int, nrows: int, dst_ptr):
         L.check(self.lib.thor_dec_get_rows(self.h, frame_num, y0, nrows, dst_ptr), "thor_dec_get_rows")
 

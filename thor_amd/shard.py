@@ -11,6 +11,16 @@ Every rank holds a full decoder context for the stream.  Per frame:
      CLPF and padding of the whole frame, replicated on every rank, so every
      rank ends the frame with the identical full reference.
 
+With band_local=True, step 3 deblocks and CLPFs only the rank's band (the
+deblocking's 2-row halo is already there from step 2), then:
+
+  4. a second all-gather, of the bands' final rows;
+  5. thor_dec_frame_finish: padding, the frame becomes a reference.
+
+Each rank's loop filters then cover 1/N of the frame, for a second exchange of
+the same size.  Every rank still ends the frame with the identical full
+reference, so the next frame's motion vectors may reach anywhere.
+
 Band b covers SB rows [b*R, (b+1)*R), R = ceil(SB rows / world); the last band
 may run past the frame (those rows are not copied).
 """
@@ -44,7 +54,7 @@ class RowShard:
     torch.distributed, initialised; `device_exchange` selects device buffers
     (nccl/RCCL) or host staging (gloo)."""
 
-    def __init__(self, dec, dist, width: int, height: int, device_exchange: bool):
+    def __init__(self, dec, dist, width: int, height: int, device_exchange: bool, band_local: bool = False):
         self.dec, self.dist = dec, dist
         self.W, self.H = width, height
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
@@ -53,6 +63,9 @@ class RowShard:
         self.device_exchange = device_exchange
         b0, b1 = band_of(height, self.world, self.rank)
         dec.set_band(b0, b1)
+        self.band_local = band_local
+        if band_local:
+            dec.set_band_local(True)
         import torch
 
         self.dstream = None
@@ -72,6 +85,14 @@ class RowShard:
     def decode(self, devframe, frame_num: int):
         d = self.dec
         d.begin(devframe)
+        self._exchange(frame_num)  # the bands' pre-deblock rows (inter reconstruction)
+        d.end()
+        if self.band_local:
+            self._exchange(frame_num)  # the bands' final rows (intra, deblocked, CLPF'd)
+            d.finish()
+
+    def _exchange(self, frame_num: int):
+        d = self.dec
         y0 = self.rank * self.rows
         if self.device_exchange:
             import torch
@@ -98,4 +119,3 @@ class RowShard:
                 if r != self.rank:
                     d.h2d(self.scratch[r], self.recv[r].numpy())
                     d.put_rows(frame_num, r * self.rows, self.rows, self.scratch[r])
-        d.end()
