@@ -693,6 +693,11 @@ def main():
                 "avg_launch_us": round(recon_ms * 1e3, 2),
                 "frames_per_launch": B,
                 "launches": "batched P-frame decode launches of group 0 alone; hipEvents on its stream",
+                "dominant_kernel_note": "by GPU time the step is k_enc_rows (83.5 %, profiles/r02i_rocprof_stats.txt), "
+                                        "the encoder's superblock worker: integer RD search with negligible HBM traffic "
+                                        "and no MFMA work, latency bound inside the wave (SQ counters: 74 % of wave "
+                                        "time in s_waitcnt, DESIGN.md 3b), so neither roofline bounds it; this object "
+                                        "is k_recon, the north star's inter-reconstruction kernel",
             },
         }
         if world == 1 and not a.no_legs:
