@@ -416,7 +416,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the kernel legs reported beside `value`")
-    ap.add_argument("--streams", type=int, default=192, help="independent streams (encoder + decoder) per GPU")
+    ap.add_argument("--streams", type=int, default=240, help="independent streams (encoder + decoder) per GPU")
     ap.add_argument("--band-local", action="store_true",
                     help="--shard rows: each rank deblocks / CLPFs only its band, then a second all-gather of final rows")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
@@ -459,7 +459,7 @@ def main():
 
     lib = L.load()
     want_bit = open(os.path.join(gold, "k4_low.bit"), "rb").read()
-    K = max(1, min(a.streams, 256))  # THOR_ENC_MAX_BATCH
+    K = max(1, min(a.streams, 512))  # THOR_ENC_MAX_BATCH
     encs = []
     for _ in range(K):
         e = GpuEncoder(params_for(meta["config"], W, H, nf, meta["extra"]), device=local)

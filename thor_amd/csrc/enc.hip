@@ -20,7 +20,8 @@
 #include "enc_gop.h"
 #include "enc_rd.h"
 
-#define THOR_ENC_MAX_BATCH 256
+#define THOR_ENC_MAX_BATCH 512
+#define TE_MAX_WORKERS 4096  // k_enc_rows workgroups per launch (4 x 1 024 SIMDs)
 #define THOR_ENC_SB_WORDS 4096  // 131072 bits of one SB's stream (trial writes included)
 
 __global__ void k_deblock_v(const FrameBatch, int, int);
@@ -478,7 +479,8 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   const int W = lead->W, H = lead->H;
   const int nrows = lead->nsbv;
   const int nwork = n * nrows;
-  int rc = pool_reserve(lead->device, (size_t)nwork, (size_t)n * (lead->nsb + 1));
+  int rc = pool_reserve(lead->device, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS),
+                        (size_t)n * (lead->nsb + 1));
   if (rc != THOR_OK) return rc;
   hipStream_t st = lead->stream;
   std::vector<TeJob> jobs(n);
@@ -495,7 +497,11 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   }
   EHIP(hipMemcpyAsync(g_pool.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
   EHIP(hipMemsetAsync(g_pool.ticket, 0, 4, st));
-  k_enc_rows<<<nwork, 64, 0, st>>>(g_pool.jobs, n, g_pool.ticket, nrows, g_pool.scratch, g_pool.err);
+  // persistent workers take row tickets until none are left: more workgroups
+  // than the chip holds at once (one per SIMD at this kernel's register and LDS
+  // use) would only start as the first ones run out of work
+  k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(g_pool.jobs, n, g_pool.ticket, nrows,
+                                                                         g_pool.scratch, g_pool.err);
   EHIP(hipGetLastError());
   const int ncell = (W / 4) * (H / 4);
   k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(g_pool.jobs);
