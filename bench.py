@@ -416,6 +416,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the kernel legs reported beside `value`")
+    ap.add_argument("--dec-slots", type=int, default=10,
+                    help="reference ring slots per decoder context (LDB: up to 4 references + the current frame)")
     ap.add_argument("--streams", type=int, default=240, help="independent streams (encoder + decoder) per GPU")
     ap.add_argument("--band-local", action="store_true",
                     help="--shard rows: each rank deblocks / CLPFs only its band, then a second all-gather of final rows")
@@ -466,7 +468,7 @@ def main():
         e.upload_sequence(clip)
         encs.append(e)
     seq, _ = parse_stream(want_bit)
-    decs = [GpuDecoder(seq, device=local) for _ in range(K)]
+    decs = [GpuDecoder(seq, device=local, slots=a.dec_slots) for _ in range(K)]
     groups = [list(range(g, min(g + 8, K))) for g in range(0, K, 8)]  # THOR_MAX_BATCH contexts per launch
     for gk in groups:  # a group's members enqueue on their leader's stream
         for k in gk[1:]:
