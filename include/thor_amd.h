@@ -306,7 +306,7 @@ int thor_enc_num_frames(const thor_enc_t *e);
 int thor_enc_next_input(const thor_enc_t *e);
 void *thor_enc_stream(thor_enc_t *e);
 /* Code the next frame of each of `n` DIFFERENT contexts (same device and
- * size, n <= 64) with one launch per stage.  orig[i]: DEVICE pointer to the
+ * size, n <= 512) with one launch per stage.  orig[i]: DEVICE pointer to the
  * context's input frame thor_enc_next_input(es[i]), planar I420, luma stride
  * orig_stride[i] (NULL: width), chroma stride half of it.  Synchronous. */
 int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
