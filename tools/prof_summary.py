@@ -100,9 +100,14 @@ def main():
     if fr and wr and len(fr) == len(wr):
         pf = [v for i, v in enumerate(fr) if i % 8 != 0]
         pw = [v for i, v in enumerate(wr) if i % 8 != 0]
-        traffic["recon_hbm_bytes_per_p_launch"] = round((sum(pf) * 2 + sum(pw)) * 1024 / len(pf))
+        # the PMC driver (profile_round.sh: tools/decode_frames.py) launches one frame per k_recon; the
+        # bench's roofline launch carries 8 frames (THOR_MAX_BATCH), so its per-launch traffic is 8 x that
+        per_frame = (sum(pf) * 2 + sum(pw)) * 1024 / len(pf)
+        traffic["recon_hbm_bytes_per_p_frame"] = round(per_frame)
+        traffic["recon_hbm_bytes_per_p_launch"] = round(8 * per_frame)
         traffic["recon_p_launches"] = len(pf)
-        traffic["recon_note"] = "bench.py --streams 8 --groups 1: one k_recon launch = 8 frames (THOR_MAX_BATCH)"
+        traffic["recon_note"] = ("tools/decode_frames.py k4_low 8: one k_recon launch per frame; per_p_launch = 8 "
+                                 "frames, the bench's batched launch (THOR_MAX_BATCH)")
     json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
     # the GPU box does not receive profiles/ (.gpurunignore): bench.py reads this copy
     json.dump(traffic, open(os.path.join(root, "tools", "traffic_latest.json"), "w"), indent=1)

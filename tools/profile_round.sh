@@ -8,7 +8,8 @@ OUT=gpurun_out/prof
 mkdir -p $OUT
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-legs"
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- $B > $OUT/trace_bench.json 2> $OUT/trace.err || { echo TRACE_FAIL; tail -20 $OUT/trace.err; exit 1; }
-# PMC passes on one group of 8 contexts (batched k_recon launches in frame order: the I frame is every 8th)
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run -- python3 bench.py --steps 2 --warmup 1 --streams 8 --no-cpu-baseline --no-legs > /dev/null 2> $OUT/fetch.err || { echo FETCH_FAIL; tail -20 $OUT/fetch.err; exit 1; }
-timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run -- python3 bench.py --steps 2 --warmup 1 --streams 8 --no-cpu-baseline --no-legs > /dev/null 2> $OUT/write.err || { echo WRITE_FAIL; tail -20 $OUT/write.err; exit 1; }
+# PMC passes on the decoder alone (the encoder's persistent workers run for minutes with counters on):
+# one 4K LDB-low frame per launch, frames in decode order I P P P P P P P
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run -- python3 tools/decode_frames.py k4_low 8 > /dev/null 2> $OUT/fetch.err || { echo FETCH_FAIL; tail -20 $OUT/fetch.err; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run -- python3 tools/decode_frames.py k4_low 8 > /dev/null 2> $OUT/write.err || { echo WRITE_FAIL; tail -20 $OUT/write.err; exit 1; }
 find $OUT -name '*.csv' | head -50
