@@ -289,7 +289,7 @@ typedef struct thor_enc_params {
 void thor_enc_default_params(thor_enc_params_t *p);
 /* 0 if the parameters are supported by the device encoder, else THOR_ERR_ARG
  * (check_parameters, enc/strings.c:431-479, plus this build's limits:
- * rdoq 0, no interp_ref, no speed-0 B frames). */
+ * rdoq 0, sync 0). */
 int thor_enc_check_params(const thor_enc_params_t *p);
 
 /* A device-resident encoder context: the reference's frame loop
@@ -306,7 +306,11 @@ int thor_enc_num_frames(const thor_enc_t *e);
 int thor_enc_next_input(const thor_enc_t *e);
 void *thor_enc_stream(thor_enc_t *e);
 /* Code the next frame of each of `n` DIFFERENT contexts (same device and
- * size, n <= 512) with one launch per stage.  orig[i]: DEVICE pointer to the
+ * size, n <= 512) with one launch per stage.  Thread-safe: calls on the same
+ * device are serialised (they share that device's work pool); a context must
+ * not be used by two calls at once.  On THOR_ERR_HIP (a device error flag,
+ * e.g. a WPP wait that gave up) no context advances: the frame can be coded
+ * again.  orig[i]: DEVICE pointer to the
  * context's input frame thor_enc_next_input(es[i]), planar I420, luma stride
  * orig_stride[i] (NULL: width), chroma stride half of it.  Synchronous. */
 int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
@@ -321,6 +325,12 @@ int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
  * window emptied, the sequence header due again): a server re-using a
  * context for the next clip of the same parameters. */
 int thor_enc_reset(thor_enc_t *e);
+/* Diagnostics only: superblock row `row` of every stream never reports its
+ * progress (-1: off), and a WPP wait gives up after `spin_ms` milliseconds
+ * (<= 0: the 5-minute default).  Each wave gives up at most once and then
+ * waits no more, so the launch drains in bounded time and the call returns
+ * THOR_ERR_HIP. */
+int thor_enc_debug_stall(int row, int spin_ms);
 
 /* ---- temporal interpolation: luma down-sampling pyramid ----------------- */
 

@@ -1,7 +1,9 @@
 """CPU: the device encoder's RD source (thor_amd/csrc/enc_*.h) built for the
 host as one lane (tools/enc_host, a debugging harness -- never the product
 path) reproduces the reference Thorenc's .bit on the first frames of two
-golden clips.  The GPU build of the same source is checked in
+golden clips, including
+hierarchical-B coding order and the temporal-interpolated reference (cif_hdbi;
+the harness builds it with the oracle's interpolate_frames).  The GPU build of the same source is checked in
 tests/test_gpu_encoder_rd.py; this test keeps the shared source honest on a
 box without a GPU."""
 import os
@@ -23,7 +25,8 @@ def enc_host():
     return os.path.join(HOST, "enc_host")
 
 
-@pytest.mark.parametrize("name,nframes", [("cif_low", 3), ("w8_low", 2), ("cif_med", 2)])
+@pytest.mark.parametrize("name,nframes", [("cif_low", 3), ("w8_low", 2), ("cif_med", 2), ("cif_hdb", 17),
+                                           ("cif_hdbi", 17)])
 def test_host_build_of_the_rd_source_matches_reference(enc_host, streams, tmp_path, name, nframes):
     meta = streams[name]
     w, h = meta["width"], meta["height"]

@@ -105,6 +105,35 @@ def test_device_encoder_more_configs(name, nframes, streams):
         enc.close()
 
 
+@pytest.mark.parametrize("name", ["cif_hdb", "cif_hdbi", "cif_hdbi_high", "k4_hdbi"])
+def test_device_encoder_hierarchical_b(name, streams):
+    """Hierarchical B (HDB16, 16-frame sub-GOP, coding order != display order):
+    cif_hdb without interpolated references; cif_hdbi / k4_hdbi (speed 2) and
+    cif_hdbi_high (speed 0: the joint mv0 = -mv1 bi-pred search,
+    enc/encode_block.c:2410-2426) with the temporal-interpolated reference
+    built on the GPU per B frame (enc/mainenc.c:324-330) -- every frame of the
+    reference Thorenc's .bit, byte for byte."""
+    _encode_and_compare(name, streams[name]["frames"], streams)
+
+
+def _encode_and_compare(name, nframes, streams):
+    from thor_amd.encoder import GpuEncoder, params_for
+
+    meta = streams[name]
+    p = params_for(meta["config"], meta["width"], meta["height"], nframes, meta["extra"])
+    enc = GpuEncoder(p)
+    try:
+        enc.upload_sequence(_input(meta, nframes))
+        want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
+        assert enc.num_frames() == len(want)
+        for i in range(enc.num_frames()):
+            got = enc.encode_next()
+            print("%s frame %d: %d bytes" % (name, i, len(got)), flush=True)  # progress (long speed-0 clips)
+            assert got == want[i], (name, i, len(got), len(want[i]))
+    finally:
+        enc.close()
+
+
 def test_encoder_reset_recodes_the_sequence(streams):
     """thor_enc_reset: the context codes its sequence again, same .bit."""
     from thor_amd.encoder import GpuEncoder, params_for
@@ -119,4 +148,33 @@ def test_encoder_reset_recodes_the_sequence(streams):
         again = [enc.encode_next() for _ in range(4)]
         assert first == want[:3] and again == want[:4]
     finally:
+        enc.close()
+
+
+def test_wpp_wait_gives_up_once_per_wave(streams):
+    """A superblock row that never reports progress (thor_enc_debug_stall) ends
+    the launch in bounded time with an error -- each wave gives up waiting at
+    most once (a per-SB give-up would cost the 30 SBs of a 1080p row 30 wait
+    periods) -- and the context has not advanced: the same frame then codes
+    normally, byte-equal to the reference."""
+    import time
+
+    from thor_amd.encoder import GpuEncoder, params_for
+
+    meta = streams["hd_low"]
+    enc = GpuEncoder(params_for(meta["config"], meta["width"], meta["height"], 2, meta["extra"]))
+    lib = enc.lib
+    try:
+        enc.upload_sequence(_input(meta, 2))
+        want = _frames(open("tests/golden/hd_low.bit", "rb").read())
+        lib.thor_enc_debug_stall(3, 500)
+        t0 = time.time()
+        with pytest.raises(RuntimeError):
+            enc.encode_next()
+        dt = time.time() - t0
+        lib.thor_enc_debug_stall(-1, 0)
+        assert dt < 6.0, dt  # one 0.5 s wait per stalled wave, not one per superblock
+        assert enc.encode_next() == want[0]
+    finally:
+        lib.thor_enc_debug_stall(-1, 0)
         enc.close()

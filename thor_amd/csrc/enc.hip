@@ -20,6 +20,9 @@
 #include "enc_gop.h"
 #include "enc_rd.h"
 
+#include <map>
+#include <mutex>
+
 #define THOR_ENC_MAX_BATCH 512
 #define TE_MAX_WORKERS 4096  // k_enc_rows workgroups per launch (4 x 1 024 SIMDs)
 #define THOR_ENC_SB_WORDS 4096  // 131072 bits of one SB's stream (trial writes included)
@@ -60,7 +63,8 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 #define TE_WPE
 #endif
 __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
-                                                 TeScratchMem *scratch, unsigned *err) {
+                                                 TeScratchMem *scratch, unsigned *err, unsigned long long spin_limit,
+                                                 int stall_row) {
   __shared__ TeTx s_tx;
   __shared__ TeNbr s_nb;
   __shared__ uint8_t s_pb[TE_BLK];
@@ -74,6 +78,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   te_load_zig();
   TeSB &sb = s_sb;
   const int lane = threadIdx.x;
+  bool dead = false;  // a wait of this wave gave up (reported): it waits no more, so the grid drains
   for (;;) {
     unsigned t = 0;
     if (lane == 0) t = atomicAdd(ticket, 1u);
@@ -91,20 +96,22 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     unsigned seen = 0;  // progress of the row above observed (and acquired) so far
     for (int l = 0; l < J.nsbh; l++) {
       const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
-      if (k > 0 && need > seen) {  // SB (k-1, l+1) (or the whole row above) must be done
+      if (k > 0 && need > seen && !dead) {  // SB (k-1, l+1) (or the whole row above) must be done
         TE_P(TP_WAIT);
-        unsigned v = 0;
+        unsigned v = 0, gave_up = 0;
         if (lane == 0) {
           const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
           while ((v = te_ld_relaxed(&J.progress[k - 1])) < need) {
             __builtin_amdgcn_s_sleep(8);
-            // a wedged dependency (5 minutes): give up, reported; never hang the GPU
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 30000000000ULL) {
+            // a wedged dependency (spin_limit, 5 minutes by default): give up, reported; never hang the GPU
+            if (__builtin_amdgcn_s_memrealtime() - t0 > spin_limit) {
               atomicOr(err, 1u);
+              gave_up = 1;
               break;
             }
           }
         }
+        if (__builtin_amdgcn_readfirstlane(gave_up)) dead = true;
         seen = __builtin_amdgcn_readfirstlane(v);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -119,7 +126,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __builtin_amdgcn_wave_barrier();
-      if (lane == 0) __hip_atomic_store(&J.progress[k], (unsigned)(l + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0 && k != stall_row)  // stall_row: a diagnostics hook (thor_enc_debug_stall), -1 normally
+        __hip_atomic_store(&J.progress[k], (unsigned)(l + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -235,7 +243,9 @@ struct thor_enc {
   int W, H, nsbh, nsbv, nsb, nsb_full;
   int sy, sc;
   long long offy, offu, offv, slot_bytes;
-  int nslots;
+  int nslots;  // the window's 33 + the frame being coded (+ the interpolation slot `islot`)
+  int islot;   // interp_ref: the frame's interpolated reference (interp_frames[0]), -1 without
+  thor_ti_t *ti;
   uint8_t *slots;
   std::vector<int> slot_of_window;  // window index -> slot (-1: empty)
   std::vector<int> slot_busy;
@@ -268,6 +278,8 @@ static int enc_alloc(thor_enc *e) {
   e->offv = yb + cb + (long long)THOR_PAD_C * e->sc + THOR_PAD_C;
   e->slot_bytes = yb + 2 * cb + 256;
   e->nslots = 34;  // the 33-frame window + the frame being coded
+  e->islot = -1;
+  if (e->p.interp_ref) e->islot = e->nslots++;
   EHIP(hipMalloc(&e->slots, e->slot_bytes * e->nslots));
   EHIP(hipMemset(e->slots, 0, e->slot_bytes * e->nslots));
   const size_t ncell = (size_t)(W / 4) * (H / 4);
@@ -289,9 +301,12 @@ static int enc_alloc(thor_enc *e) {
   return THOR_OK;
 }
 
-// Work pools shared by the streams of one launch (per device)
+// Work pools shared by the streams of one launch: one per device, held (its
+// mutex) for the whole of a thor_enc_frames call, so concurrent callers on one
+// device take turns and callers on different devices never share buffers.
+// A pool lives as long as the process (a few MB of scratch per device).
 struct EncPool {
-  int device = -1;
+  std::mutex mu;
   size_t nwork = 0;
   TeScratchMem *scratch = nullptr;
   unsigned *ticket = nullptr, *err = nullptr;
@@ -299,29 +314,44 @@ struct EncPool {
   long long *scan = nullptr;
   size_t scan_n = 0;
 };
-static EncPool g_pool;
+static std::mutex g_pools_mu;
+static std::map<int, EncPool *> g_pools;
 
-static int pool_reserve(int device, size_t nwork, size_t scan_n) {
-  if (g_pool.device != device) {
-    g_pool = EncPool();
-    g_pool.device = device;
-    EHIP(hipMalloc(&g_pool.ticket, 64));
-    EHIP(hipMalloc(&g_pool.err, 64));
-    EHIP(hipMemset(g_pool.err, 0, 64));
-    EHIP(hipMalloc(&g_pool.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
+static EncPool &pool_for(int device) {
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  EncPool *&p = g_pools[device];
+  if (!p) p = new EncPool();
+  return *p;
+}
+
+// (the caller holds P.mu and has made P's device current)
+static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n) {
+  if (!P.ticket) {
+    EHIP(hipMalloc(&P.ticket, 64));
+    EHIP(hipMalloc(&P.err, 64));
+    EHIP(hipMemset(P.err, 0, 64));
+    EHIP(hipMalloc(&P.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
   }
-  if (nwork > g_pool.nwork) {
-    if (g_pool.scratch) (void)hipFree(g_pool.scratch);
-    EHIP(hipMalloc(&g_pool.scratch, nwork * sizeof(TeScratchMem)));
-    g_pool.nwork = nwork;
+  if (nwork > P.nwork) {
+    if (P.scratch) (void)hipFree(P.scratch);
+    P.scratch = nullptr;
+    P.nwork = 0;
+    EHIP(hipMalloc(&P.scratch, nwork * sizeof(TeScratchMem)));
+    P.nwork = nwork;
   }
-  if (scan_n > g_pool.scan_n) {
-    if (g_pool.scan) (void)hipFree(g_pool.scan);
-    EHIP(hipMalloc(&g_pool.scan, scan_n * sizeof(long long)));
-    g_pool.scan_n = scan_n;
+  if (scan_n > P.scan_n) {
+    if (P.scan) (void)hipFree(P.scan);
+    P.scan = nullptr;
+    P.scan_n = 0;
+    EHIP(hipMalloc(&P.scan, scan_n * sizeof(long long)));
+    P.scan_n = scan_n;
   }
   return THOR_OK;
 }
+
+// diagnostics (thor_enc_debug_stall): the WPP wait bound and a row that never publishes
+static unsigned long long g_spin_limit = 30000000000ULL;  // s_memrealtime ticks (100 MHz): 5 minutes
+static int g_stall_row = -1;
 
 extern "C" {
 
@@ -348,7 +378,8 @@ thor_enc_t *thor_enc_create(const thor_enc_params_t *p, int device) {
   e->last_slot = -1;
   e->last_frame_num = -1;
   e->slot_of_window.assign(33, -1);
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || enc_alloc(e) != THOR_OK) {
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || enc_alloc(e) != THOR_OK ||
+      (p->interp_ref && !(e->ti = thor_ti_create(e->W, e->H, device)))) {
     thor_enc_destroy(e);
     return nullptr;
   }
@@ -365,6 +396,7 @@ void thor_enc_destroy(thor_enc_t *e) {
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->ti) thor_ti_destroy(e->ti);
   delete e->gop;
   delete e;
 }
@@ -383,6 +415,7 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   std::vector<int> held(e->nslots, 0);
   for (int w = 0; w < 33; w++)
     if (e->slot_of_window[w] >= 0) held[e->slot_of_window[w]] = 1;
+  if (e->islot >= 0) held[e->islot] = 1;
   cur_slot = -1;
   for (int s = 0; s < e->nslots && cur_slot < 0; s++)
     if (!held[s]) cur_slot = s;
@@ -403,8 +436,15 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   F.rsc = e->sc;
   for (int r = 0; r < pl.num_ref; r++) {
     const int w = pl.ref_array[r];
-    if (w < 0 || w >= 33 || e->slot_of_window[w] < 0) return THOR_ERR_REF;
-    const uint8_t *rs = e->slots + (long long)e->slot_of_window[w] * e->slot_bytes;
+    int slot;
+    if (w < 0) {  // the interpolated reference (encode_block.c: `r >= 0 ? ref[r] : interp_frames[0]`)
+      if (!pl.interp_ref || e->islot < 0) return THOR_ERR_REF;
+      slot = e->islot;
+    } else {
+      if (w >= 33 || e->slot_of_window[w] < 0) return THOR_ERR_REF;
+      slot = e->slot_of_window[w];
+    }
+    const uint8_t *rs = e->slots + (long long)slot * e->slot_bytes;
     F.refy[r] = rs + e->offy;
     F.refu[r] = rs + e->offu;
     F.refv[r] = rs + e->offv;
@@ -460,6 +500,37 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   return THOR_OK;
 }
 
+static thor_yuv_planes_t enc_slot_planes(const thor_enc *e, int slot) {
+  uint8_t *b = e->slots + (long long)slot * e->slot_bytes;
+  return thor_yuv_planes_t{b + e->offy, b + e->offu, b + e->offv, e->sy, e->sc};
+}
+
+// The frame's interpolated reference into the interpolation slot, on the
+// context's stream: interpolate_frames + pad_yuv_frame (enc/mainenc.c:328-330,
+// :385-387), the decoder's kernels (tme.hip, k_pad).
+static int enc_interp(thor_enc *e, const TeFramePlan &pl) {
+  const int a = pl.interp_a, b = pl.interp_b;
+  if (!e->ti || e->islot < 0 || a < 0 || a >= 33 || b < 0 || b >= 33 || e->slot_of_window[a] < 0 ||
+      e->slot_of_window[b] < 0)
+    return THOR_ERR_REF;
+  const thor_yuv_planes_t ra = enc_slot_planes(e, e->slot_of_window[a]), rb = enc_slot_planes(e, e->slot_of_window[b]);
+  const thor_yuv_planes_t o = enc_slot_planes(e, e->islot);
+  const int rc = thor_interpolate_frames(e->ti, &ra, &rb, THOR_PAD_Y, &o, pl.interp_ratio, pl.interp_pos, e->stream);
+  if (rc != THOR_OK) return rc;
+  FrameBatch fb;
+  memset(&fb, 0, sizeof(fb));
+  fb.f[0].cy = o.y;
+  fb.f[0].cu = o.u;
+  fb.f[0].cv = o.v;
+  fb.f[0].sy = e->sy;
+  fb.f[0].sc = e->sc;
+  fb.f[0].W = e->W;
+  fb.f[0].H = e->H;
+  k_pad<<<dim3((pad_chunks(e->W, e->H) + 255) / 256, 1), 256, 0, e->stream>>>(fb);
+  EHIP(hipGetLastError());
+  return THOR_OK;
+}
+
 // Encode the next frame (coding order) of each of `n` contexts with one
 // launch per stage.  orig[i]: DEVICE pointer to context i's input frame
 // thor_enc_next_input(es[i]) as planar I420 (luma stride orig_stride[i],
@@ -479,8 +550,9 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   const int W = lead->W, H = lead->H;
   const int nrows = lead->nsbv;
   const int nwork = n * nrows;
-  int rc = pool_reserve(lead->device, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS),
-                        (size_t)n * (lead->nsb + 1));
+  EncPool &P = pool_for(lead->device);
+  std::lock_guard<std::mutex> pool_lock(P.mu);
+  int rc = pool_reserve(P, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS), (size_t)n * (lead->nsb + 1));
   if (rc != THOR_OK) return rc;
   hipStream_t st = lead->stream;
   std::vector<TeJob> jobs(n);
@@ -495,16 +567,30 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
     if ((rc = enc_prepare(e, orig[i], s, jobs[i], plans[i], cur[i])) != THOR_OK) return rc;
     EHIP(hipStreamSynchronize(e->stream));  // per-context header / memsets (tiny) before the shared stream
   }
-  EHIP(hipMemcpyAsync(g_pool.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
-  EHIP(hipMemsetAsync(g_pool.ticket, 0, 4, st));
+  // interpolated references: each context's on its own stream (they overlap), all done before the RD loop
+  bool any_interp = false;
+  for (int i = 0; i < n; i++)
+    if (plans[i].interp_ref) {
+      if ((rc = enc_interp(es[i], plans[i])) != THOR_OK) return rc;
+      any_interp = true;
+    }
+  if (any_interp)
+    for (int i = 0; i < n; i++)
+      if (plans[i].interp_ref) {
+        EHIP(hipStreamSynchronize(es[i]->stream));
+        if ((rc = thor_ti_status(es[i]->ti)) != THOR_OK) return rc;
+      }
+  EHIP(hipMemcpyAsync(P.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
+  EHIP(hipMemsetAsync(P.ticket, 0, 4, st));
   // persistent workers take row tickets until none are left: more workgroups
   // than the chip holds at once (one per SIMD at this kernel's register and LDS
   // use) would only start as the first ones run out of work
-  k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(g_pool.jobs, n, g_pool.ticket, nrows,
-                                                                         g_pool.scratch, g_pool.err);
+  k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(P.jobs, n, P.ticket, nrows,
+                                                                         P.scratch, P.err, g_spin_limit,
+                                                                         g_stall_row);
   EHIP(hipGetLastError());
   const int ncell = (W / 4) * (H / 4);
-  k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(g_pool.jobs);
+  k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(P.jobs);
   EHIP(hipGetLastError());
   // loop filters: the decoder's kernels over each stream's frame
   for (int o = 0; o < n; o += THOR_MAX_BATCH) {
@@ -539,24 +625,24 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
       EHIP(hipGetLastError());
     }
     if (lead->p.clpf && lead->nsb_full > 0) {
-      k_enc_clpf<<<dim3(lead->nsb_full, m), 64, 0, st>>>(g_pool.jobs + o);
+      k_enc_clpf<<<dim3(lead->nsb_full, m), 64, 0, st>>>(P.jobs + o);
       k_clpf<<<dim3(lead->nsb_full, m), 256, 0, st>>>(fb);
       EHIP(hipGetLastError());
     }
     k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, m), 256, 0, st>>>(fb);
     EHIP(hipGetLastError());
   }
-  k_enc_pack<<<n, 256, 0, st>>>(g_pool.jobs, g_pool.scan, lead->out_cap_words);
+  k_enc_pack<<<n, 256, 0, st>>>(P.jobs, P.scan, lead->out_cap_words);
   EHIP(hipGetLastError());
   // read back every stream's frame
   std::vector<int> nbits(n);
   for (int i = 0; i < n; i++) EHIP(hipMemcpyAsync(&nbits[i], es[i]->out_bits, sizeof(int), hipMemcpyDeviceToHost, st));
   EHIP(hipStreamSynchronize(st));
   unsigned err = 0;
-  EHIP(hipMemcpy(&err, g_pool.err, sizeof(unsigned), hipMemcpyDeviceToHost));
+  EHIP(hipMemcpy(&err, P.err, sizeof(unsigned), hipMemcpyDeviceToHost));
   if (err) {
     fprintf(stderr, "thor_amd enc: device error flags 0x%x\n", err);
-    EHIP(hipMemset(g_pool.err, 0, 4));
+    EHIP(hipMemset(P.err, 0, 4));
     return THOR_ERR_HIP;
   }
   for (int i = 0; i < n; i++) {
@@ -593,6 +679,15 @@ int thor_enc_reset(thor_enc_t *e) {
   e->last_frame_num = -1;
   e->slot_of_window.assign(33, -1);
   e->chunk.clear();
+  return THOR_OK;
+}
+
+// Diagnostics: superblock row `row` of every stream never reports progress
+// (-1: off) and a WPP wait gives up after `spin_ms` (<= 0: the 5-minute
+// default), so the bounded-time failure path can be exercised.
+int thor_enc_debug_stall(int row, int spin_ms) {
+  g_stall_row = row;
+  g_spin_limit = spin_ms > 0 ? (unsigned long long)spin_ms * 100000ULL : 30000000000ULL;
   return THOR_OK;
 }
 

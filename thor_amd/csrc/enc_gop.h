@@ -53,6 +53,9 @@ struct TeFramePlan {
   int frame_type, qp, b_level, num_ref, interp_ref, num_intra_modes;
   int ref_array[TE_GOP_MAX_REF];  // indices into the sliding window (ref[0] = most recently coded)
   int ref_fnum[TE_GOP_MAX_REF];   // frame numbers of those references when this frame is coded
+  // interp_ref: ref index 0 is interpolate_frames(window[interp_a], window[interp_b],
+  // interp_ratio, interp_pos), numbered frame_num (enc/mainenc.c:324-330, :381-387)
+  int interp_a, interp_b, interp_ratio, interp_pos;
   double lambda;
 };
 
@@ -110,6 +113,8 @@ struct TeGop {
     f.qp = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
     f.num_ref = f.frame_type == 0 ? 0 : (num_encoded < P.max_num_ref ? num_encoded : P.max_num_ref);
     f.interp_ref = 0;
+    f.interp_a = f.interp_b = -1;
+    f.interp_ratio = f.interp_pos = 0;
     int *ra = f.ref_array;
     for (int r = 0; r < TE_GOP_MAX_REF; r++) ra[r] = 0;
     if (f.num_ref > 0) {
@@ -128,6 +133,10 @@ struct TeGop {
               ra[1] = mini(num_encoded - 1, coded_phase - te_display_to_code(sub_gop, display_phase - ref_offset + 1) - 1);
               ra[2] = mini(num_encoded - 1, coded_phase - te_display_to_code(sub_gop, display_phase + ref_offset + 1) - 1);
               ra[0] = -1;
+              f.interp_a = ra[1];
+              f.interp_b = ra[2];
+              f.interp_ratio = 2;
+              f.interp_pos = 1;
               for (int r = 3; r < f.num_ref; r++) ra[r] = r - 3;
             } else {
               ra[0] = mini(num_encoded - 1, coded_phase - te_display_to_code(sub_gop, display_phase - ref_offset + 1) - 1);
@@ -148,6 +157,10 @@ struct TeGop {
               ra[1] = 0;
               if (f.num_ref > 1) ra[2] = phase == 0 ? mini(sub_gop, num_encoded - 1) : mini(phase, num_encoded - 1);
               ra[0] = -1;
+              f.interp_a = ra[1];
+              f.interp_b = ra[2];
+              f.interp_ratio = sub_gop - phase;
+              f.interp_pos = phase != 0 ? 1 : sub_gop - phase - 1;
               if (f.num_ref > 2) ra[3] = mini(phase ? phase + sub_gop : 2 * sub_gop, num_encoded - 1);
               for (int r = 4; r < f.num_ref; r++) ra[r] = r - 4 + 1;
             } else {
@@ -194,7 +207,7 @@ struct TeGop {
           f.num_ref--;
         }
     for (int r = 0; r < TE_GOP_MAX_REF; r++)
-      f.ref_fnum[r] = (r < f.num_ref && ra[r] >= 0 && ra[r] < 33) ? window_fnum[ra[r]] : -1;
+      f.ref_fnum[r] = r >= f.num_ref ? -1 : (ra[r] < 0 ? f.frame_num : (ra[r] < 33 ? window_fnum[ra[r]] : -1));
     f.num_intra_modes = (P.intra_rdo == 0 || (f.frame_type != 0 && P.encoder_speed > 0)) ? 4 : 10;
     // lambda (enc/encode_frame.c:77-94): float coefficients promoted to double
     float lc;
@@ -365,9 +378,7 @@ static inline int te_check_params(const thor_enc_params_t *p) {
   if (p->width <= 0 || p->height <= 0 || (p->width & 7) || (p->height & 7)) return THOR_ERR_ARG;
   if (p->qp < 0 || p->qp > 51 || p->max_num_ref < 1 || p->max_num_ref > 4 || p->HQperiod < 1) return THOR_ERR_ARG;
   if (p->rdoq) return THOR_ERR_ARG;          // full RDOQ is not implemented
-  if (p->interp_ref) return THOR_ERR_ARG;    // temporal-interpolated references: not yet
   if (p->sync) return THOR_ERR_ARG;
-  if (p->num_reorder_pics > 0 && p->encoder_speed == 0 && p->enable_bipred) return THOR_ERR_ARG;  // me_mode 1
   if (p->num_reorder_pics + 1 > 16) return THOR_ERR_ARG;
   return THOR_OK;
 }

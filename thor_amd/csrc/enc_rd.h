@@ -897,6 +897,94 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
   return (uint32_t)(min_sad / 2);
 }
 
+// One candidate of motion_estimate_bi (enc/encode_block.c:1141-1160): the
+// vector clipped for ref0's leg (sign 0), that clipped vector clipped again for
+// ref1's negated leg; the truncating average of the two bi-table predictions
+// against the original; *c returns the doubly clipped vector, which is what
+// the MV cost and the result use.
+TE_FN uint32_t te_bi_joint_sad(const TeFrame &F, TeScratch S, const uint8_t *org, const uint8_t *p0, const uint8_t *p1,
+                               int size, int ypos, int xpos, TeMv *c, TeMv mvp) {
+  const TeMv c0 = te_clip_mv(*c, ypos, xpos, F.W, F.H, size, 0);
+  te_mc_luma(S.pb0, size, p0, F.rsy, size, size, c0, 0, 2);
+  const TeMv c1 = te_clip_mv(c0, ypos, xpos, F.W, F.H, size, 1);
+  te_mc_luma(S.pb1, size, p1, F.rsy, size, size, c1, 1, 2);
+  te_avg_rect(S.rf, size, S.pb0, size, S.pb1, size, size, size);
+  te_sync();
+  *c = c1;
+  return te_sad(org, F.osy, S.rf, size, size, size) + te_lambda_bits(F.sqrt_lambda, te_mv_bits(c1.y - mvp.y, c1.x - mvp.x));
+}
+
+// search_bipred_prediction_params with me_mode 1 (enc/encode_block.c:2079-2111,
+// B frames at speed 0): one vector for both legs, mv on ref_idx 0 (1 with an
+// interpolated reference) and -mv on the next index, found by
+// motion_estimate_bi (:1102-1216): a telescope from a 32-pel grid down to
+// quarter pel around the rounded centre, then the candidate list.  That list
+// is read as stored -- integer-rounded vectors used as quarter-pel ones -- and
+// is first rewritten in place (slots num..3 zeroed, slot 4 = mvp, slot 5 = 0,
+// :1171-1179), which later searches of the superblock see too.
+TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeScratch S_, TeSB &sb_, const TeBlockInfo &bi_,
+                                     const TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_out) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_local(S_);
+  TeSB &sb = *te_lds(&sb_);
+  const TeBlockInfo &bi = *te_lds(&bi_);
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
+  const int r0 = F.interp_ref ? 1 : 0, r1 = F.interp_ref ? 2 : 1;
+  const uint8_t *org = F.oy + ypos * F.osy + xpos;
+  const uint8_t *p0 = F.refy[r0] + ypos * F.rsy + xpos, *p1 = F.refy[r1] + ypos * F.rsy + xpos;
+  uint32_t min_sad = TE_MAX_UINT32;
+  TeMv mv_opt, mv_ref;
+  mv_opt.x = mv_opt.y = 0;
+  mv_ref.y = (int16_t)((((int)mv_center[r0].y + 2) >> 2) << 2);
+  mv_ref.x = (int16_t)((((int)mv_center[r0].x + 2) >> 2) << 2);
+  for (int step = 32; step > 0; step >>= 1) {
+    for (int k = -step; k <= step; k += step)
+      for (int l = -step; l <= step; l += step) {
+        if (step < 32 && !k && !l) continue;
+        if (step == 1) {
+          const int vf = mv_ref.y & 3, hf = mv_ref.x & 3;
+          const int ak = k < 0 ? -k : k, al = l < 0 ? -l : l;
+          if (!vf && !hf) {
+            if (ak != al) continue;  // integer pel: diagonal neighbours only
+          } else if (vf == 2 && hf == 2) {
+            continue;
+          } else if (ak == al) {
+            continue;
+          }
+        }
+        TeMv c;
+        c.y = (int16_t)(mv_ref.y + k);
+        c.x = (int16_t)(mv_ref.x + l);
+        const uint32_t sad = te_bi_joint_sad(F, S, org, p0, p1, size, ypos, xpos, &c, mvp);
+        if (sad < min_sad) {
+          min_sad = sad;
+          mv_opt = c;
+        }
+      }
+    mv_ref = mv_opt;
+  }
+  {  // the candidate list rewritten in place (every lane stores the same values)
+    TeMv z;
+    z.x = z.y = 0;
+    for (int idx = sb.mc.num[r0]; idx < 4; idx++) sb.mc.mv[r0][idx] = z;
+    sb.mc.mv[r0][4] = mvp;
+    sb.mc.mv[r0][5] = z;
+    te_sync();
+  }
+  for (int idx = 0; idx < 6; idx++) {  // ME_CANDIDATES, common/global.h:70
+    TeMv c = sb.mc.mv[r0][idx];
+    const uint32_t sad = te_bi_joint_sad(F, S, org, p0, p1, size, ypos, xpos, &c, mvp);
+    if (sad < min_sad) {
+      min_sad = sad;
+      mv_opt = c;
+    }
+  }
+  TE_TR(F.frame_num, 14, ypos, xpos, size, r0 | r1 << 4, min_sad, (mv_opt.x & 0xffff) | (int)mv_opt.y << 16);
+  *ref_idx0 = r0;
+  *ref_idx1 = r1;
+  for (int i = 0; i < 4; i++) mv_out[i] = mv_opt;
+}
+
 // mode_decision_rdo, enc/encode_block.c:2204-2479
 TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
   const TeFrame &F = *te_lds(&F_);
@@ -1039,7 +1127,23 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
           te_copy_best(bi, tmp);
           te_keep_best_bits(b, bi, nbits);
         }
-        // B frames at speed 0 add a joint mv0 = -mv1 search (me_mode 1): rejected by the host
+        if (frame_type == TE_B && F.speed == 0) {  // joint mv0 = -mv1 search (me_mode 1, :2410-2426)
+          TeMv aj[4];
+          te_search_bipred_joint(F, S, sb, bi, mv_center, mvp, &r0, &r1, aj);
+          tmp.pb_part = 0;
+          tmp.ref_idx0 = r0;
+          tmp.ref_idx1 = r1;
+          for (int i = 0; i < 4; i++) tmp.mv0[i] = tmp.mv1[i] = aj[i];
+          tmp.mode = TE_BIPRED;
+          tmp.tb_param = 0;
+          const int nbj = te_encode_block(F, S, b, bi, tmp);
+          cost = te_cost(F, bi, bi.rec, size, size, nbj);
+          if (cost < min_cost) {
+            min_cost = cost;
+            te_copy_best(bi, tmp);
+            te_keep_best_bits(b, bi, nbj);
+          }
+        }
       }
     }
     if (do_intra) {

@@ -213,15 +213,20 @@ __device__ __forceinline__ uint32_t ti_win4(const TiWin &W, int pic, int u, int 
 }
 
 // Spin (uniformly) until the published word of a step of the row above carries
-// this launch's generation.
-__device__ __forceinline__ unsigned long long ti_spin(const unsigned long long *p, unsigned gen, unsigned *err) {
+// this launch's generation.  A wedged wavefront (60 s) is reported once and the
+// wave stops waiting for the rest of its row (`dead`), so the launch drains in
+// bounded time whatever the number of steps.
+__device__ __forceinline__ unsigned long long ti_spin(const unsigned long long *p, unsigned gen, unsigned *err,
+                                                      bool &dead) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long w;
   while (__builtin_amdgcn_readfirstlane(
              (uint32_t)((w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32)) != gen) {
+    if (dead) break;
     __builtin_amdgcn_s_sleep(1);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 6000000000ULL) {  // 60 s: report, never hang the GPU
       if (threadIdx.x == 0) atomicOr(err, 1u);
+      dead = true;
       break;
     }
   }
@@ -283,6 +288,7 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
   uint32_t up_l = 0, up = 0;  // row above: steps c-1 and c (rolled forward)
   uint32_t up_r = 0;
   unsigned long long next = 0;  // prefetched published word of the row above
+  bool dead = false;            // a wait of this wave gave up: wait no more
   if (row > 0) next = ti_ld64(above + (ncols > 1 ? 1 : 0));
   for (int c = 0; c < ncols; c++) {
     const int xp = 2 * c, x0 = xp * 8;
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
     if (row > 0) {
       // above-right (or, at the last column, nothing new: its vectors are already held)
       if (c == 0) {
-        up = __builtin_amdgcn_readfirstlane((uint32_t)ti_spin(above, L.gen, L.err));
+        up = __builtin_amdgcn_readfirstlane((uint32_t)ti_spin(above, L.gen, L.err, dead));
         up_l = 0;
       } else {
         up_l = up;
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(64) void k_ti_search(const TiLevel L) {
       }
       if (c + 1 < ncols) {
         unsigned long long w = next;
-        if (__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) != L.gen) w = ti_spin(above + c + 1, L.gen, L.err);
+        if (__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) != L.gen) w = ti_spin(above + c + 1, L.gen, L.err, dead);
         up_r = __builtin_amdgcn_readfirstlane((uint32_t)w);
         if (c + 2 < ncols) next = ti_ld64(above + c + 2);  // the next step's, early
       }

@@ -61,7 +61,7 @@ BATCHED_SYMBOLS = [
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_frames", "thor_enc_frame", "thor_enc_frame_bytes",
-    "thor_enc_read_recon", "thor_enc_reset",
+    "thor_enc_read_recon", "thor_enc_reset", "thor_enc_debug_stall",
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
@@ -151,6 +151,8 @@ def load(path: str = LIB_PATH):
     L.thor_enc_next_input.restype = i
     L.thor_enc_reset.argtypes = [P]
     L.thor_enc_reset.restype = i
+    L.thor_enc_debug_stall.argtypes = [i, i]
+    L.thor_enc_debug_stall.restype = i
     L.thor_enc_stream.argtypes = [P]
     L.thor_enc_stream.restype = P
     L.thor_enc_frames.argtypes = [P, i, P, P]

@@ -71,7 +71,7 @@ int main(int argc, char **argv) {
   TeGop gop(P);
   std::vector<HostFrame *> window(33, nullptr);
   for (auto &w : window) w = new HostFrame(W, H);
-  HostFrame cur(W, H);
+  HostFrame cur(W, H), interp(W, H);
   std::vector<TeCell> cells((size_t)(W / 4) * (H / 4));
   std::vector<or_cell_t> ocells(cells.size());
   TeScratchMem *SM = (TeScratchMem *)calloc(1, sizeof(TeScratchMem));
@@ -100,8 +100,14 @@ int main(int argc, char **argv) {
     F.rv = cur.f.v;
     F.rsy = cur.f.stride_y;
     F.rsc = cur.f.stride_c;
+    if (pl.interp_ref) {  // the interpolated reference (enc/mainenc.c:324-330, :381-387)
+      or_interpolate_frames(&window[pl.interp_a]->f, &window[pl.interp_b]->f, 96, &interp.f, W, H, pl.interp_ratio,
+                            pl.interp_pos, nullptr, nullptr);
+      or_pad_frame(&interp.f, W, H, 96, 48);
+      interp.f.frame_num = pl.frame_num;
+    }
     for (int r = 0; r < pl.num_ref; r++) {
-      const HostFrame *rf = window[pl.ref_array[r]];
+      const HostFrame *rf = pl.ref_array[r] < 0 ? &interp : window[pl.ref_array[r]];
       F.refy[r] = rf->f.y;
       F.refu[r] = rf->f.u;
       F.refv[r] = rf->f.v;

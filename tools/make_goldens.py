@@ -54,6 +54,8 @@ STREAMS = [
     ("cif_hdbi", 352, 288, 17, "config_HDB16_low_complexity.txt", [], 10),
     ("cif_hdbi_high", 352, 288, 17, "config_HDB16_high_efficiency.txt", [], 11),
     ("k4_hdbi", 3840, 2160, 17, "config_HDB16_low_complexity.txt", [], 12),
+    # round 3: BASELINE config 5 at its stated size and operating point (speed 0 B frames: joint bi-pred search)
+    ("k4_hdbi_high", 3840, 2160, 17, "config_HDB16_high_efficiency.txt", [], 13),
 ]
 
 
