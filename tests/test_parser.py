@@ -10,7 +10,7 @@ from conftest import GOLD, trace_path
 from thor_amd.trace import load_trace
 
 STREAMS = ["cif_low", "cif_med", "cif_high", "cif_hdb", "hd_low", "k4_low", "k4_med", "w8_low", "hd_high", "cif_hdbi",
-           "cif_hdbi_high", "k4_hdbi"]
+           "cif_hdbi_high", "k4_hdbi", "k4_hdbi_high"]
 # fields the reference sets for every mode (pb_part / intra_mode only for
 # INTER / INTRA: read_block leaves them stale otherwise, dec/read_bits.c:380, :582)
 COMMON = ["ypos", "xpos", "size", "bwidth", "bheight", "mode", "tb_split", "dir", "qp", "cbp_y", "cbp_u", "cbp_v",
