@@ -3,23 +3,28 @@
 
 Metric (BASELINE.json): Mpixels/s encode+decode, 4K (3840x2160)
 config_LDB_low_complexity, bit-exact vs the reference.  Workload
-(config.workload): the seeded synthetic 8-frame 4K clip of tests/golden/k4_low
-(thor_amd/synth.py; no real clips or network), input frames resident in HBM.
+(config.workload): 8 distinct seeded synthetic 8-frame 4K clips
+(thor_amd/synth.py; no real clips or network; tests/golden/bench_clips.json
+holds the reference encoder's and decoder's md5 for each).
 
-One step, per GPU, for K independent streams (a server coding K clips):
+One step, per GPU, for K independent streams (a server coding K clips;
+stream k codes clip k mod 8):
+  input   every stream's raw frames from pinned host memory to its HBM buffer
+          (H2D on a copy stream, frame-major; the encoder's frame i waits for
+          frame i's copies only);
   encode  every stream's 8 frames through the device-resident encoder
           (thor_enc_frames: WPP RD loop, loop filters, CLPF decision and bit
           packing on the GPU, one launch per stage for the K streams) -> the
-          streams' .bit, each checked byte for byte against the reference
-          Thorenc's tests/golden/k4_low.bit;
+          streams' .bit, each checked against the reference Thorenc's for its
+          clip;
   decode  every .bit: host parse (thor_parse_frame, 16 threads) -> upload of
           the parse output -> batched GPU reconstruction (thor_dec_frames),
-          each decoded sequence checked against the reference Thordec md5.
-The two legs are frame-pipelined: the host parse, upload and GPU
-reconstruction of frame i run while the GPU encodes frame i + 1.
-value = K x W x H x frames / wall time of the step (both legs complete, host
-parse and the H2D of its output included).  One extra step runs the legs one
-after the other to report their split (config.serial_*).
+          each decoded sequence checked against the reference Thordec's.
+The legs are frame-pipelined: the host parse, upload and GPU reconstruction
+of frame i run while the GPU encodes frame i + 1.  value = K x W x H x frames
+/ wall time of the step (input upload, both legs, host parse and the H2D of
+its output all included).  One extra step runs the legs one after the other
+to report their split (config.serial_*).
 
 Reported beside it (not part of `value`): the single-stream enc+dec latency,
 decode_only (the reconstruction of resident parse output, the round-1
@@ -27,7 +32,9 @@ figure), the k_recon roofline (the north-star 4K inter-reconstruction kernel,
 hipEvents on its stream) and a few kernel legs.
 
 N > 1: one process per GPU, each with its own K streams (no data-path
-collective): scaling "weak".  Prints one JSON line (rank 0).
+collective): scaling "weak"; `bench.py --gpus N` run directly starts the N
+ranks itself (launch_ranks), under torch.distributed.run it is one of them.
+The time is the max over ranks.  Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -321,31 +328,41 @@ def interp_frames_leg(torch, lib, clip: np.ndarray, reps: int = 10):
             "note": "hipEvents on torch's current stream; latency-bound (the search is a wavefront of step rows)"}
 
 
-def cpu_baseline(meta, clip: np.ndarray, procs: int = HOST_THREADS, budget_s: float = 8.0):
+def cpu_baseline(bc, clips_meta, clips, procs: int = HOST_THREADS, budget_s: float = 8.0):
     """The reference encoder + decoder (oracle/_ref/Thorenc, Thordec: SIMD
-    build, -O3) on the same clip and configuration: `procs` concurrent
-    encode->decode pipelines on the host cores (one stream each), plus one
-    pipeline alone (1 core).  Returns None when the reference binaries are not
-    present (they are built from /root/reference by oracle/Makefile)."""
+    build, -O3) on the bench's clips and configuration: `procs` concurrent
+    encode->decode pipelines on the host cores (one stream each, round-robin
+    over the clips, each reading its YUV from a file as the reference does),
+    plus one pipeline alone (1 core).  Every bitstream and decoded md5 is
+    checked against tests/golden/bench_clips.json.  Returns None when the
+    reference binaries are not present (they are built from /root/reference by
+    oracle/Makefile)."""
     from thor_amd.configs import flags
 
     enc = os.path.join(ROOT, "oracle", "_ref", "Thorenc")
     dec = os.path.join(ROOT, "oracle", "_ref", "Thordec")
     if not (os.path.exists(enc) and os.path.exists(dec)):
         return None
-    W, H, n = meta["width"], meta["height"], meta["frames"]
+    W, H, n = bc["width"], bc["height"], bc["frames"]
     px = W * H * n
     tmp = "/tmp/thor_bench_%d" % os.getpid()
     os.makedirs(tmp, exist_ok=True)
-    yuv = os.path.join(tmp, "in.yuv")
-    clip.tofile(yuv)
-    fl = flags(meta["config"], W, H, n, meta["extra"])
+    for c, clip in enumerate(clips):
+        clip.tofile(os.path.join(tmp, "in%d.yuv" % c))
+    fl = flags(bc["config"], W, H, n, bc["extra"])
 
     def pipeline(k):
+        c = k % len(clips)
         bit, out = os.path.join(tmp, "%d.bit" % k), os.path.join(tmp, "%d.yuv" % k)
         cmd = "%s -if %s -of %s %s >/dev/null 2>&1 && %s %s %s >/dev/null 2>&1" % (
-            shlex.quote(enc), yuv, bit, " ".join(shlex.quote(f) for f in fl), shlex.quote(dec), bit, out)
+            shlex.quote(enc), os.path.join(tmp, "in%d.yuv" % c), bit, " ".join(shlex.quote(f) for f in fl),
+            shlex.quote(dec), bit, out)
         return subprocess.Popen(["/bin/sh", "-c", cmd])
+
+    def check(k):
+        c = clips_meta[k % len(clips)]
+        return (hashlib.md5(open(os.path.join(tmp, "%d.bit" % k), "rb").read()).hexdigest() == c["bit_md5"] and
+                hashlib.md5(open(os.path.join(tmp, "%d.yuv" % k), "rb").read()).hexdigest() == c["dec_md5"])
 
     try:
         # one pipeline alone, repeated within the budget
@@ -355,8 +372,7 @@ def cpu_baseline(meta, clip: np.ndarray, procs: int = HOST_THREADS, budget_s: fl
             assert pipeline(0).wait() == 0
             t1 += time.perf_counter() - t0
             runs += 1
-        ok = hashlib.md5(open(os.path.join(tmp, "0.bit"), "rb").read()).hexdigest() == meta["bit_md5"]
-        ok &= hashlib.md5(open(os.path.join(tmp, "0.yuv"), "rb").read()).hexdigest() == meta["dec_md5"]
+        ok = check(0)
         one = px * runs / t1 / 1e6
         # `procs` pipelines at once on the host cores
         t0 = time.perf_counter()
@@ -365,25 +381,30 @@ def cpu_baseline(meta, clip: np.ndarray, procs: int = HOST_THREADS, budget_s: fl
         tp = time.perf_counter() - t0
         assert all(r == 0 for r in rcs), rcs
         for k in range(procs):
-            ok &= hashlib.md5(open(os.path.join(tmp, "%d.yuv" % k), "rb").read()).hexdigest() == meta["dec_md5"]
+            ok &= check(k)
     finally:
         for f in os.listdir(tmp):
             os.remove(os.path.join(tmp, f))
         os.rmdir(tmp)
     return {"value": round(px * procs / tp / 1e6, 3), "unit": "Mpixels/s", "cores": procs, "kind": "reference",
-            "sample": "reference Thorenc -> Thordec (SIMD build, -O3) on the same 4K 8-frame LDB-low clip: "
-                      "%d concurrent single-threaded pipelines (one per host core of the GPU's share), %.1f s wall; "
-                      "bitstream + decoded md5 %s" % (procs, tp, "ok" if ok else "MISMATCH"),
+            "sample": "reference Thorenc -> Thordec (SIMD build, -O3) on the bench's 4K 8-frame LDB-low clips: "
+                      "%d concurrent single-threaded pipelines (one per host core of the GPU's share, round-robin "
+                      "over %d clips), %.1f s wall; bitstream + decoded md5 %s" % (
+                          procs, len(clips), tp, "ok" if ok else "MISMATCH"),
             "single_core_mpx_s": round(one, 3), "single_core_s_per_pass": round(t1 / runs, 3)}
 
 
-def roofline_pass(lib, decs, groups, devs, frames, seq, isteps):
+ST_COUNT = 7  # capi.hip stage marks: prep, inter, intra, deblock, clpf, pad, interpolated reference
+
+
+def roofline_pass(lib, decs, groups, devs, frames_of, seq, isteps):
     """Instrumented decode of group 0 alone (resident parse output): hipEvents
     around every stage of every batched launch on its stream -> the stage
-    breakdown and the k_recon roofline (one launch = the group's B frames)."""
+    breakdown and the k_recon roofline (one launch = the group's B frames, one
+    per member; frames_of[j]: member j's parsed frames)."""
     lead = decs[groups[0][0]]
     B = len(groups[0])
-    nf = len(frames)
+    nf = len(frames_of[0])
     from thor_amd.decoder import decode_batch
 
     lib.thor_dec_set_timing(lead.h, 1)
@@ -396,17 +417,64 @@ def roofline_pass(lib, decs, groups, devs, frames, seq, isteps):
     nm = lib.thor_dec_stage_marks(lead.h, mk_stage, mk_ms, cap)
     lib.thor_dec_set_timing(lead.h, 0)
     per_frame, cur = [], None
-    for k in range(nm):  # every frame opens with its side-info stage (0)
-        if mk_stage[k] == 0:
-            cur = [0.0] * 6
+    for k in range(nm):  # a frame opens with its interpolated reference (6) or else its side-info stage (0)
+        st = mk_stage[k]
+        if cur is None or st == 6 or (st == 0 and not (cur[6] > 0 and sum(cur[:6]) == 0)):
+            cur = [0.0] * ST_COUNT
             per_frame.append(cur)
-        cur[mk_stage[k]] += mk_ms[k]
+        cur[st] += mk_ms[k]
     assert len(per_frame) == isteps * nf, (len(per_frame), isteps, nf)
-    stage_ms = [sum(f[i] for f in per_frame) / isteps / B for i in range(6)]  # per stream pass
+    stage_ms = [sum(f[i] for f in per_frame) / isteps / B for i in range(ST_COUNT)]  # per stream pass
+    frames = frames_of[0]
     pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]  # the I frame has no inter pixels
     recon_ms = sum(per_frame[s * nf + i][1] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
-    alg = B * sum(recon_alg_bytes(frames[i], seq.width, seq.height) for i in pidx) / len(pidx)  # per launch
+    # per launch: the members' P frames of one frame index, averaged over the P frame indices
+    alg = sum(recon_alg_bytes(fs[i], seq.width, seq.height) for fs in frames_of for i in pidx) / len(pidx)
     return stage_ms, recon_ms, alg, B
+
+
+def launch_ranks(n: int) -> int:
+    """bench.py --gpus N run directly (no torch.distributed.run): start N ranks
+    of this script, one per GPU, before anything here touches a GPU, with the
+    launcher's environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*); the
+    children inherit stdout, so rank 0's JSON line is the output.  Returns the
+    worst exit status."""
+    port = str(29500 + os.getpid() % 1000)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
+
+
+def reduce_max(dist, device, x: float) -> float:
+    """max over ranks (the slowest rank's time); identity without a group."""
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def launcher_selftest(a) -> None:
+    """--launcher-selftest (CPU, gloo): the N-rank plumbing of a --gpus N run
+    without a GPU -- rank spawn, process group, barrier, max-over-ranks time,
+    min-over-ranks bit-exactness -- and rank 0's one JSON line."""
+    import torch.distributed as dist
+
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.barrier()
+    elapsed = reduce_max(dist, "cpu", 1.0 + rank)
+    ok = -reduce_max(dist, "cpu", -1.0)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "selftest": True, "max_elapsed": elapsed,
+                          "bit_exact": ok == 1.0}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
@@ -419,6 +487,7 @@ def main():
     ap.add_argument("--dec-slots", type=int, default=10,
                     help="reference ring slots per decoder context (LDB: up to 4 references + the current frame)")
     ap.add_argument("--streams", type=int, default=240, help="independent streams (encoder + decoder) per GPU")
+    ap.add_argument("--clips", type=int, default=8, help="distinct seeded clips the streams are drawn from (<= 8)")
     ap.add_argument("--band-local", action="store_true",
                     help="--shard rows: each rank deblocks / CLPFs only its band, then a second all-gather of final rows")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
@@ -427,21 +496,31 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per k_recon launch (default tools/traffic_latest.json, "
                          "copied from profiles/<tag>_traffic.json by tools/prof_summary.py)")
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
 
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:  # not under torch.distributed.run: be the launcher
+        sys.exit(launch_ranks(a.gpus))
+    if a.launcher_selftest:
+        return launcher_selftest(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gold = os.path.join(ROOT, "tests", "golden")
-    meta = json.load(open(os.path.join(gold, "streams.json")))["k4_low"]
-    W, H, nf = meta["width"], meta["height"], meta["frames"]
+    bc = json.load(open(os.path.join(gold, "bench_clips.json")))
+    W, H, nf = bc["width"], bc["height"], bc["frames"]
+    clips_meta = bc["clips"][:max(1, min(a.clips, len(bc["clips"])))]
+    nclip = len(clips_meta)
 
-    clip = None
-    if a.shard == "streams":  # synthesise the input before anything touches the GPU (worker processes fork)
+    clips = None
+    if a.shard == "streams":  # synthesise the inputs before anything touches the GPU (worker processes fork)
         from thor_amd import synth
 
-        clip = synth.synth_frames(W, H, nf, meta["seed"], workers=8)
-        assert hashlib.md5(clip.tobytes()).hexdigest() == meta["synth_md5"], "synthetic clip drifted"
+        clips = []
+        for cm in clips_meta:
+            c = synth.synth_frames(W, H, nf, cm["seed"], workers=8)
+            assert hashlib.md5(c.tobytes()).hexdigest() == cm["synth_md5"], "synthetic clip %d drifted" % cm["seed"]
+            clips.append(c)
 
     import torch
 
@@ -460,14 +539,22 @@ def main():
     from thor_amd.encoder import GpuEncoder, encode_batch, params_for
 
     lib = L.load()
-    want_bit = open(os.path.join(gold, "k4_low.bit"), "rb").read()
+    dev = torch.device("cuda", local)
     K = max(1, min(a.streams, 512))  # THOR_ENC_MAX_BATCH
+    clip_of = [k % nclip for k in range(K)]
+    fsize = W * H * 3 // 2
+    # the raw input: each clip in pinned host memory; each stream's frames in its own HBM buffer, filled by
+    # H2D copies inside the timed region (a copy stream, frame-major, overlapped with encoding)
+    host = [torch.from_numpy(c.reshape(nf, fsize)).pin_memory() for c in clips]
+    inbuf = [torch.empty((nf, fsize), dtype=torch.uint8, device=dev) for _ in range(K)]
+    copy_stream = torch.cuda.Stream(device=dev)
     encs = []
-    for _ in range(K):
-        e = GpuEncoder(params_for(meta["config"], W, H, nf, meta["extra"]), device=local)
-        e.upload_sequence(clip)
+    for k in range(K):
+        e = GpuEncoder(params_for(bc["config"], W, H, nf, bc["extra"]), device=local)
+        e.use_device_sequence(inbuf[k].data_ptr(), nf)
         encs.append(e)
-    seq, _ = parse_stream(want_bit)
+    want_bit = [None] * nclip  # the reference Thorenc's .bit per clip: md5 in bench_clips.json
+    seq, _ = parse_stream(open(os.path.join(gold, "k4_low.bit"), "rb").read())  # sequence header (all clips share it)
     decs = [GpuDecoder(seq, device=local, slots=a.dec_slots) for _ in range(K)]
     groups = [list(range(g, min(g + 8, K))) for g in range(0, K, 8)]  # THOR_MAX_BATCH contexts per launch
     for gk in groups:  # a group's members enqueue on their leader's stream
@@ -476,26 +563,45 @@ def main():
     pools = [[{} for _ in range(nf)] for _ in range(K)]  # per stream and frame: re-used device buffers
     pool = ThreadPoolExecutor(HOST_THREADS)
 
+    def upload_inputs(ks):
+        """Enqueue every input frame of streams ks (frame-major) on the copy
+        stream; returns one event per frame index (that frame of every stream
+        resident)."""
+        evs = []
+        with torch.cuda.stream(copy_stream):
+            for i in range(nf):
+                for k in ks:
+                    inbuf[k][i].copy_(host[clip_of[k]][i], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_stream)
+                evs.append(ev)
+        return evs
+
+    def enc_wait(ks, ev):  # the batch runs on its first member's stream: it waits for the frame's copies
+        torch.cuda.ExternalStream(encs[ks[0]].stream(), device=dev).wait_event(ev)
+
     def encode(ks):
         for k in ks:
             encs[k].reset()
+        evs = upload_inputs(ks)
         bits = [[] for _ in ks]
         fms = []
-        for _ in range(nf):
+        for i in range(nf):
             t0 = time.perf_counter()
+            enc_wait(ks, evs[i])
             for j, ch in enumerate(encode_batch([encs[k] for k in ks])):
                 bits[j].append(ch)
             fms.append((time.perf_counter() - t0) * 1e3)
         return [b"".join(b) for b in bits], fms
 
     def decode(ks, bits):
-        def host(j):  # parse + upload of one stream (GIL released inside the C calls)
+        def host_leg(j):  # parse + upload of one stream (GIL released inside the C calls)
             k = ks[j]
             _, frames = parse_stream(bits[j])
             return [decs[k].upload(fr, pools[k][i]) for i, fr in enumerate(frames)]
 
         t0 = time.perf_counter()
-        devs = list(pool.map(host, range(len(ks))))
+        devs = list(pool.map(host_leg, range(len(ks))))
         dec_host_s[0] += time.perf_counter() - t0
         gs = [[j for j, k in enumerate(ks) if k in gk] for gk in groups]
         for i in range(nf):
@@ -510,13 +616,16 @@ def main():
     pipe_tl = {}  # the last pipelined step's timeline (ms from its start)
 
     def step_pipe(ks):
-        """Frame-pipelined encode + decode: while the GPU codes frame i + 1 of
-        every stream, a consumer thread parses frame i's chunks (one parser
-        per stream, 16 host threads), uploads the parse output and enqueues
-        its GPU reconstruction on the decoder streams.  Returns the wall time
-        of both legs complete, the .bit files and the device frames."""
+        """One timed step: H2D of every stream's raw frames on a copy stream,
+        frame-pipelined encode + decode (while the GPU codes frame i + 1 of
+        every stream, a consumer thread parses frame i's chunks -- one parser
+        per stream, 16 host threads --, uploads the parse output and enqueues
+        its GPU reconstruction on the decoder streams).  Returns the wall time
+        of everything complete, the .bit files and the device frames."""
+        t0 = time.perf_counter()
         for k in ks:
             encs[k].reset()
+        evs = upload_inputs(ks)
         pipe_tl.update(enc_done_ms=[0.0] * nf, dec_enq_ms=[0.0] * nf)
         parsers = [Parser() for _ in ks]
         bits = [[] for _ in ks]
@@ -529,11 +638,13 @@ def main():
             try:
                 for i in range(nf):
                     chunks = q.get()
+                    if chunks is None:
+                        return
 
-                    def host(j):
+                    def host_leg(j):
                         return decs[ks[j]].upload(parsers[j].parse(chunks[j]), pools[ks[j]][i])
 
-                    ds = list(pool.map(host, range(len(ks))))
+                    ds = list(pool.map(host_leg, range(len(ks))))
                     for g in gs:
                         if g:
                             decode_batch([decs[ks[j]] for j in g], [ds[j] for j in g])
@@ -543,17 +654,21 @@ def main():
             except BaseException as e:  # re-raised by the caller
                 err.append(e)
 
-        t0 = time.perf_counter()
         th = threading.Thread(target=consumer)
         th.start()
+        sent = 0
         try:
             for i in range(nf):
+                enc_wait(ks, evs[i])
                 chunks = encode_batch([encs[k] for k in ks])
                 for j, ch in enumerate(chunks):
                     bits[j].append(ch)
                 q.put([ch[4:] for ch in chunks])  # payload after the 4-byte chunk length (dec/getbits.c:48-69)
+                sent += 1
                 pipe_tl["enc_done_ms"][i] = round((time.perf_counter() - t0) * 1e3, 1)
         finally:
+            if sent < nf:
+                q.put(None)
             th.join()
         pipe_tl["consumer_done_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         for k in ks:
@@ -573,20 +688,38 @@ def main():
         t2 = time.perf_counter()
         return t1 - t0, t2 - t1, bits, devs, fms
 
+    def bits_ok(ks, bits):
+        """every stream's .bit == the reference Thorenc's for its clip (md5)"""
+        ok = True
+        for j, k in enumerate(ks):
+            c = clip_of[k]
+            if want_bit[c] is None:
+                if hashlib.md5(bits[j]).hexdigest() != clips_meta[c]["bit_md5"]:
+                    return False
+                want_bit[c] = bits[j]
+            ok &= bits[j] == want_bit[c]
+        return ok
+
+    def decoded_ok(ks):
+        """every stream's decoded sequence == the reference Thordec's for its
+        clip: the first stream of each clip by md5, the others byte for byte
+        against it"""
+        ref = {}
+        ok = True
+        for k in ks:
+            got = b"".join(decs[k].read_i420(fr) for fr in range(nf))
+            c = clip_of[k]
+            if c not in ref:
+                ok &= hashlib.md5(got).hexdigest() == clips_meta[c]["dec_md5"]
+                ref[c] = got
+            else:
+                ok &= got == ref[c]
+        return ok
+
     allk = list(range(K))
     for _ in range(max(1, a.warmup)):
         _, bits, devs = step_pipe(allk)
-    # bit-exactness: every stream's .bit vs the reference Thorenc, every decode vs the reference Thordec
-    def decoded_ok():
-        """Every stream's decoded sequence vs the reference Thordec: stream 0
-        by md5, the others (same clip) byte for byte against stream 0's."""
-        ref = b"".join(decs[0].read_i420(fr) for fr in range(nf))
-        ok = hashlib.md5(ref).hexdigest() == meta["dec_md5"]
-        for k in allk[1:]:
-            ok &= b"".join(decs[k].read_i420(fr) for fr in range(nf)) == ref
-        return ok
-
-    bit_exact = all(b == want_bit for b in bits) and decoded_ok()
+    bit_exact = bits_ok(allk, bits) and decoded_ok(allk)
 
     if dist is not None:
         dist.barrier()
@@ -595,31 +728,28 @@ def main():
     for _ in range(a.steps):
         te, bits, devs = step_pipe(allk)
         elapsed += te
-        bit_exact &= all(b == want_bit for b in bits)
-        bit_exact &= decoded_ok()  # every timed step's decode checked too (outside the timed region)
+        bit_exact &= bits_ok(allk, bits)
+        bit_exact &= decoded_ok(allk)  # every timed step's decode checked too (outside the timed region)
     torch.cuda.synchronize(local)
+    if dist is not None:
+        dist.barrier()
     # the two legs one after the other (one untimed-for-value step): the split of the work
     dec_host_s[0] = 0.0
     t_enc, t_dec, bits, devs, fms = step(allk)
-    bit_exact &= all(b == want_bit for b in bits)
+    bit_exact &= bits_ok(allk, bits)
     enc_frame_ms = fms
     dec_host_ms = dec_host_s[0] * 1e3
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        ok = torch.tensor([1 if bit_exact else 0], device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        bit_exact = bool(ok.item())
+    elapsed = reduce_max(dist, dev, elapsed)
+    bit_exact = -reduce_max(dist, dev, -1.0 if bit_exact else 0.0) == 1.0
     px_stream = W * H * nf
     value = world * K * px_stream * a.steps / elapsed / 1e6
+    in_bytes = K * nf * fsize
 
     # ---- beside `value` ----
-    # single-stream latency: stream 0 alone, encode + decode
+    # single-stream latency: stream 0 alone, encode (its input upload included) + decode
     lat = [step([0])[:2] for _ in range(2)]
     lat_enc, lat_dec = min(x[0] for x in lat), min(x[1] for x in lat)
     # decode_only: reconstruction of every stream's resident parse output (no parse, no upload)
-    frames = parse_stream(want_bit)[1]
     dsteps = 5
     for k in allk:
         decs[k].sync()
@@ -631,7 +761,8 @@ def main():
     for k in allk:
         decs[k].sync()
     t_do = (time.perf_counter() - t0) / dsteps
-    stage_ms, recon_ms, alg, B = roofline_pass(lib, decs, groups, devs, frames, seq, 3)
+    frames_of = [parse_stream(bits[k])[1] for k in groups[0]]
+    stage_ms, recon_ms, alg, B = roofline_pass(lib, decs, [groups[0]], devs, frames_of, seq, 3)
     achieved = alg / (recon_ms / 1e3) / 1e9 if recon_ms > 0 else 0.0
     traffic = None
     tj = a.traffic_json or os.path.join(ROOT, "tools", "traffic_latest.json")
@@ -651,22 +782,30 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8/i16",
-            "data": "synthetic (seeded 4K clip, thor_amd/synth.py), input frames resident in HBM",
+            "data": "synthetic: %d distinct seeded 4K clips (thor_amd/synth.py, seeds %s), streams round-robin over "
+                    "them; every step uploads each stream's raw frames from pinned host memory inside the timed "
+                    "region (H2D on a copy stream, overlapped with encoding); decoded frames stay in HBM"
+                    % (nclip, [c["seed"] for c in clips_meta]),
             "bit_exact": bit_exact,
+            "bit_exact_scope": "every stream of every timed step: .bit md5 == the reference Thorenc's for its clip, "
+                               "decoded sequence == the reference Thordec's (tests/golden/bench_clips.json)",
             "config": {
-                "workload": "encode + decode of the 4K (3840x2160) 8-frame config_LDB_low_complexity stream: "
-                            "device-resident encoder (RD loop, loop filters, CLPF, bit packing) -> .bit == reference "
-                            "Thorenc's; host parse -> upload -> GPU reconstruction == reference Thordec's output",
-                "frames": nf, "width": W, "height": H,
+                "workload": "encode + decode of 4K (3840x2160) 8-frame config_LDB_low_complexity streams: "
+                            "raw frames host -> HBM, device-resident encoder (RD loop, loop filters, CLPF, bit "
+                            "packing) -> .bit == reference Thorenc's; host parse -> upload -> GPU reconstruction "
+                            "== reference Thordec's output",
+                "frames": nf, "width": W, "height": H, "clips": nclip,
                 "parallelism": "streams: %d GPU(s) x %d independent streams" % (world, K),
                 "streams_per_gpu": K,
-                "pipelining": "frame-pipelined: the host parse + upload + GPU reconstruction of frame i "
-                              "run while the GPU encodes frame i + 1 (value = wall time of both legs complete)",
+                "h2d_bytes_per_step": in_bytes,
+                "pipelining": "frame-pipelined: the H2D of frame i + 1's raw input and the host parse + upload + "
+                              "GPU reconstruction of frame i run while the GPU encodes frame i + 1 (value = wall "
+                              "time of everything complete)",
                 "pipe_timeline_last_step": pipe_tl,
                 "serial_t_enc_ms": round(t_enc * 1e3, 2),
                 "serial_t_dec_ms": round(t_dec * 1e3, 2),
                 "serial_mpx_s": round(K * px_stream / (t_enc + t_dec) / 1e6, 2),
-                "serial_note": "one extra step with the legs one after the other: encode all frames, then "
+                "serial_note": "one extra step with the legs one after the other: upload + encode all frames, then "
                                "parse + upload + reconstruct (the split of the work; not `value`)",
                 "t_dec_host_ms": round(dec_host_ms, 2),
                 "t_dec_host_note": "host parse (thor_parse_frame) + upload of the parse output, %d threads, "
@@ -680,7 +819,7 @@ def main():
                 "decode_only_mpx_s": round(K * px_stream / t_do / 1e6, 1),
                 "decode_only_note": "GPU reconstruction of the K streams' resident parse output (no parse, "
                                     "no upload): the round-1 headline",
-                "stage_ms_per_stream_pass": {k: round(v, 4) for k, v in zip(STAGES, stage_ms)},
+                "stage_ms_per_stream_pass": {k: round(v, 4) for k, v in zip(STAGES + ["interp"], stage_ms)},
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             },
             "roofline": {
@@ -694,21 +833,22 @@ def main():
                 "alg_bytes_per_launch": round(alg),
                 "avg_launch_us": round(recon_ms * 1e3, 2),
                 "frames_per_launch": B,
-                "launches": "batched P-frame decode launches of group 0 alone; hipEvents on its stream",
-                "dominant_kernel_note": "by GPU time the step is k_enc_rows (83.5 %, profiles/r02i_rocprof_stats.txt), "
-                                        "the encoder's superblock worker: integer RD search with negligible HBM traffic "
-                                        "and no MFMA work, latency bound inside the wave (SQ counters: 74 % of wave "
-                                        "time in s_waitcnt, DESIGN.md 3b), so neither roofline bounds it; this object "
-                                        "is k_recon, the north star's inter-reconstruction kernel",
+                "launches": "batched P-frame decode launches of group 0 alone (streams of clips 0..7, the inter "
+                            "stage: k_recon + k_recon_multi for the half SBs with several keys); hipEvents on its "
+                            "stream",
+                "dominant_kernel_note": "by GPU time the step is k_enc_rows, the encoder's superblock worker: "
+                                        "integer RD search with negligible HBM traffic and no MFMA work, latency "
+                                        "bound inside the wave (DESIGN.md 3b), so neither roofline bounds it; this "
+                                        "object is k_recon, the north star's inter-reconstruction kernel",
             },
         }
         if world == 1 and not a.no_legs:
             out["encoder_tu_chain"] = encoder_leg(torch, lib)
             out["temporal_pyramid"] = pyramid_leg(torch, lib)
             out["temporal_interp_comp"] = interp_leg(torch, lib)
-            out["temporal_interp_frame"] = interp_frames_leg(torch, lib, clip)
+            out["temporal_interp_frame"] = interp_frames_leg(torch, lib, clips[0])
         if not a.no_cpu_baseline and world == 1:
-            cb = cpu_baseline(meta, clip)
+            cb = cpu_baseline(bc, clips_meta, clips)
             if cb is not None:
                 out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)

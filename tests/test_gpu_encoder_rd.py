@@ -116,7 +116,17 @@ def test_device_encoder_hierarchical_b(name, streams):
     _encode_and_compare(name, streams[name]["frames"], streams)
 
 
-def _encode_and_compare(name, nframes, streams):
+def test_device_encoder_4k_hdb16_high_efficiency(streams):
+    """BASELINE config 5 at its stated size and operating point: 4K
+    config_HDB16_high_efficiency (speed 0, interpolated references, 4
+    references, tb / pb split, delta-qp).  The first three coded frames of the
+    17-frame plan -- the I frame, the P frame 16 and the B frame 8 (joint
+    bi-pred search against the interpolated reference) -- byte-equal to the
+    reference Thorenc's tests/golden/k4_hdbi_high.bit."""
+    _encode_and_compare("k4_hdbi_high", streams["k4_hdbi_high"]["frames"], streams, limit=3)
+
+
+def _encode_and_compare(name, nframes, streams, limit=None):
     from thor_amd.encoder import GpuEncoder, params_for
 
     meta = streams[name]
@@ -126,7 +136,7 @@ def _encode_and_compare(name, nframes, streams):
         enc.upload_sequence(_input(meta, nframes))
         want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
         assert enc.num_frames() == len(want)
-        for i in range(enc.num_frames()):
+        for i in range(enc.num_frames() if limit is None else limit):
             got = enc.encode_next()
             print("%s frame %d: %d bytes" % (name, i, len(got)), flush=True)  # progress (long speed-0 clips)
             assert got == want[i], (name, i, len(got), len(want[i]))

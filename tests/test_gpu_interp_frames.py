@@ -73,7 +73,7 @@ def _md5(b):
     return hashlib.md5(b).hexdigest()
 
 
-@pytest.mark.parametrize("name", ["cif_hdbi", "cif_hdbi_high", "k4_hdbi"])
+@pytest.mark.parametrize("name", ["cif_hdbi", "cif_hdbi_high", "k4_hdbi", "k4_hdbi_high"])
 def test_gpu_decode_interp_ref_stream(name, streams):
     """.bit -> host parser -> GPU decode with the interpolated references built
     on the GPU (dec/decode_frame.c:91-109); CIF checked at every stage."""

@@ -26,11 +26,13 @@ namespace {
 struct TpBits {
   std::vector<uint8_t> buf;
   size_t nbits = 0, pos = 0;
+  bool err = false;  // a malformed code word (corrupt input): the frame is rejected
   void set(const uint8_t *p, size_t nbytes) {
     buf.assign(nbytes + 16, 0);
     if (nbytes) memcpy(buf.data(), p, nbytes);
     nbits = nbytes * 8;
     pos = 0;
+    err = false;
   }
   uint32_t show(int n) const {  // n <= 32
     if (n <= 0) return 0;
@@ -82,6 +84,10 @@ int get_vlc(TpBits &b, int n) {
       if (!b.show(1)) {
         lead++;
         b.flush(1);
+        if (lead > 30) {  // no valid code word is this long (corrupt or truncated input)
+          b.err = true;
+          return 0;
+        }
       } else {
         const int tmp = (int)b.get(lead + 1);
         return 6 * (1 << n) + tmp - (1 << n);
@@ -94,7 +100,10 @@ int get_vlc(TpBits &b, int n) {
     if (!b.show(1)) {
       lead++;
       b.flush(1);
-      if (lead > 40) return 0;  // corrupt stream: stop consuming
+      if (lead > 30) {  // corrupt stream: stop consuming
+        b.err = true;
+        return 0;
+      }
     } else {
       return (int)b.get(lead + 1) - 1;
     }
@@ -165,6 +174,10 @@ int read_coeff(TpBits &b, int16_t *tile, int size, int type) {
     } else {
       if (b.show(2) == 2) code = (int)b.get(2) - 2;
       else code = get_vlc(b, 2) - 1;
+    }
+    if (code < 0) {  // only a malformed (all-zero) code word decodes below 0
+      b.err = true;
+      break;
     }
     const int index = find_index(code, maxrun, chroma);
     if (index == -1) break;
@@ -540,6 +553,7 @@ void process_block(thor_parser *P, int size, int ypos, int xpos) {
     const int a = get_vlc(P->b, 0);
     const int s = a > 0 ? (int)P->b.get(1) : 0;
     P->qpb = P->qp + (s ? -a : a);
+    if (P->qpb < 0 || P->qpb > 51) P->error = 1;  // corrupt input: the tables are indexed by qp
   }
   if (split) {
     if (size <= 8) {
@@ -591,7 +605,10 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
     P->seq.clpf = (int)b.get(1);
     P->use_block_contexts = (int)b.get(1);
     P->seq.bipred = (int)b.get(1);
-    if (P->seq.width <= 0 || P->seq.height <= 0 || (P->seq.width & 7) || (P->seq.height & 7)) return THOR_ERR_ARG;
+    // 16-bit sizes; this build also caps them at 16384 (a corrupt header must not size GBs of side info)
+    if (P->seq.width <= 0 || P->seq.height <= 0 || (P->seq.width & 7) || (P->seq.height & 7) ||
+        P->seq.width > 16384 || P->seq.height > 16384)
+      return THOR_ERR_ARG;
     P->have_seq = 1;
     P->cells.assign((size_t)(P->seq.width / 4) * (P->seq.height / 4), TeCell());
   }
@@ -612,6 +629,7 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
     P->num_ref = 0;
   }
   P->frame_num = (int)b.get(16);
+  if (P->qp > 51) return THOR_ERR_ARG;  // corrupt header: qp indexes the dequantisation / loop-filter tables
   for (int r = 0; r < P->num_ref; r++) {
     if (P->ref_array[r] == -1) continue;  // the interpolated reference
     if (P->ref_array[r] < 0 || P->ref_array[r] > 32 || P->window[P->ref_array[r]] < 0) return THOR_ERR_REF;
@@ -663,7 +681,7 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
       for (int l = 0; l < nh; l++)
         if (cand[k * nh + l]) P->clpf[k * nh + l] = all ? 1 : (uint8_t)b.get(1);
   }
-  if (b.pos > b.nbits) return THOR_ERR_ARG;  // read past the payload: truncated or corrupt
+  if (b.pos > b.nbits || b.err) return THOR_ERR_ARG;  // read past the payload / malformed: truncated or corrupt
   // slide the window (decode_frame.c:135-147)
   for (int r = 32; r > 0; r--) P->window[r] = P->window[r - 1];
   P->window[0] = P->frame_num;

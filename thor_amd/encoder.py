@@ -48,15 +48,16 @@ class GpuEncoder:
         self.W, self.H = params.width, params.height
         self.fsize = self.W * self.H * 3 // 2
         self.seq_dev = None
+        self.own_seq = False
         self.nin = 0
 
     def close(self):
         if self.h:
             self.lib.thor_enc_destroy(self.h)
             self.h = None
-        if self.seq_dev:
+        if self.seq_dev and self.own_seq:
             self.lib.thor_dev_free(self.seq_dev)
-            self.seq_dev = None
+        self.seq_dev = None
 
     def __del__(self):  # pragma: no cover
         try:
@@ -71,7 +72,15 @@ class GpuEncoder:
         self.seq_dev = self.lib.thor_dev_alloc(a.nbytes)
         if not self.seq_dev:
             raise MemoryError("thor_dev_alloc")
+        self.own_seq = True
         L.check(self.lib.thor_h2d(self.seq_dev, a.ctypes.data, a.nbytes), "thor_h2d")
+
+    def use_device_sequence(self, ptr: int, nframes: int):
+        """Read the input from `nframes` I420 frames the caller keeps (and
+        fills) at DEVICE address `ptr`, frame k at ptr + k * W*H*3/2."""
+        if self.seq_dev and self.own_seq:
+            self.lib.thor_dev_free(self.seq_dev)
+        self.seq_dev, self.own_seq, self.nin = ptr, False, nframes
 
     def reset(self):
         """Start the sequence again (thor_enc_reset): same input, same .bit."""
@@ -87,6 +96,10 @@ class GpuEncoder:
         if k >= self.nin:
             raise IndexError("input frame %d not uploaded" % k)
         return self.seq_dev + k * self.fsize
+
+    def stream(self) -> int:
+        """The context's HIP stream (thor_enc_stream): a batch runs on its first member's."""
+        return self.lib.thor_enc_stream(self.h) or 0
 
     def encode_next(self) -> bytes:
         ptr = self.next_input_ptr()
