@@ -487,6 +487,9 @@ def main():
     ap.add_argument("--dec-slots", type=int, default=10,
                     help="reference ring slots per decoder context (LDB: up to 4 references + the current frame)")
     ap.add_argument("--streams", type=int, default=240, help="independent streams (encoder + decoder) per GPU")
+    ap.add_argument("--dec-priority", type=int, default=1,
+                    help="1: decoder groups on high-priority HIP streams (their launches dispatch ahead of the "
+                         "encoder's queued workgroups); 0: default priority")
     ap.add_argument("--clips", type=int, default=8, help="distinct seeded clips the streams are drawn from (<= 8)")
     ap.add_argument("--band-local", action="store_true",
                     help="--shard rows: each rank deblocks / CLPFs only its band, then a second all-gather of final rows")
@@ -557,7 +560,12 @@ def main():
     seq, _ = parse_stream(open(os.path.join(gold, "k4_low.bit"), "rb").read())  # sequence header (all clips share it)
     decs = [GpuDecoder(seq, device=local, slots=a.dec_slots) for _ in range(K)]
     groups = [list(range(g, min(g + 8, K))) for g in range(0, K, 8)]  # THOR_MAX_BATCH contexts per launch
+    dec_streams = []
     for gk in groups:  # a group's members enqueue on their leader's stream
+        if a.dec_priority:  # the short decode launches ahead of the encoder's queued row workers
+            ps = torch.cuda.Stream(device=dev, priority=-1)
+            dec_streams.append(ps)
+            decs[gk[0]].set_stream(C.c_void_p(ps.cuda_stream))
         for k in gk[1:]:
             decs[k].set_stream(C.c_void_p(decs[gk[0]].stream()))
     pools = [[{} for _ in range(nf)] for _ in range(K)]  # per stream and frame: re-used device buffers
@@ -821,6 +829,7 @@ def main():
                                     "no upload): the round-1 headline",
                 "stage_ms_per_stream_pass": {k: round(v, 4) for k, v in zip(STAGES + ["interp"], stage_ms)},
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                "decoder_stream_priority": "high" if a.dec_priority else "default",
             },
             "roofline": {
                 "bound": "hbm",

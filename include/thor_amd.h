@@ -107,8 +107,19 @@ typedef struct thor_dec thor_dec_t;
 
 /* Create a device-resident decoder: a ring of padded reference frames (pad 96
  * luma / 48 chroma, stride as create_yuv_frame, common/common_frame.c:324-351)
- * on HIP device `device`.  Returns NULL on failure. */
+ * on HIP device `device`.  Returns NULL on failure; thor_last_create_error
+ * says why.  num_slots <= 1: 34 (the reference's 33-frame window + the frame
+ * being decoded); a reference evicted from a smaller ring is reported as
+ * THOR_ERR_REF by the decode call that names it, never decoded wrongly. */
 thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots);
+
+/* Why the last thor_dec_create / thor_enc_create / thor_ti_create of the
+ * calling thread returned NULL: THOR_ERR_ARG (unsupported parameters, e.g. a
+ * ring over the 2 GiB one buffer descriptor addresses), THOR_ERR_NOMEM (HBM
+ * exhausted; *bytes = the size of the allocation that failed) or THOR_ERR_HIP;
+ * THOR_OK after a successful create.  `msg` (may be NULL) receives a one-line
+ * reason naming the buffer. */
+int thor_last_create_error(size_t *bytes, char *msg, size_t cap);
 void thor_dec_destroy(thor_dec_t *d);
 
 /* Decode (reconstruct) one frame.  `blocks`, `coeffs`, `clpf_flags` and

@@ -2,6 +2,7 @@
 reference encoder's own bitstreams (tests/golden/<name>.bit, written by the
 reference Thorenc from the seeded synthetic clips) must come out byte for
 byte, frame by frame."""
+import time
 import hashlib
 
 import numpy as np
@@ -137,8 +138,10 @@ def _encode_and_compare(name, nframes, streams, limit=None):
         want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
         assert enc.num_frames() == len(want)
         for i in range(enc.num_frames() if limit is None else limit):
+            t0 = time.perf_counter()
             got = enc.encode_next()
-            print("%s frame %d: %d bytes" % (name, i, len(got)), flush=True)  # progress (long speed-0 clips)
+            print("%s frame %d: %d bytes, %.2f s" % (name, i, len(got), time.perf_counter() - t0),
+                  flush=True)  # progress (long speed-0 clips)
             assert got == want[i], (name, i, len(got), len(want[i]))
     finally:
         enc.close()

@@ -57,6 +57,8 @@ struct thor_dec {
   unsigned *progress;  // intra wavefront progress per (SB row, component)
   int16_t *resid;      // residual planes (Y, U, V; int16), written by k_prep_resid, read by k_recon / k_intra
   uint8_t *edge;       // SB-row edge rows (FrameCtx::edge)
+  uint4 *hplan;        // per half SB prediction plans (FrameCtx::hplan)
+  unsigned plan_gen;   // tag of the latest frame's plans
   int ewy, ewc;
   unsigned long long *dbg;  // optional per-row intra timing (debug)
   unsigned long long *dbg_recon;  // optional k_recon phase stamps (debug)
@@ -132,11 +134,25 @@ int thor_d2h(void *dst, const void *src, size_t bytes) {
   return THOR_OK;
 }
 
+int thor_last_create_error(size_t *bytes, char *msg, size_t cap) {
+  if (bytes) *bytes = g_create_err.bytes;
+  if (msg && cap) snprintf(msg, cap, "%s", g_create_err.msg);
+  return g_create_err.code;
+}
+
 thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
-  if (!seq || seq->width <= 0 || seq->height <= 0 || (seq->width & 7) || (seq->height & 7)) return nullptr;  // multiples of 8 (enc/strings.c:437)
+  create_begin();
+  if (!seq || seq->width <= 0 || seq->height <= 0 || (seq->width & 7) || (seq->height & 7)) {  // multiples of 8 (enc/strings.c:437)
+    create_fail(THOR_ERR_ARG, 0, "thor_dec_create: frame size must be positive multiples of 8");
+    return nullptr;
+  }
   if (num_slots <= 1) num_slots = 34;  // 33 references + the frame being decoded
   if (num_slots > THOR_MAX_SLOTS) num_slots = THOR_MAX_SLOTS;
-  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    create_fail(THOR_ERR_ARG, 0, "thor_dec_create: no HIP device %d", device);
+    return nullptr;
+  }
   thor_dec *d = new thor_dec();
   d->seq = *seq;
   d->device = device;
@@ -152,6 +168,9 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->offv = ybytes + cbytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
   d->slot_bytes = ybytes + 2 * cbytes + 256;
   if (d->slot_bytes * (num_slots + (seq->interp_ref ? 1 : 0)) >= (1LL << 31)) {  // k_recon addresses the ring with 32-bit buffer offsets
+    create_fail(THOR_ERR_ARG, (size_t)(d->slot_bytes * (num_slots + (seq->interp_ref ? 1 : 0))),
+                "thor_dec_create: a ring of %d slots of %lld bytes exceeds the 2 GiB a buffer descriptor addresses",
+                num_slots, d->slot_bytes);
     delete d;
     return nullptr;
   }
@@ -166,6 +185,8 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->progress = nullptr;
   d->resid = nullptr;
   d->edge = nullptr;
+  d->hplan = nullptr;
+  d->plan_gen = 0;
   d->dbg = nullptr;
   d->dbg_recon = nullptr;
   d->dbg_flags = 0;
@@ -177,24 +198,28 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->pending = nullptr;
   d->ev_used = 0;
   bool ok = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking) == hipSuccess;
+  if (!ok) create_fail(THOR_ERR_HIP, 0, "thor_dec_create: hipStreamCreate failed");
   d->stream = d->own_stream;
-  ok = ok && hipMalloc(&d->slots, d->slot_bytes * alloc_slots) == hipSuccess;
+  ok = ok && dev_alloc(&d->slots, d->slot_bytes * alloc_slots, "thor_dec_create: reference ring");
   ok = ok && hipMemset(d->slots, 0, d->slot_bytes * alloc_slots) == hipSuccess;
   if (ok && seq->interp_ref) ok = (d->ti = thor_ti_create(W, H, device)) != nullptr;
   size_t ncell = (size_t)(W / 4) * (H / 4);
-  ok = ok && hipMalloc(&d->cellinfo, ncell * sizeof(uint16_t)) == hipSuccess;
-  ok = ok && hipMalloc(&d->cellmc, ncell * sizeof(uint2)) == hipSuccess;
+  ok = ok && dev_alloc(&d->cellinfo, ncell * sizeof(uint16_t), "thor_dec_create: cell side info");
+  ok = ok && dev_alloc(&d->cellmc, ncell * sizeof(uint2), "thor_dec_create: cell MC words");
   ok = ok && hipMemset(d->cellmc, 0, ncell * sizeof(uint2)) == hipSuccess;
-  ok = ok && hipMalloc(&d->cellmv1, ncell * sizeof(int32_t)) == hipSuccess;
+  ok = ok && dev_alloc(&d->cellmv1, ncell * sizeof(int32_t), "thor_dec_create: cell mv1");
   ok = ok && hipMemset(d->cellmv1, 0, ncell * sizeof(int32_t)) == hipSuccess;
   ok = ok && hipMemset(d->cellinfo, 0, ncell * sizeof(uint16_t)) == hipSuccess;
-  ok = ok && hipMalloc(&d->ctl, 64) == hipSuccess;
-  ok = ok && hipMalloc(&d->resid, (size_t)W * H * 3) == hipSuccess;  // 1.5 px/luma px x 2 B
+  ok = ok && dev_alloc(&d->ctl, 64, "thor_dec_create: control words");
+  ok = ok && dev_alloc(&d->resid, (size_t)W * H * 3, "thor_dec_create: residual planes");  // 1.5 px/luma px x 2 B
   // intra progress words (3 per SB row), then the rows' intra-list segments (nrows + 1)
-  ok = ok && hipMalloc(&d->progress, (size_t)4 * ((H + 63) / 64 + 2) * sizeof(unsigned)) == hipSuccess;
+  ok = ok && dev_alloc(&d->progress, (size_t)4 * ((H + 63) / 64 + 2) * sizeof(unsigned), "thor_dec_create: progress");
   d->ewy = (W + 2 * EDGE_MARGIN + 15) & ~15;
   d->ewc = (W / 2 + 2 * EDGE_MARGIN + 15) & ~15;
-  ok = ok && hipMalloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc)) == hipSuccess;
+  ok = ok && dev_alloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc), "thor_dec_create: edge rows");
+  const size_t nhalf = 2 * (size_t)((W + 63) / 64) * ((H + 63) / 64);
+  ok = ok && dev_alloc(&d->hplan, nhalf * sizeof(uint4), "thor_dec_create: half-SB plans");
+  ok = ok && hipMemset(d->hplan, 0, nhalf * sizeof(uint4)) == hipSuccess;  // tag 0: no plan (gen starts at 1)
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
   for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&d->xev[i], hipEventDisableTiming) == hipSuccess;
   {  // k_intra stages a row's CU words in LDS (up to (W/8) x 8 CUs)
@@ -204,6 +229,8 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
                      hipSuccess;
   }
   if (!ok) {
+    create_fail(THOR_ERR_HIP, 0, "thor_dec_create: HIP call failed");  // no-op when an allocation said why
+    (void)hipGetLastError();
     thor_dec_destroy(d);
     return nullptr;
   }
@@ -222,6 +249,7 @@ void thor_dec_destroy(thor_dec_t *d) {
   if (d->progress) (void)hipFree(d->progress);
   if (d->resid) (void)hipFree(d->resid);
   if (d->edge) (void)hipFree(d->edge);
+  if (d->hplan) (void)hipFree(d->hplan);
   if (d->ti) thor_ti_destroy(d->ti);
   for (int i = 0; i < 2; i++)
     if (d->xev[i]) (void)hipEventDestroy(d->xev[i]);
@@ -343,9 +371,14 @@ static int dec_frames_chunk(thor_dec_t *const *ds, int n, const thor_frame_hdr_t
 
 int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins) {
   if (!ds || !hdrs || !ins || n <= 0) return THOR_ERR_ARG;
-  for (int i = 0; i < n; i++)
+  for (int i = 0; i < n; i++) {
+    if (!ds[i]) return THOR_ERR_ARG;
+    // a band-local context decodes through thor_dec_frame_begin / _end / _finish only; rejected here,
+    // before any chunk is enqueued, so a refused call leaves no frame half decoded
+    if (ds[i]->band_local && ds[i]->band1 > 0) return THOR_ERR_ARG;
     for (int j = 0; j < i; j++)
       if (ds[i] == ds[j]) return THOR_ERR_ARG;  // one frame per context per call (a stream's frames are serial)
+  }
   for (int o = 0; o < n; o += THOR_MAX_BATCH) {  // THOR_MAX_BATCH frames per launch
     const int rc = dec_frames_chunk(ds + o, n - o < THOR_MAX_BATCH ? n - o : THOR_MAX_BATCH, hdrs + o, ins + o);
     if (rc != THOR_OK) return rc;
@@ -400,6 +433,9 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
       b.ipos[i] = hdrs[i].interp_pos;
       f.islot = d->islot;
     }
+    f.hplan = d->hplan;
+    if (++d->plan_gen == 0) d->plan_gen = 1;  // tag 0 marks "no plan"
+    f.gen = (int)d->plan_gen;
     f.blk = in.blocks;
     f.coeffs = in.coeffs;
     f.tus = in.tu_list;

@@ -5,9 +5,52 @@
 
 #include "../../include/thor_amd.h"
 
+#include <stdarg.h>
+#include <stdio.h>
+
 #define THOR_MAX_SLOTS 40
 #define THOR_PAD_Y 96
 #define THOR_PAD_C 48
+
+// Why the last create call (thor_dec_create / thor_enc_create / thor_ti_create)
+// of the calling thread returned NULL: thor_last_create_error.
+struct ThorCreateErr {
+  int code;
+  size_t bytes;  // THOR_ERR_NOMEM: the allocation that failed
+  char msg[192];
+};
+static thread_local ThorCreateErr g_create_err = {THOR_OK, 0, {0}};
+static inline void create_fail(int code, size_t bytes, const char *fmt, ...) {
+  if (g_create_err.code != THOR_OK) return;  // keep the first (root) cause of this create call
+  g_create_err.code = code;
+  g_create_err.bytes = bytes;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_create_err.msg, sizeof(g_create_err.msg), fmt, ap);
+  va_end(ap);
+}
+static inline void create_begin() {
+  g_create_err.code = THOR_OK;
+  g_create_err.bytes = 0;
+  g_create_err.msg[0] = 0;
+}
+// hipMalloc that records the failure (out of memory -> THOR_ERR_NOMEM with the
+// bytes asked for) and clears HIP's sticky last error so later launches do not
+// report it.
+template <class T>
+static inline bool dev_alloc(T **p, size_t bytes, const char *what) {
+  void *q = nullptr;
+  const hipError_t e = hipMalloc(&q, bytes);
+  if (e == hipSuccess) {
+    *p = (T *)q;
+    return true;
+  }
+  *p = nullptr;
+  (void)hipGetLastError();
+  create_fail(e == hipErrorOutOfMemory ? THOR_ERR_NOMEM : THOR_ERR_HIP, bytes, "%s: hipMalloc(%zu bytes): %s", what,
+              bytes, hipGetErrorString(e));
+  return false;
+}
 
 // block_mode_t, common/types.h:83-90
 enum { M_SKIP = 0, M_INTRA = 1, M_INTER = 2, M_BIPRED = 3, M_MERGE = 4 };
@@ -53,6 +96,13 @@ struct FrameCtx {
   int band0, band1;  // SB rows k_recon reconstructs (row-band sharding); all by default
   int islot;         // slot of the frame's temporal-interpolated reference (blocks' ref -2), -1 none
   int pb0, pb1;      // band-local phase B: luma rows [pb0, pb1) deblocked / CLPF'd here; pb1 = 0: whole frame
+  // Per half SB (64x32 luma) prediction plan, written by k_frame_prep for the
+  // halves one 64x64 inter CU covers with a single (MV, reference) key per
+  // prediction pass: (mv0, MC meta word, mv1, tag).  A record is this frame's
+  // iff tag == gen (no clearing between frames); k_recon then skips the
+  // per-cell resolution.  Null: no plans (every half takes the per-cell path).
+  uint4 *hplan;
+  int gen;
 };
 // A batch of frames travels in the kernel argument segment (8 x 384 B, under
 // the 4 KB kernarg limit): the host fills it per call, no upload copy.  Every

@@ -230,7 +230,8 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
     hipError_t e_ = (x);                                                                                \
     if (e_ != hipSuccess) {                                                                             \
       fprintf(stderr, "thor_amd enc: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
-      return THOR_ERR_HIP;                                                                              \
+      (void)hipGetLastError();                                                                          \
+      return e_ == hipErrorOutOfMemory ? THOR_ERR_NOMEM : THOR_ERR_HIP;                                 \
     }                                                                                                   \
   } while (0)
 
@@ -280,21 +281,21 @@ static int enc_alloc(thor_enc *e) {
   e->nslots = 34;  // the 33-frame window + the frame being coded
   e->islot = -1;
   if (e->p.interp_ref) e->islot = e->nslots++;
-  EHIP(hipMalloc(&e->slots, e->slot_bytes * e->nslots));
+  if (!dev_alloc(&e->slots, e->slot_bytes * e->nslots, "thor_enc_create: reconstruction ring")) return g_create_err.code;
   EHIP(hipMemset(e->slots, 0, e->slot_bytes * e->nslots));
   const size_t ncell = (size_t)(W / 4) * (H / 4);
-  EHIP(hipMalloc(&e->cells, ncell * sizeof(TeCell)));
-  EHIP(hipMalloc(&e->cellinfo, ncell * sizeof(uint16_t)));
-  EHIP(hipMalloc(&e->sb_words, (size_t)e->nsb * THOR_ENC_SB_WORDS * 4));
-  EHIP(hipMalloc(&e->sb_nbits, (size_t)e->nsb * sizeof(int)));
-  EHIP(hipMalloc(&e->progress, (size_t)e->nsbv * sizeof(unsigned)));
-  EHIP(hipMalloc(&e->clpf_bits, (size_t)e->nsb_full + 1));
-  EHIP(hipMalloc(&e->clpf_flags, (size_t)e->nsb_full + 1));
-  EHIP(hipMalloc(&e->es_thr, 2 * 52 * 4 * sizeof(int)));
-  EHIP(hipMalloc(&e->hdr_words, 64 * 4));
+  if (!dev_alloc(&e->cells, ncell * sizeof(TeCell), "thor_enc_create: cell state")) return g_create_err.code;
+  if (!dev_alloc(&e->cellinfo, ncell * sizeof(uint16_t), "thor_enc_create: cell side info")) return g_create_err.code;
+  if (!dev_alloc(&e->sb_words, (size_t)e->nsb * THOR_ENC_SB_WORDS * 4, "thor_enc_create: SB bit strings")) return g_create_err.code;
+  if (!dev_alloc(&e->sb_nbits, (size_t)e->nsb * sizeof(int), "thor_enc_create: SB bit counts")) return g_create_err.code;
+  if (!dev_alloc(&e->progress, (size_t)e->nsbv * sizeof(unsigned), "thor_enc_create: WPP progress")) return g_create_err.code;
+  if (!dev_alloc(&e->clpf_bits, (size_t)e->nsb_full + 1, "thor_enc_create: CLPF bits")) return g_create_err.code;
+  if (!dev_alloc(&e->clpf_flags, (size_t)e->nsb_full + 1, "thor_enc_create: CLPF flags")) return g_create_err.code;
+  if (!dev_alloc(&e->es_thr, 2 * 52 * 4 * sizeof(int), "thor_enc_create: early-skip thresholds")) return g_create_err.code;
+  if (!dev_alloc(&e->hdr_words, 64 * 4, "thor_enc_create: header words")) return g_create_err.code;
   e->out_cap_words = (int)(((size_t)W * H * 2) / 4 + 1024);  // 16 bits per pixel: far above any real frame
-  EHIP(hipMalloc(&e->out_words, (size_t)e->out_cap_words * 4 + 8));
-  EHIP(hipMalloc(&e->out_bits, sizeof(int)));
+  if (!dev_alloc(&e->out_words, (size_t)e->out_cap_words * 4 + 8, "thor_enc_create: output words")) return g_create_err.code;
+  if (!dev_alloc(&e->out_bits, sizeof(int), "thor_enc_create: output bit count")) return g_create_err.code;
   std::vector<int> es(2 * 52 * 4);
   te_es_thresholds(e->p.early_skip_thr, es.data());
   EHIP(hipMemcpy(e->es_thr, es.data(), es.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -361,8 +362,16 @@ void thor_enc_default_params(thor_enc_params_t *p) {
 int thor_enc_check_params(const thor_enc_params_t *p) { return p ? te_check_params(p) : THOR_ERR_ARG; }
 
 thor_enc_t *thor_enc_create(const thor_enc_params_t *p, int device) {
-  if (!p || te_check_params(p) != THOR_OK) return nullptr;
-  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  create_begin();
+  if (!p || te_check_params(p) != THOR_OK) {
+    create_fail(THOR_ERR_ARG, 0, "thor_enc_create: parameters the device encoder does not support (thor_enc_check_params)");
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    create_fail(THOR_ERR_ARG, 0, "thor_enc_create: no HIP device %d", device);
+    return nullptr;
+  }
   thor_enc *e = new thor_enc();
   e->p = *p;
   e->gop = new TeGop(*p);
@@ -380,6 +389,8 @@ thor_enc_t *thor_enc_create(const thor_enc_params_t *p, int device) {
   e->slot_of_window.assign(33, -1);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || enc_alloc(e) != THOR_OK ||
       (p->interp_ref && !(e->ti = thor_ti_create(e->W, e->H, device)))) {
+    create_fail(THOR_ERR_HIP, 0, "thor_enc_create: HIP call failed");  // no-op when an allocation said why
+    (void)hipGetLastError();
     thor_enc_destroy(e);
     return nullptr;
   }

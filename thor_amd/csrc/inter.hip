@@ -497,6 +497,28 @@ __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bi
   it.pend &= ~((m0 ? 1u : 0u) | (m1 ? 2u : 0u));
 }
 
+// The half's plan says every cell has key K in this pass: filter straight
+// into the prediction registers (no per-segment key match).
+__device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bipred, int x0, uint32_t ty[8],
+                                           uint32_t tc[4], bool acc) {
+  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
+  const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
+  const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
+  const LdsChroma c{w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3)};
+  if (K.fx == 2 && K.fy == 2) {
+    luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ty, acc);
+  } else {
+    int v01, v23, v45;
+    tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45);
+    luma_rows<0, 8>(l, (uint32_t)(lwb & 3), g_taps.luma[bipred][K.fx][0], g_taps.luma[bipred][K.fx][1], v01, v23, v45,
+                    ty, acc);
+  }
+  const int cvt = g_taps.chroma[K.cfy];
+  chroma_rows<0, 4>(c, (uint32_t)(cwb & 3), g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
+                    (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc, acc);
+}
+
 // Waves whose items need several keys: every item straight from the ring,
 // per-lane keys (one pass, no per-key staging round trips).
 __device__ __forceinline__ void filter_direct(const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, int bipred, int x0,
@@ -564,6 +586,70 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   const int sby = sb / sbw, sbx = sb - sby * sbw;
   if (sby < f.band0 || sby >= f.band1) return;  // another shard's rows (row-band sharding)
   const int cs = f.W >> 2;
+  const int x0 = sbx * 64, y0 = sby * 64 + 32 * h, cc = lane & 15, gr = lane >> 4;
+
+  // ---- fast path: the half's plan (k_frame_prep: one 64x64 inter CU, one key
+  // per pass, inside the frame) replaces the per-cell resolution (P0): one
+  // scalar load, then straight to the window staging ----
+  if (f.hplan) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 pv;  // a scalar (uniform) load through the constant cache
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(pv) : "s"(f.hplan + hsb) : "memory");
+    const uint4 pl = make_uint4(pv.x, pv.y, pv.z, pv.w);
+    if ((int)pl.w == f.gen) {
+      const __amdgpu_buffer_rsrc_t ring =
+          __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
+      const unsigned meta = pl.y;
+      uint32_t ly[8], lc[4];
+      {
+        const Key K = make_key((int)pl.x, (int)(meta & 255));
+        WinLoad W;
+        win_issue(W, f, ring, K, x0, y0);
+        win_commit(W, L.win);
+        wave_lds_sync();
+        STAMP(4);
+        filter_all(L.win, K, f.bipred, x0, ly, lc, false);
+      }
+      if (meta & CELL_BI) {  // pass 1: mv1, truncating average with pass 0
+        const Key K = make_key((int)pl.z, (int)((meta >> 8) & 255));
+        wave_lds_sync();
+        WinLoad W;
+        win_issue(W, f, ring, K, x0, y0);
+        win_commit(W, L.win);
+        wave_lds_sync();
+        filter_all(L.win, K, f.bipred, x0, ly, lc, true);
+      }
+      STAMP(3);
+      const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
+      const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
+      const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int y = yb + i;
+        uint32_t v = ly[i];
+        if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
+        *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
+        if (i == 7 && h == 1 && gr == 3)  // SB row 63: the edge row k_intra's next SB row reads
+          *(uint32_t *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + x) = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int y = ycb + i;
+        uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
+        if (meta & CELL_RES(1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
+        if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
+        *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
+        *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
+        if (i == 3 && h == 1 && gr == 3) {  // chroma SB row 31
+          uint8_t *e = f.edge + (long long)f.nsbrows * f.ewy + (long long)sby * f.ewc + EDGE_MARGIN + xc;
+          *(uint16_t *)e = (uint16_t)vu;
+          *(uint16_t *)(e + (long long)f.nsbrows * f.ewc) = (uint16_t)vv;
+        }
+      }
+      STAMP(5);
+      return;
+    }
+  }
 
   // reference lookup table (packed by the host)
   if (lane < 32) *(int *)&L.lut[4 * lane] = f.slot_lut[lane];
@@ -605,7 +691,6 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   // ---- P1: prediction (pass 0: mv0; pass 1: mv1 of the bi-pred cells) ----
   const __amdgpu_buffer_rsrc_t ring =  // one descriptor over the whole ring (< 2 GiB: 32-bit offsets)
       __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
-  const int x0 = sbx * 64, y0 = sby * 64 + 32 * h, cc = lane & 15, gr = lane >> 4;
   uint32_t ly[8], lc[4];  // the lane's prediction: 8 luma rows x 4 px, 4 chroma rows x 2 px x (U, V)
   for (int pass = 0; pass <= (int)any_bi; pass++) {
     Items it = job_items(L, pass);

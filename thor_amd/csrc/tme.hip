@@ -482,10 +482,17 @@ static int ti_levels_host(int w, int h) {  // max_levels (:977)
 extern "C" {
 
 thor_ti_t *thor_ti_create(int width, int height, int device) {
-  if (width <= 0 || height <= 0 || (width & 7) || (height & 7)) return nullptr;
-  const int nl = ti_levels_host(width, height);
-  if (nl < 1) return nullptr;
-  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  create_begin();
+  const int nl = width <= 0 || height <= 0 || (width & 7) || (height & 7) ? 0 : ti_levels_host(width, height);
+  if (nl < 1) {
+    create_fail(THOR_ERR_ARG, 0, "thor_ti_create: unsupported frame size %dx%d", width, height);
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    create_fail(THOR_ERR_ARG, 0, "thor_ti_create: no HIP device %d", device);
+    return nullptr;
+  }
   thor_ti *t = new thor_ti();  // value-initialised: every pointer null
   t->width = width;
   t->height = height;
@@ -509,12 +516,15 @@ thor_ti_t *thor_ti_create(int width, int height, int device) {
   }
   bool ok = true;
   // + 256: the search window's last 16-byte tile of a row may run past the last plane's end
-  if (pbytes) ok = hipMalloc(&t->pyr, pbytes + 256) == hipSuccess;
-  ok = ok && hipMalloc(&t->fields, fwords * 4) == hipSuccess;
-  ok = ok && hipMalloc(&t->pub, pwords * 8) == hipSuccess && hipMemset(t->pub, 0, pwords * 8) == hipSuccess;
-  ok = ok && hipMalloc(&t->tickets, 64) == hipSuccess;
-  ok = ok && hipMalloc(&t->err, 64) == hipSuccess && hipMemset(t->err, 0, 64) == hipSuccess;
+  if (pbytes) ok = dev_alloc(&t->pyr, pbytes + 256, "thor_ti_create: pyramids");
+  ok = ok && dev_alloc(&t->fields, fwords * 4, "thor_ti_create: vector fields");
+  ok = ok && dev_alloc(&t->pub, pwords * 8, "thor_ti_create: publication words") &&
+       hipMemset(t->pub, 0, pwords * 8) == hipSuccess;
+  ok = ok && dev_alloc(&t->tickets, 64, "thor_ti_create: tickets");
+  ok = ok && dev_alloc(&t->err, 64, "thor_ti_create: error word") && hipMemset(t->err, 0, 64) == hipSuccess;
   if (!ok) {
+    create_fail(THOR_ERR_HIP, 0, "thor_ti_create: HIP call failed");
+    (void)hipGetLastError();
     thor_ti_destroy(t);
     return nullptr;
   }

@@ -70,7 +70,7 @@ class GpuDecoder:
                        getattr(seq, "interp_ref", 0))
         self.h = self.lib.thor_dec_create(C.byref(cs), device, slots)
         if not self.h:
-            raise RuntimeError("thor_dec_create failed")
+            raise L.create_error("thor_dec_create")
         self._bufs = []
 
     def close(self):

@@ -44,7 +44,7 @@ class GpuEncoder:
             raise ValueError("encoder parameters not supported")
         self.h = self.lib.thor_enc_create(C.byref(params), device)
         if not self.h:
-            raise RuntimeError("thor_enc_create failed")
+            raise L.create_error("thor_enc_create")
         self.W, self.H = params.width, params.height
         self.fsize = self.W * self.H * 3 // 2
         self.seq_dev = None

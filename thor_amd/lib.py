@@ -65,6 +65,7 @@ BATCHED_SYMBOLS = [
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
+    "thor_last_create_error",
 ]
 L2_SURFACE_SYMBOLS = ["deblock_frame_y", "deblock_frame_uv", "make_top_and_left", "get_intra_prediction", "dequantize",
                       "reconstruct_block", "quantize"]
@@ -217,6 +218,8 @@ def load(path: str = LIB_PATH):
     L.thor_h2d.restype = i
     L.thor_d2h.argtypes = [P, P, C.c_size_t]
     L.thor_d2h.restype = i
+    L.thor_last_create_error.argtypes = [C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
+    L.thor_last_create_error.restype = i
     _lib = L
     return L
 
@@ -224,3 +227,28 @@ def load(path: str = LIB_PATH):
 def check(rc: int, what: str):
     if rc != 0:
         raise RuntimeError("%s failed with status %d" % (what, rc))
+
+
+class CreateError(RuntimeError):
+    """A thor_*_create returned NULL: `code` (THOR_ERR_ARG / _NOMEM / _HIP),
+    `bytes` (THOR_ERR_NOMEM: the allocation that failed) and the library's
+    one-line reason."""
+
+    def __init__(self, what: str, code: int, nbytes: int, reason: str):
+        super().__init__("%s failed (%s%s): %s" % (what, ERR_NAMES.get(code, str(code)),
+                                                   ", %d bytes" % nbytes if code == THOR_ERR_NOMEM else "", reason))
+        self.code, self.bytes, self.reason = code, nbytes, reason
+
+
+THOR_ERR_ARG, THOR_ERR_HIP, THOR_ERR_NOMEM, THOR_ERR_REF = -1, -2, -3, -4
+ERR_NAMES = {THOR_ERR_ARG: "THOR_ERR_ARG", THOR_ERR_HIP: "THOR_ERR_HIP", THOR_ERR_NOMEM: "THOR_ERR_NOMEM",
+             THOR_ERR_REF: "THOR_ERR_REF"}
+
+
+def create_error(what: str) -> CreateError:
+    """The reason the calling thread's last create returned NULL."""
+    L = load()
+    n = C.c_size_t(0)
+    buf = C.create_string_buffer(256)
+    code = L.thor_last_create_error(C.byref(n), buf, len(buf))
+    return CreateError(what, code, n.value, buf.value.decode(errors="replace"))
