@@ -65,16 +65,12 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
                                                  TeScratchMem *scratch, unsigned *err, unsigned long long spin_limit,
                                                  int stall_row) {
-  __shared__ TeTx s_tx;
-  __shared__ TeNbr s_nb;
-  __shared__ uint8_t s_pb[TE_BLK];
-  __shared__ TeBlockInfo s_bi[4];
-  __shared__ TeParam s_tmp;
   __shared__ TeFrame s_F;  // the job's frame parameters, read all through the RD loop
   __shared__ TeSB s_sb;    // the superblock's bit writer and ME candidate lists
-  __shared__ TeSmallLv s_sl;  // the small quadtree levels' buffers
-  const TeScratch S = te_scratch(scratch[blockIdx.x], &s_tx, &s_nb, s_pb, s_bi, &s_tmp, &s_sl);
-  te_load_basis(s_tx);
+  // the worker's buffers (te_here): LDS at fixed addresses (g_te_*), global at
+  // fixed offsets from its TeScratchMem
+  g_te_mem = &scratch[blockIdx.x];
+  te_load_basis(g_te_tx);
   te_load_zig();
   TeSB &sb = s_sb;
   const int lane = threadIdx.x;
@@ -119,7 +115,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
       const int sbi = k * J.nsbh + l;
       sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
       sb.bits.cap = THOR_ENC_SB_WORDS * 32;
-      te_encode_sb(s_F, S, sb, k, l);
+      te_encode_sb(s_F, sb, k, l);
       if (lane == 0) {
         J.sb_nbits[sbi] = sb.bits.pos;
         if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);

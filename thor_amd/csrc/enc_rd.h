@@ -72,6 +72,27 @@ TE_FN TeScratch te_local(TeScratch S) {
   S.sl = te_lds(S.sl);
   return S;
 }
+// The worker's buffer table, rebuilt where it is needed instead of passed
+// down the call tree (a table passed by value was copied to the scratch stack
+// at every call, one through LDS had to be held in registers): on the device
+// the LDS members sit at fixed addresses and the global ones at fixed offsets
+// from the worker's TeScratchMem, whose address k_enc_rows leaves in LDS.
+#if defined(TE_HOST)
+static TeScratch g_te_scratch;  // the harness's buffers
+static inline void te_set_scratch(const TeScratch &S) { g_te_scratch = S; }
+static inline TeScratch te_here() { return g_te_scratch; }
+#else
+__shared__ TeTx g_te_tx;
+__shared__ TeNbr g_te_nb;
+__shared__ uint8_t g_te_pb[TE_BLK];
+__shared__ TeBlockInfo g_te_bi[4];
+__shared__ TeParam g_te_tmp;
+__shared__ TeSmallLv g_te_sl;
+__shared__ TeScratchMem *g_te_mem;
+__device__ __forceinline__ TeScratch te_here() {
+  return te_local(te_scratch(*g_te_mem, &g_te_tx, &g_te_nb, g_te_pb, g_te_bi, &g_te_tmp, &g_te_sl));
+}
+#endif
 // State of the superblock being encoded (frame_info mvcand / best_ref are
 // reset per SB, enc/encode_frame.c:117-121) and its bit stream.
 struct TeSB {
@@ -235,10 +256,10 @@ TE_FN void te_recon(uint8_t *rec, int rs, const uint8_t *pb, int ps, const TeTx 
 // encode_and_reconstruct_block_inter, enc/encode_block.c:1469-1532, one
 // component: orig (frame, stride os) - pred -> levels (tiles of `coef`) ->
 // rec (compact, stride size).  Returns cbp (4-bit mask when tb-split).
-TE_NOINL int te_enc_inter_comp(const TeFrame &F_, TeScratch S_, const uint8_t *org, int os, int size, int qp,
+TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, int size, int qp,
                                const uint8_t *pb_, int16_t *coef, uint8_t *rec, int type, int tb_split, int ts) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   const uint8_t *pb = te_lds(pb_);
   TE_P(TP_INTER_COMP);
   TeTx &X = *S.tx;
@@ -279,11 +300,11 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, TeScratch S_, const uint8_t *o
 
 // encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
 // component.  rf / fs: the frame being reconstructed at the CU origin.
-TE_NOINL int te_enc_intra_comp(const TeFrame &F_, TeScratch S_, const uint8_t *org, int os, const uint8_t *rf, int fs,
+TE_NOINL int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs,
                                int ypos, int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
                                int tb_split, int mode, int ur, int dl, int ts) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   uint8_t *pb = te_lds(pb_);
   TE_P(TP_INTRA_COMP);
   TeTx &X = *S.tx;
@@ -365,9 +386,9 @@ TE_FN void te_put_kept(TeBits &b, const uint32_t *w, int nbits) {
 
 // encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
 // bi.rec, write the block's syntax.  Returns the bit count.
-TE_NOINL int te_encode_block(const TeFrame &F_, TeScratch S_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
+TE_NOINL int te_encode_block(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeBlockInfo &bi = *te_lds(&bi_);
   TeBits &b = *te_lds(&b_);
   TeParam &p = *te_lds(&p_);
@@ -392,11 +413,11 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeScratch S_, TeBits &b_, TeBloc
   const int itype = (F.frame_type == TE_I) << 1;  // quantisation type follows the frame type (:1764)
   if (mode == TE_INTRA) {
     const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
-    cy = te_enc_intra_comp(F, S, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb,
+    cy = te_enc_intra_comp(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb,
                            p.coeff, recY, itype | 0, tb_split, p.intra_mode, ur, dl, p.ts);
-    cu = te_enc_intra_comp(F, S, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
+    cu = te_enc_intra_comp(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
                            p.coeff + p.cs, recU, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
-    cv = te_enc_intra_comp(F, S, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
+    cv = te_enc_intra_comp(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
                            p.coeff + 2 * p.cs, recV, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
   } else {
     const int bip = F.enable_bipred;
@@ -427,10 +448,10 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeScratch S_, TeBits &b_, TeBloc
       if (zero_block) {
         te_copy_bytes(bi.rec, S.pb, size * size + 2 * sC * sC);
       } else {
-        cy = te_enc_inter_comp(F, S, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
-        cu = te_enc_inter_comp(F, S, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1,
+        cy = te_enc_inter_comp(F, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
+        cu = te_enc_inter_comp(F, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1,
                                tb_split && size > 8, p.ts);
-        cv = te_enc_inter_comp(F, S, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV,
+        cv = te_enc_inter_comp(F, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV,
                                itype | 1, tb_split && size > 8, p.ts);
       }
     }
@@ -470,9 +491,9 @@ TE_CONST int8_t te_qp_m[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, te_qp_n[9] = {0, -1
 
 // search_intra_prediction_params, enc/encode_block.c:1230-1329: SAD over the
 // first `num_modes` modes in the order DC, HOR, VER, PLANAR, [UPLEFT ...].
-TE_NOINL int te_search_intra(const TeFrame &F_, TeScratch S_, const TeBlockInfo &bi_, int num_modes, int *mode_out) {
+TE_NOINL int te_search_intra(const TeFrame &F_, const TeBlockInfo &bi_, int num_modes, int *mode_out) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   const TeBlockInfo &bi = *te_lds(&bi_);
   TE_P(TP_SEARCH_INTRA);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
@@ -524,11 +545,11 @@ TE_FN uint32_t te_lambda_bits(double lam, int bits) { return (uint32_t)(lam * (d
 // motion_estimate, enc/encode_block.c:830-1016 (params->sync = 0).  `org` /
 // `os`: the block (or partition) of the original; `ref`: the reference at the
 // block (partition) origin; size: the CU size (clip_mv, the size-16 rules).
-TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeScratch S_, TeSB &sb_, int r, const uint8_t *org, int os,
+TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const uint8_t *org, int os,
                                      const uint8_t *ref, int size, int width, int height, TeMv *mv, TeMv mvc, TeMv mvp,
                                      int sign, int xpos, int ypos, int enable_bipred) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   TE_P(TP_ME);
   const int rs = F.rsy, s = sign ? -1 : 1;
@@ -675,28 +696,29 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeScratch S_, TeSB &sb_,
 }
 
 // search_inter_prediction_params, enc/encode_block.c:1331-1396
-TE_FN uint32_t te_search_inter(const TeFrame &F, TeScratch S, TeSB &sb, int r, const uint8_t *org, int os,
+TE_FN uint32_t te_search_inter(const TeFrame &F, TeSB &sb, int r, const uint8_t *org, int os,
                                const TeBlockInfo &bi, TeMv mvc, TeMv mvp, TeMv *mv_arr, int part, int sign,
                                int enable_bipred) {
+  const TeScratch S = te_here();
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, rs = F.rsy;
   const uint8_t *ref_y = F.refy[r] + ypos * rs + xpos;
   TeMv mv, mvp2 = mvp;
   uint32_t sad = 0;
   if (part == 0) {
-    sad += te_motion_estimate(F, S, sb, r, org, os, ref_y, size, size, size, &mv, mvc, mvp2, sign, xpos, ypos,
+    sad += te_motion_estimate(F, sb, r, org, os, ref_y, size, size, size, &mv, mvc, mvp2, sign, xpos, ypos,
                               enable_bipred);
     mv_arr[0] = mv_arr[1] = mv_arr[2] = mv_arr[3] = mv;
   } else if (part == 1) {  // PART_HOR
     for (int index = 0; index < 4; index += 2) {
       const int py = index >> 1;
-      sad += te_motion_estimate(F, S, sb, r, org + py * (size / 2) * os, os, ref_y + py * (size / 2) * rs, size, size,
+      sad += te_motion_estimate(F, sb, r, org + py * (size / 2) * os, os, ref_y + py * (size / 2) * rs, size, size,
                                 size / 2, &mv, mvc, mvp2, sign, xpos, ypos, enable_bipred);
       mv_arr[index] = mv_arr[index + 1] = mv;
       mvp2 = mv_arr[0];
     }
   } else if (part == 2) {  // PART_VER
     for (int index = 0; index < 2; index++) {
-      sad += te_motion_estimate(F, S, sb, r, org + index * (size / 2), os, ref_y + index * (size / 2), size, size / 2,
+      sad += te_motion_estimate(F, sb, r, org + index * (size / 2), os, ref_y + index * (size / 2), size, size / 2,
                                 size, &mv, mvc, mvp2, sign, xpos, ypos, enable_bipred);
       mv_arr[index] = mv_arr[index + 2] = mv;
       mvp2 = mv_arr[0];
@@ -704,7 +726,7 @@ TE_FN uint32_t te_search_inter(const TeFrame &F, TeScratch S, TeSB &sb, int r, c
   } else {  // PART_QUAD
     for (int index = 0; index < 4; index++) {
       const int px = index & 1, py = (index & 2) >> 1;
-      sad += te_motion_estimate(F, S, sb, r, org + py * (size / 2) * os + px * (size / 2), os,
+      sad += te_motion_estimate(F, sb, r, org + py * (size / 2) * os + px * (size / 2), os,
                                 ref_y + py * (size / 2) * rs + px * (size / 2), size, size / 2, size / 2, &mv, mvc,
                                 mvp2, sign, xpos, ypos, enable_bipred);
       mv_arr[index] = mv;
@@ -794,11 +816,11 @@ TE_FN void te_commit_block(const TeFrame &F, const TeBlockInfo &bi) {
 
 // search_bipred_prediction_params, enc/encode_block.c:2047-2202, me_mode 0
 // (the iterative uni-pred search on the modified target org8)
-TE_NOINL uint32_t te_search_bipred(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int part,
+TE_NOINL uint32_t te_search_bipred(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_, int part,
                                    TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_arr0,
                                    TeMv *mv_arr1) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   TeBlockInfo &bi = *te_lds(&bi_);
   const int size = bi.size;
@@ -871,7 +893,7 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
       for (int r = ref_start; r <= ref_end; r++) {
         const int sg = F.ref_fnum[r] > F.frame_num;
         const TeMv mvp2 = (F.frame_type == TE_B && list == 1) ? mv : mvp;
-        const int sad = (int)te_search_inter(F, S, sb, r, S.org8, size, bi, mv_center[r], mvp2, mv_all, part, sg, 1);
+        const int sad = (int)te_search_inter(F, sb, r, S.org8, size, bi, mv_center[r], mvp2, mv_all, part, sg, 1);
         for (int i = 0; i < 4; i++) te_add_mvcand(sb.mc, r, mv_all[i]);
         if (sad < min_sad) {
           min_sad = sad;
@@ -902,8 +924,9 @@ TE_NOINL uint32_t te_search_bipred(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
 // ref1's negated leg; the truncating average of the two bi-table predictions
 // against the original; *c returns the doubly clipped vector, which is what
 // the MV cost and the result use.
-TE_FN uint32_t te_bi_joint_sad(const TeFrame &F, TeScratch S, const uint8_t *org, const uint8_t *p0, const uint8_t *p1,
+TE_FN uint32_t te_bi_joint_sad(const TeFrame &F, const uint8_t *org, const uint8_t *p0, const uint8_t *p1,
                                int size, int ypos, int xpos, TeMv *c, TeMv mvp) {
+  const TeScratch S = te_here();
   const TeMv c0 = te_clip_mv(*c, ypos, xpos, F.W, F.H, size, 0);
   te_mc_luma(S.pb0, size, p0, F.rsy, size, size, c0, 0, 2);
   const TeMv c1 = te_clip_mv(c0, ypos, xpos, F.W, F.H, size, 1);
@@ -922,10 +945,10 @@ TE_FN uint32_t te_bi_joint_sad(const TeFrame &F, TeScratch S, const uint8_t *org
 // is read as stored -- integer-rounded vectors used as quarter-pel ones -- and
 // is first rewritten in place (slots num..3 zeroed, slot 4 = mvp, slot 5 = 0,
 // :1171-1179), which later searches of the superblock see too.
-TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeScratch S_, TeSB &sb_, const TeBlockInfo &bi_,
+TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeSB &sb_, const TeBlockInfo &bi_,
                                      const TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_out) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   const TeBlockInfo &bi = *te_lds(&bi_);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
@@ -955,7 +978,7 @@ TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeScratch S_, TeSB &sb_,
         TeMv c;
         c.y = (int16_t)(mv_ref.y + k);
         c.x = (int16_t)(mv_ref.x + l);
-        const uint32_t sad = te_bi_joint_sad(F, S, org, p0, p1, size, ypos, xpos, &c, mvp);
+        const uint32_t sad = te_bi_joint_sad(F, org, p0, p1, size, ypos, xpos, &c, mvp);
         if (sad < min_sad) {
           min_sad = sad;
           mv_opt = c;
@@ -973,7 +996,7 @@ TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeScratch S_, TeSB &sb_,
   }
   for (int idx = 0; idx < 6; idx++) {  // ME_CANDIDATES, common/global.h:70
     TeMv c = sb.mc.mv[r0][idx];
-    const uint32_t sad = te_bi_joint_sad(F, S, org, p0, p1, size, ypos, xpos, &c, mvp);
+    const uint32_t sad = te_bi_joint_sad(F, org, p0, p1, size, ypos, xpos, &c, mvp);
     if (sad < min_sad) {
       min_sad = sad;
       mv_opt = c;
@@ -986,9 +1009,9 @@ TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeScratch S_, TeSB &sb_,
 }
 
 // mode_decision_rdo, enc/encode_block.c:2204-2479
-TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
+TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   TeBlockInfo &bi = *te_lds(&bi_);
   TE_P(TP_MODE);
@@ -1018,7 +1041,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
       tmp.mv1[0] = bi.skip_c[k].mv1;
       tmp.dir = bi.skip_c[k].bipred_flag;
       tmp.mode = TE_SKIP;
-      const int nbits = te_encode_block(F, S, b, bi, tmp);
+      const int nbits = te_encode_block(F, b, bi, tmp);
       cost = te_cost(F, bi, bi.rec, bi.bwidth, bi.bheight, nbits);
       if (cost < min_cost) {
         min_cost = cost;
@@ -1038,7 +1061,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         tmp.mv1[0] = bi.merge_c[k].mv1;
         tmp.dir = bi.merge_c[k].bipred_flag;
         tmp.mode = TE_MERGE;
-        const int nbits = te_encode_block(F, S, b, bi, tmp);
+        const int nbits = te_encode_block(F, b, bi, tmp);
         cost = te_cost(F, bi, bi.rec, size, size, nbits);
         if (cost < min_cost) {
           min_cost = cost;
@@ -1047,7 +1070,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         }
       }
       if (intra_inter_sad) {
-        sad_intra = (uint32_t)te_search_intra(F, S, bi, F.num_intra_modes, &intra_mode);
+        sad_intra = (uint32_t)te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
         sad_intra += (uint32_t)(int)(F.sqrt_lambda * (double)2 + 0.5);
       }
       // inter: ME per reference
@@ -1071,7 +1094,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         mv_center[r] = mvp;
         sad_inter = TE_MAX_UINT32;
         for (int part = 0; part < bi.max_num_pb_part; part++) {
-          const uint32_t sad = te_search_inter(F, S, sb, r, F.oy + ypos * F.osy + xpos, F.osy, bi, mv_center[r], mvp,
+          const uint32_t sad = te_search_inter(F, sb, r, F.oy + ypos * F.osy + xpos, F.osy, bi, mv_center[r], mvp,
                                                mv_all[part], part, sign, F.enable_bipred);
           for (int i = 0; i < 4; i++) te_add_mvcand(sb.mc, r, mv_all[part][i]);
           te_sync();
@@ -1090,7 +1113,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
             tmp.mode = TE_INTER;
             for (int tbp = min_tb; tbp <= max_tb; tbp++) {
               tmp.tb_param = tbp;
-              const int nbits = te_encode_block(F, S, b, bi, tmp);
+              const int nbits = te_encode_block(F, b, bi, tmp);
               cost = te_cost(F, bi, bi.rec, size, size, nbits);
               // worst_cost = max(worst_cost, cost), best_cost = min(best_cost, cost): int vs uint32 compares
               worst_cost = (uint32_t)worst_cost > cost ? worst_cost : (int32_t)cost;
@@ -1110,7 +1133,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         int r0, r1;
         TeMv a0[4], a1[4];
         const int part = 0;
-        te_search_bipred(F, S, sb, bi, part, mv_center, mvp, &r0, &r1, a0, a1);
+        te_search_bipred(F, sb, bi, part, mv_center, mvp, &r0, &r1, a0, a1);
         tmp.pb_part = part;
         tmp.ref_idx0 = r0;
         tmp.ref_idx1 = r1;
@@ -1120,7 +1143,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         }
         tmp.mode = TE_BIPRED;
         tmp.tb_param = 0;
-        const int nbits = te_encode_block(F, S, b, bi, tmp);
+        const int nbits = te_encode_block(F, b, bi, tmp);
         cost = te_cost(F, bi, bi.rec, size, size, nbits);
         if (cost < min_cost) {
           min_cost = cost;
@@ -1129,14 +1152,14 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         }
         if (frame_type == TE_B && F.speed == 0) {  // joint mv0 = -mv1 search (me_mode 1, :2410-2426)
           TeMv aj[4];
-          te_search_bipred_joint(F, S, sb, bi, mv_center, mvp, &r0, &r1, aj);
+          te_search_bipred_joint(F, sb, bi, mv_center, mvp, &r0, &r1, aj);
           tmp.pb_part = 0;
           tmp.ref_idx0 = r0;
           tmp.ref_idx1 = r1;
           for (int i = 0; i < 4; i++) tmp.mv0[i] = tmp.mv1[i] = aj[i];
           tmp.mode = TE_BIPRED;
           tmp.tb_param = 0;
-          const int nbj = te_encode_block(F, S, b, bi, tmp);
+          const int nbj = te_encode_block(F, b, bi, tmp);
           cost = te_cost(F, bi, bi.rec, size, size, nbj);
           if (cost < min_cost) {
             min_cost = cost;
@@ -1156,7 +1179,7 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
           for (int tbp = 0; tbp <= max_tb; tbp++) {
             tmp.tb_param = tbp;
             tmp.mode = TE_INTRA;
-            const int nbits = te_encode_block(F, S, b, bi, tmp);
+            const int nbits = te_encode_block(F, b, bi, tmp);
             cost = te_cost(F, bi, bi.rec, size, size, nbits);
             if (cost < min_icost) {
               min_icost = cost;
@@ -1166,13 +1189,13 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
         }
         intra_mode = best_mode;
       } else {
-        te_search_intra(F, S, bi, F.num_intra_modes, &intra_mode);
+        te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
       }
       tmp.intra_mode = intra_mode;
       for (int tbp = 0; tbp <= max_tb; tbp++) {
         tmp.tb_param = tbp;
         tmp.mode = TE_INTRA;
-        const int nbits = te_encode_block(F, S, b, bi, tmp);
+        const int nbits = te_encode_block(F, b, bi, tmp);
         cost = te_cost(F, bi, bi.rec, size, size, nbits);
         if (cost < min_cost) {
           min_cost = cost;
@@ -1190,7 +1213,8 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeScratch S_, TeSB &sb_, T
 // ---- early skip (enc/encode_block.c:2481-2783) -------------------------------
 // check_early_skip_sub_block (luma, :2505-2538): 2x2-average + (N/2)-point
 // transform against half the threshold (N = 4: plain 4-point transform).
-TE_FN int te_es_luma(TeScratch S, const uint8_t *org, int os, int size, const uint8_t *pb, int thr) {
+TE_FN int te_es_luma(const uint8_t *org, int os, int size, const uint8_t *pb, int thr) {
+  const TeScratch S = te_here();
   TeTx &X = *S.tx;
   int n = size;
   if (size > 4) {
@@ -1242,9 +1266,9 @@ TE_FN int te_es_chroma(const uint8_t *org, int os, int size, const uint8_t *pb, 
 }
 
 // check_early_skip_block, :2613-2741.  Returns 1 when every sub-block is insignificant.
-TE_NOINL int te_check_early_skip(const TeFrame &F_, TeScratch S_, const TeBlockInfo &bi_, const TeParam &p_) {
+TE_NOINL int te_check_early_skip(const TeFrame &F_, const TeBlockInfo &bi_, const TeParam &p_) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   const TeBlockInfo &bi = *te_lds(&bi_);
   const TeParam &p = *te_lds(&p_);
   TE_P(TP_ES_CHECK);
@@ -1268,7 +1292,7 @@ TE_NOINL int te_check_early_skip(const TeFrame &F_, TeScratch S_, const TeBlockI
         te_mc_luma(pb1, size0, F.refy[p.ref_idx1] + ry, F.rsy, size0, size0, m1, sg1, bip);
         te_avg_rect(pb, size0, pb0, size0, pb1, size0, size0, size0);
         te_sync();
-        if (te_es_luma(S, oY, F.osy, size0, pb, thr_y)) return 0;
+        if (te_es_luma(oY, F.osy, size0, pb, thr_y)) return 0;
         // chroma legs use the unclipped vectors (:2680-2702)
         for (int c = 0; c < 2; c++) {
           te_mc_chroma(pb0, s0c, (c ? F.refv : F.refu)[p.ref_idx0] + rc, F.rsc, s0c, s0c, p.mv0[0], sg0);
@@ -1282,7 +1306,7 @@ TE_NOINL int te_check_early_skip(const TeFrame &F_, TeScratch S_, const TeBlockI
         // the vector is clipped in place for every sub-block (:2722), and the clipped one serves chroma
         TeMv mv = te_clip_mv(p.mv0[0], ypos, xpos, F.W, F.H, size0, sign);
         te_mc_luma(pb, size0, F.refy[p.ref_idx0] + ry, F.rsy, size0, size0, mv, sign, bip);
-        if (te_es_luma(S, oY, F.osy, size0, pb, thr_y)) return 0;
+        if (te_es_luma(oY, F.osy, size0, pb, thr_y)) return 0;
         te_mc_chroma(pb, s0c, F.refu[p.ref_idx0] + rc, F.rsc, s0c, s0c, mv, sign);
         if (te_es_chroma(oU, F.osc, s0c, pb, thr_c)) return 0;
         te_mc_chroma(pb, s0c, F.refv[p.ref_idx0] + rc, F.rsc, s0c, s0c, mv, sign);
@@ -1293,9 +1317,9 @@ TE_NOINL int te_check_early_skip(const TeFrame &F_, TeScratch S_, const TeBlockI
 }
 
 // search_early_skip_candidates, :2743-2783
-TE_NOINL int te_search_early_skip(const TeFrame &F_, TeScratch S_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
+TE_NOINL int te_search_early_skip(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   TeBlockInfo &bi = *te_lds(&bi_);
   TE_P(TP_ES_SEARCH);
@@ -1315,10 +1339,10 @@ TE_NOINL int te_search_early_skip(const TeFrame &F_, TeScratch S_, TeSB &sb_, Te
     tmp.mv0[0] = bi.skip_c[k].mv0;
     tmp.mv1[0] = bi.skip_c[k].mv1;
     tmp.dir = bi.skip_c[k].bipred_flag;
-    if (te_check_early_skip(F, S, bi, tmp)) {
+    if (te_check_early_skip(F, bi, tmp)) {
       early = 1;
       tmp.mode = TE_SKIP;
-      const int nbits = te_encode_block(F, S, sb.bits, bi, tmp);
+      const int nbits = te_encode_block(F, sb.bits, bi, tmp);
       const uint32_t cost = te_cost(F, bi, bi.rec, bi.size, bi.size, nbits);
       if (cost < min_cost) {
         min_cost = cost;
@@ -1334,9 +1358,9 @@ TE_NOINL int te_search_early_skip(const TeFrame &F_, TeScratch S_, TeSB &sb_, Te
 // Template over the CU size: the quadtree recursion unrolls at compile time
 // (64 -> 32 -> 16 -> 8); level L = log2(64 / SIZE) owns TeScratch::lv[L].
 template <int SIZE>
-TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, int ypos, int xpos, int qp) {
+TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeSB &sb_, int ypos, int xpos, int qp) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_local(S_);
+  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   constexpr int L = SIZE == 64 ? 0 : (SIZE == 32 ? 1 : (SIZE == 16 ? 2 : 3));
   const int W = F.W, H = F.H, ft = F.frame_type;
@@ -1381,14 +1405,14 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, i
   }
   if (encode_this && ft != TE_I && F.early_skip_thr > 0.0f) {
     bi.final_encode = 2;
-    const int early = te_search_early_skip(F, S, sb, bi, tmp_coef);
+    const int early = te_search_early_skip(F, sb, bi, tmp_coef);
     te_rewind(b, pos_ref);
     if (early) {
       bi.final_encode = 3;
       if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
-      const int nbit = te_encode_block(F, S, b, bi, bi.bp);
+      const int nbit = te_encode_block(F, b, bi, bi.bp);
       cost = te_cost(F, bi, bi.rec, SIZE, SIZE, nbit);
       te_commit_block(F, bi);
       return cost;
@@ -1401,44 +1425,44 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, i
       else if (ft != TE_I) te_put(b, 1, 0);
       if (SIZE == 64 && F.max_delta_qp) te_write_delta_qp(b, bi.delta_qp);
       cost_small = 0;
-      cost_small += te_process_block<NS>(F, S, sb, ypos, xpos, qp);
-      cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos, qp);
-      cost_small += te_process_block<NS>(F, S, sb, ypos, xpos + NS, qp);
-      cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos + NS, qp);
+      cost_small += te_process_block<NS>(F, sb, ypos, xpos, qp);
+      cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos, qp);
+      cost_small += te_process_block<NS>(F, sb, ypos, xpos + NS, qp);
+      cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos + NS, qp);
     }
   }
   if (encode_this) {
     bi.final_encode = 0;
     // the tmp coefficient set: whichever of cbuf[0..1] the best does not hold
-    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
+    cost = te_mode_decision(F, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
     const int me_threshold = SIZE * SIZE * te_iq8[qp] / 8;
     if constexpr (SIZE > 8) {
       if (top_down && cost > (uint32_t)me_threshold) {
         constexpr int NS = SIZE / 2;
         te_write_super_mode(b, F, bi, 0, 0, 1);
         cost_small = 0;
-        cost_small += te_process_block<NS>(F, S, sb, ypos, xpos, qp);
-        cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos, qp);
-        cost_small += te_process_block<NS>(F, S, sb, ypos, xpos + NS, qp);
-        cost_small += te_process_block<NS>(F, S, sb, ypos + NS, xpos + NS, qp);
+        cost_small += te_process_block<NS>(F, sb, ypos, xpos, qp);
+        cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos, qp);
+        cost_small += te_process_block<NS>(F, sb, ypos, xpos + NS, qp);
+        cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos + NS, qp);
       }
     }
     if (cost <= cost_small) {
       te_rewind(b, pos_ref);
       bi.final_encode = 1;
-      te_encode_block(F, S, b, bi, bi.bp);
+      te_encode_block(F, b, bi, bi.bp);
       te_commit_block(F, bi);
     }
   } else if (encode_rect) {
     bi.final_encode = 0;
-    cost = te_mode_decision(F, S, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
+    cost = te_mode_decision(F, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
     if (cost <= cost_small) {
       te_rewind(b, pos_ref);
       bi.final_encode = 1;
       if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
-      te_encode_block(F, S, b, bi, bi.bp);
+      te_encode_block(F, b, bi, bi.bp);
       te_commit_block(F, bi);
     }
   }
@@ -1449,7 +1473,8 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeScratch S_, TeSB &sb_, i
 // the ME candidate lists, then process_block(64) -- with the delta-qp RD
 // search when max_delta_qp is set (trials leave their candidates behind, as
 // there).  Returns the SB's bit count in sb.bits.
-TE_FN void te_encode_sb(const TeFrame &F, TeScratch S, TeSB &sb, int k, int l) {
+TE_FN void te_encode_sb(const TeFrame &F, TeSB &sb, int k, int l) {
+  const TeScratch S = te_here();
   TE_P(TP_SB);
   const int ypos = k * 64, xpos = l * 64;
   for (int r = 0; r < F.num_ref; r++) {
@@ -1461,7 +1486,7 @@ TE_FN void te_encode_sb(const TeFrame &F, TeScratch S, TeSB &sb, int k, int l) {
   if (F.max_delta_qp) {
     int min_cost = 1 << 30, best_qp = F.qp;
     for (int q = F.qp - F.max_delta_qp; q <= F.qp + F.max_delta_qp; q += F.delta_qp_step) {
-      const int cost = (int)te_process_block<64>(F, S, sb, ypos, xpos, q);
+      const int cost = (int)te_process_block<64>(F, sb, ypos, xpos, q);
       TE_TR(F.frame_num, 6, ypos, xpos, q, cost, 0, 0);
       if (cost < min_cost) {
         min_cost = cost;
@@ -1469,9 +1494,9 @@ TE_FN void te_encode_sb(const TeFrame &F, TeScratch S, TeSB &sb, int k, int l) {
       }
     }
     te_rewind(sb.bits, 0);
-    te_process_block<64>(F, S, sb, ypos, xpos, best_qp);
+    te_process_block<64>(F, sb, ypos, xpos, best_qp);
   } else {
-    te_process_block<64>(F, S, sb, ypos, xpos, F.qp);
+    te_process_block<64>(F, sb, ypos, xpos, F.qp);
   }
   te_bits_flush(sb.bits);
 }

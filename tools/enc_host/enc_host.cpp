@@ -75,7 +75,7 @@ int main(int argc, char **argv) {
   std::vector<TeCell> cells((size_t)(W / 4) * (H / 4));
   std::vector<or_cell_t> ocells(cells.size());
   TeScratchMem *SM = (TeScratchMem *)calloc(1, sizeof(TeScratchMem));
-  const TeScratch S = te_scratch(*SM, &SM->tx, &SM->nb, SM->pb, SM->bi, &SM->tmp, &SM->sl);
+  te_set_scratch(te_scratch(*SM, &SM->tx, &SM->nb, SM->pb, SM->bi, &SM->tmp, &SM->sl));
   te_load_basis(SM->tx);
   TeSB sb;
   std::vector<uint32_t> sbw(1 << 17);
@@ -143,7 +143,7 @@ int main(int argc, char **argv) {
     te_frame_header(fb, pl);
     for (int k = 0; k < nsbv; k++)
       for (int l = 0; l < nsbh; l++) {
-        te_encode_sb(F, S, sb, k, l);
+        te_encode_sb(F, sb, k, l);
         fb.append_words(sb.bits.w, sb.bits.pos);
         if (verbose > 1) fprintf(stderr, "frame %d sb %d,%d bits %d\n", pl.frame_num, k, l, sb.bits.pos);
       }
