@@ -497,26 +497,153 @@ __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bi
   it.pend &= ~((m0 ? 1u : 0u) | (m1 ? 2u : 0u));
 }
 
+// ---- fast-path filters (the half's plan: one key for every cell) ----
+// The fast path's dot products: the builtins (v_dot4c / v_dot2c, each chain
+// seeded by one v_mov).  The VOP3P forms written as inline asm were tried:
+// v_dot4_i32_i8 so written gave wrong, run-to-run varying sums in this kernel
+// (tools/probes/luma_fast_check.hip) and the v_dot2 form measured no faster.
+__device__ __forceinline__ int vdot4(uint32_t a, int taps, int acc) { return dot4(a, taps, acc); }
+__device__ __forceinline__ int vdot2(uint32_t a, int taps, int acc) { return dot2(a, taps, acc); }
+__device__ __forceinline__ int vdot2_0(uint32_t a, int taps) { return dot2(a, taps, 0); }
+
+// The rounding constant of the 2-D filters folded into the horizontal sums:
+// every tap set sums to 64, so adding HB to each H' adds 64 * HB = MC_RND to
+// every vertical sum, and H' + HB stays inside int16 for every table (luma
+// [-12017, 11953] + 8224, chroma [-10232, 10168] + 8224).
+#define HB 8224
+
+// Tap words of a k-tap filter (int8 taps packed from byte 0) placed at byte
+// offset o of a 12-byte window: word w holds the taps that land on bytes
+// 4w .. 4w + 3 (zeros elsewhere).  Uniform: scalar arithmetic.
+__device__ __forceinline__ void shifted_taps(unsigned long long t48, int o, int &w0, int &w1, int &w2) {
+  const unsigned long long lo = t48 << (8 * o);
+  w0 = (int)(uint32_t)lo;
+  w1 = (int)(uint32_t)(lo >> 32);
+  w2 = o > 2 ? (int)(uint32_t)(t48 >> (64 - 8 * o)) : 0;
+}
+
+// Eight luma rows of the lane's 4-px column, generic 6x6 taps.  `base` = the
+// window byte of strip row -2, column -2 rounded down to a dword; sh = the
+// byte offset of column -2 in it (uniform).  Horizontal: three dot4 per pixel
+// on the unshifted dwords with per-pixel shifted tap words (no v_alignbyte);
+// vertical: three dot2 per pixel on (H'[r], H'[r+1]) pairs.
+__device__ __forceinline__ void luma8_fast(const uint8_t *base, int sh, unsigned long long th48, int v01, int v23,
+                                           int v45, uint32_t out[8], bool acc, bool k0 = true, bool k1 = true) {
+  int T[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; j++) shifted_taps(th48, sh + j, T[j][0], T[j][1], T[j][2]);
+  const int hb = HB;  // in a VGPR: the chains' seed (one scalar operand per instruction)
+  int hp[4];
+  uint32_t pa[6][4];
+  auto hrow = [&](int r) {  // strip row r (-2 .. 10) -> P(r - 1)
+    const uint32_t *q = (const uint32_t *)(base + (r + 2) * WL_P);
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+    int hc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) hc[j] = vdot4(d0, T[j][0], vdot4(d1, T[j][1], vdot4(d2, T[j][2], hb)));
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (r > -2) pa[(r + 5) % 6][j] = pack_lo16(hp[j], hc[j]);
+      hp[j] = hc[j];
+    }
+  };
+#pragma unroll
+  for (int r = -2; r <= 2; r++) hrow(r);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    hrow(i + 3);
+    int v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      v[j] = vdot2(pa[(i + 2 + 6) % 6][j], v45, vdot2(pa[(i + 6) % 6][j], v23, vdot2_0(pa[(i - 2 + 6) % 6][j], v01))) >>
+             12;
+    const uint32_t o = pack4_u8(v[0], v[1], v[2], v[3]);
+    if (i < 4 ? k0 : k1) out[i] = acc ? avg_bytes(out[i], o) : o;  // k0 / k1: the segment's key matches
+  }
+}
+
+// Four chroma rows of the lane's 2-px column, U and V (4x4 taps).  sh = byte
+// offset of column -1 in the first dword (uniform).
+__device__ __forceinline__ void chroma4_fast(const uint8_t *bu, const uint8_t *bv, int sh, unsigned long long tc32,
+                                             int v01, int v23, uint32_t out[4], bool acc, bool k0 = true,
+                                             bool k1 = true) {
+  int T[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const unsigned long long x = tc32 << (8 * (sh + j));
+    T[j][0] = (int)(uint32_t)x;
+    T[j][1] = (int)(uint32_t)(x >> 32);
+  }
+  const int hb = HB;
+  int pu_prev[2], pv_prev[2];
+  uint32_t pu[4][2], pv[4][2];
+  auto hrow = [&](int r) {  // strip row r (-1 .. 5)
+    const uint32_t *qu = (const uint32_t *)(bu + (r + 1) * WC_P), *qv = (const uint32_t *)(bv + (r + 1) * WC_P);
+    const uint32_t u0 = qu[0], u1 = qu[1], w0 = qv[0], w1 = qv[1];
+    int hu[2], hv[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      hu[j] = vdot4(u0, T[j][0], vdot4(u1, T[j][1], hb));
+      hv[j] = vdot4(w0, T[j][0], vdot4(w1, T[j][1], hb));
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      if (r > -1) {
+        pu[(r + 3) % 4][j] = pack_lo16(pu_prev[j], hu[j]);
+        pv[(r + 3) % 4][j] = pack_lo16(pv_prev[j], hv[j]);
+      }
+      pu_prev[j] = hu[j];
+      pv_prev[j] = hv[j];
+    }
+  };
+#pragma unroll
+  for (int r = -1; r <= 1; r++) hrow(r);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    hrow(i + 2);
+    int au[2], av[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      au[j] = vdot2(pu[(i + 1) % 4][j], v23, vdot2_0(pu[(i + 3) % 4][j], v01)) >> 12;
+      av[j] = vdot2(pv[(i + 1) % 4][j], v23, vdot2_0(pv[(i + 3) % 4][j], v01)) >> 12;
+    }
+    const uint32_t uv = pack4_u8(au[0], au[1], av[0], av[1]);
+    if (i < 2 ? k0 : k1) out[i] = acc ? avg_bytes(out[i], uv) : uv;
+  }
+}
+
 // The half's plan says every cell has key K in this pass: filter straight
 // into the prediction registers (no per-segment key match).
 __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bipred, int x0, uint32_t ty[8],
-                                           uint32_t tc[4], bool acc) {
+                                           uint32_t tc[4], bool acc, bool k0 = true, bool k1 = true) {
   const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
   const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
   const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
   const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
   const LdsChroma c{w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3)};
   if (K.fx == 2 && K.fy == 2) {
-    luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ty, acc);
+    if (k0 && k1) {
+      luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ty, acc);
+    } else {
+      uint32_t ny[8];
+      luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ny, false);
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (i < 4 ? k0 : k1) ty[i] = acc ? avg_bytes(ty[i], ny[i]) : ny[i];
+    }
   } else {
     int v01, v23, v45;
     tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45);
-    luma_rows<0, 8>(l, (uint32_t)(lwb & 3), g_taps.luma[bipred][K.fx][0], g_taps.luma[bipred][K.fx][1], v01, v23, v45,
-                    ty, acc);
+    const unsigned long long th48 = (unsigned long long)(uint32_t)g_taps.luma[bipred][K.fx][0] |
+                                    ((unsigned long long)(uint32_t)(g_taps.luma[bipred][K.fx][1] & 0xffff) << 32);
+    luma8_fast(w.y + 8 * gr * WL_P + (lwb & ~3), lwb & 3, th48, v01, v23, v45, ty, acc, k0, k1);
   }
   const int cvt = g_taps.chroma[K.cfy];
-  chroma_rows<0, 4>(c, (uint32_t)(cwb & 3), g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
-                    (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc, acc);
+  chroma4_fast(w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3), cwb & 3,
+               (unsigned long long)(uint32_t)g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
+               (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc, acc, k0, k1);
+  (void)l;
+  (void)c;
 }
 
 // Waves whose items need several keys: every item straight from the ring,
@@ -589,7 +716,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   const int x0 = sbx * 64, y0 = sby * 64 + 32 * h, cc = lane & 15, gr = lane >> 4;
 
   // ---- fast path: the half's plan (k_frame_prep: one 64x64 inter CU, one key
-  // per pass, inside the frame) replaces the per-cell resolution (P0): one
+  // per pass) replaces the per-cell resolution (P0): one
   // scalar load, then straight to the window staging ----
   if (f.hplan) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -623,9 +750,13 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
       const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
       const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
       const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
+      // a half at the frame's bottom / right edge stores only its pixels inside
+      // (W, H multiples of 8: a lane's 4 luma / 2 chroma columns are all in or all out)
+      const bool xin = x < f.W;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const int y = yb + i;
+        if (!xin || y >= f.H) continue;
         uint32_t v = ly[i];
         if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
         *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
@@ -635,6 +766,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int y = ycb + i;
+        if (!xin || y >= (f.H >> 1)) continue;
         uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
         if (meta & CELL_RES(1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
         if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);

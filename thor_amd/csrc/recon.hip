@@ -67,15 +67,15 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
     f.cellmc[idx] = make_uint2((uint32_t)((m0x & 0xffff) | (m0y << 16)), meta);
     if (act && bi) f.cellmv1[idx] = (m1x & 0xffff) | (m1y << 16);
   }
-  // Half-SB plans (FrameCtx::hplan): lane h of a 64x64 inter CU inside the
-  // frame writes half h's record when quarters 2h and 2h+1 share their MVs
+  // Half-SB plans (FrameCtx::hplan): lane h of a 64x64 inter CU whose half h
+  // has rows inside the frame writes half h's record when quarters 2h and 2h+1 share their MVs
   // (always so for SKIP / MERGE, which use mv_arr[0]; INTER / BIPRED halves of
   // a horizontal split too).
   if (f.hplan && S == 64 && lane < 2 && mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0)) {
     const int h = lane, q0 = quarters ? 2 * h : 0, q1 = quarters ? 2 * h + 1 : 0;
     const bool same = B.mv0[2 * q0] == B.mv0[2 * q1] && B.mv0[2 * q0 + 1] == B.mv0[2 * q1 + 1] &&
                       (!bi || (B.mv1[2 * q0] == B.mv1[2 * q1] && B.mv1[2 * q0 + 1] == B.mv1[2 * q1 + 1]));
-    const bool inside = B.xpos + 64 <= f.W && B.ypos + 32 * (h + 1) <= f.H;
+    const bool inside = B.ypos + 32 * h < f.H;  // rows / columns past the frame edge are not stored (k_recon)
     if (same && inside) {
       int m0x = B.mv0[2 * q0], m0y = B.mv0[2 * q0 + 1], m1x = B.mv1[2 * q0], m1y = B.mv1[2 * q0 + 1];
       if (sg0) { m0x = -m0x; m0y = -m0y; }
