@@ -487,7 +487,7 @@ def main():
     ap.add_argument("--dec-slots", type=int, default=10,
                     help="reference ring slots per decoder context (LDB: up to 4 references + the current frame)")
     ap.add_argument("--streams", type=int, default=240, help="independent streams (encoder + decoder) per GPU")
-    ap.add_argument("--dec-priority", type=int, default=1,
+    ap.add_argument("--dec-priority", type=int, default=0,
                     help="1: decoder groups on high-priority HIP streams (their launches dispatch ahead of the "
                          "encoder's queued workgroups); 0: default priority")
     ap.add_argument("--clips", type=int, default=8, help="distinct seeded clips the streams are drawn from (<= 8)")

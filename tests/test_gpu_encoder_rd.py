@@ -2,6 +2,7 @@
 reference encoder's own bitstreams (tests/golden/<name>.bit, written by the
 reference Thorenc from the seeded synthetic clips) must come out byte for
 byte, frame by frame."""
+import os
 import time
 import hashlib
 
@@ -117,6 +118,9 @@ def test_device_encoder_hierarchical_b(name, streams):
     _encode_and_compare(name, streams[name]["frames"], streams)
 
 
+@pytest.mark.skipif(not os.environ.get("THOR_LONG_GPU_TESTS"),
+                    reason="minutes per frame at speed 0 on one stream: run with THOR_LONG_GPU_TESTS=1 "
+                           "(tools/gpu_long.sh; log in profiles/)")
 def test_device_encoder_4k_hdb16_high_efficiency(streams):
     """BASELINE config 5 at its stated size and operating point: 4K
     config_HDB16_high_efficiency (speed 0, interpolated references, 4

@@ -240,7 +240,7 @@ class CreateError(RuntimeError):
         self.code, self.bytes, self.reason = code, nbytes, reason
 
 
-THOR_ERR_ARG, THOR_ERR_HIP, THOR_ERR_NOMEM, THOR_ERR_REF = -1, -2, -3, -4
+THOR_OK, THOR_ERR_ARG, THOR_ERR_HIP, THOR_ERR_NOMEM, THOR_ERR_REF = 0, -1, -2, -3, -4
 ERR_NAMES = {THOR_ERR_ARG: "THOR_ERR_ARG", THOR_ERR_HIP: "THOR_ERR_HIP", THOR_ERR_NOMEM: "THOR_ERR_NOMEM",
              THOR_ERR_REF: "THOR_ERR_REF"}
 

@@ -7,5 +7,5 @@ TAG=$1; T=$2; TO=${3:-900}
 ( while sleep 30; do date +%T >> gpurun_out/${TAG}_heartbeat; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-timeout -k 10 $TO python -u -m pytest "$T" -x -v -s --timeout $((TO - 30)) --timeout-method thread > gpurun_out/${TAG}_long.log 2>&1 || { echo LONG_FAIL; tail -30 gpurun_out/${TAG}_long.log; exit 1; }
+THOR_LONG_GPU_TESTS=1 timeout -k 10 $TO python -u -m pytest "$T" -x -v -s --timeout $((TO - 30)) --timeout-method thread > gpurun_out/${TAG}_long.log 2>&1 || { echo LONG_FAIL; tail -30 gpurun_out/${TAG}_long.log; exit 1; }
 tail -5 gpurun_out/${TAG}_long.log
