@@ -182,6 +182,17 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
  * rank's loop filters then cover 1/N of the frame instead of all of it. */
 int thor_dec_set_band_local(thor_dec_t *d, int on);
 int thor_dec_frame_finish(thor_dec_t *d);
+/* MV-reach halo exchange (band-local contexts, thor_amd/shard.py halo mode):
+ * instead of all-gathering every band's final rows, each rank fetches, before
+ * a frame's thor_dec_frame_begin, only the rows of its references that the
+ * frame's vectors in its band can reach.  put_ref_rows writes rows
+ * [y0, y0 + nrows) (y0, nrows even; same packing as get_rows) into the
+ * resident frame `frame_num` without touching the intra edge rows;
+ * pad_frame then redoes that frame's border padding from its edge pixels (the
+ * rows a rank holds final are padded correctly; a vector reaching past the
+ * frame edge makes its rank fetch the edge row). */
+int thor_dec_put_ref_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const void *src);
+int thor_dec_pad_frame(thor_dec_t *d, int frame_num);
 
 /* Host helper: write the decode-order indices of the intra CUs of a frame
  * (host descriptors) to `out` (may be NULL to count); returns the count. */

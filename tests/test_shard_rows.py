@@ -32,8 +32,11 @@ class NumpyContext:
         self.W, self.H, self.truth = W, H, truth
         self.band = None
         self.local = False
+        self.halo = False
         self.cur = None
         self.bufs = {}
+        self.refs = {}
+        self.frames = {}  # halo mode: parse-output stand-ins, to check the fetched rows
 
     def set_band(self, b0, b1):
         self.band = (b0, b1)
@@ -42,6 +45,14 @@ class NumpyContext:
         self.local = on
 
     def begin(self, fnum):  # the "device frame" is the frame number here
+        if self.halo and fnum in self.frames:  # every reference row the band's vectors reach is final
+            from thor_amd.shard import halo_requests
+
+            r0, r1 = 64 * self.band[0], min(64 * self.band[1], self.H)
+            for f, (lo, hi) in halo_requests(self.frames[fnum], self.H, r0, r1).items():
+                for k, (got, want) in enumerate(zip(self.refs[f], self.truth[f])):
+                    a, b = (lo, hi) if k == 0 else (lo // 2, hi // 2)
+                    assert np.array_equal(got[a:b], want[a:b]), (fnum, f, k, lo, hi)
         y, u, v = (np.zeros_like(p) for p in self.truth[fnum])
         r0, r1 = 64 * self.band[0], min(64 * self.band[1], self.H)
         y[r0:r1] = self.truth[fnum][0][r0:r1]
@@ -55,8 +66,8 @@ class NumpyContext:
         return k
 
     def get_rows(self, fnum, y0, n, key):
-        assert fnum == self.cur[0]
-        buf, (y, u, v) = self.bufs[key], self.cur[1]
+        planes = self.cur[1] if self.cur is not None and fnum == self.cur[0] else self.refs[fnum]
+        buf, (y, u, v) = self.bufs[key], planes
         m = max(0, min(n, self.H - y0))
         W = self.W
         buf[:m * W] = y[y0:y0 + m].reshape(-1)
@@ -76,11 +87,11 @@ class NumpyContext:
             p[y0 // 2:y0 // 2 + m // 2] = buf[o:o + (m // 2) * (W // 2)].reshape(m // 2, W // 2)
             o += (n // 2) * (W // 2)
 
-    def d2h(self, out, key):
-        out[:] = self.bufs[key]
+    def d2h(self, out, key):  # the first out.nbytes bytes, as GpuDecoder.d2h
+        out[:] = self.bufs[key][:out.size]
 
     def h2d(self, key, arr):
-        self.bufs[key][:] = arr
+        self.bufs[key][:arr.size] = arr
 
     def end(self):
         fnum, planes = self.cur
@@ -96,8 +107,28 @@ class NumpyContext:
     def finish(self):
         assert self.local
         fnum, planes = self.cur
-        for got, want in zip(planes, self.truth[fnum]):
-            assert np.array_equal(got, want), fnum
+        if not self.halo:
+            for got, want in zip(planes, self.truth[fnum]):
+                assert np.array_equal(got, want), fnum
+        self.refs[fnum] = planes  # a reference from now on (halo mode: final in the band only)
+        self.cur = None
+
+    # --- halo mode (MV-reach exchange of reference rows) ---
+    def put_ref_rows(self, fnum, y0, n, key):
+        buf, (y, u, v) = self.bufs[key], self.refs[fnum]
+        m = max(0, min(n, self.H - y0))
+        W = self.W
+        y[y0:y0 + m] = buf[:m * W].reshape(m, W)
+        o = n * W
+        for p in (u, v):
+            p[y0 // 2:y0 // 2 + m // 2] = buf[o:o + (m // 2) * (W // 2)].reshape(m // 2, W // 2)
+            o += (n // 2) * (W // 2)
+
+    def pad_frame(self, fnum):
+        assert fnum in self.refs
+
+    def sync(self):
+        pass
 
 
 def _worker(rank, world, port, W, H, q, local=False):
@@ -133,6 +164,109 @@ def test_row_shard_exchange_gloo(world, W, H, local):
     q = ctx.Queue()
     port = random.randint(20000, 40000)
     procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q, local)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(r, "ok") for r in range(world)], res
+
+
+class FakeFrame:
+    """Parse-output stand-in for halo_requests: 64x64 inter CUs with random
+    vectors (display-order reference = the previous frame)."""
+
+    def __init__(self, fnum, W, H, rng, reach):
+        from thor_amd.trace import BLOCK_DTYPE
+
+        self.frame_num = fnum
+        self.interp_refs = (-1, -1)
+        self.interp_ratio = 0
+        n = ((W + 63) // 64) * ((H + 63) // 64) if fnum > 0 else 0
+        b = np.zeros(n, BLOCK_DTYPE)
+        k = 0
+        for sy in range(0, H, 64):
+            for sx in range(0, W, 64):
+                if k >= n:
+                    break
+                b[k]["ypos"], b[k]["xpos"], b[k]["size"] = sy, sx, 64
+                b[k]["bwidth"], b[k]["bheight"] = min(64, W - sx), min(64, H - sy)
+                b[k]["mode"] = 2
+                b[k]["ref0"], b[k]["ref1"] = fnum - 1, -1
+                b[k]["mv0"][:] = rng.integers(-4 * reach, 4 * reach + 1, 8)
+                k += 1
+        self.blocks = b
+
+
+def test_halo_requests_cover_every_footprint():
+    """Every 6-tap luma / 4-tap chroma footprint of every inter CU of a band,
+    for either sign of its vectors, lies inside the requested rows."""
+    from thor_amd.shard import halo_requests
+
+    rng = np.random.default_rng(3)
+    W, H = 192, 320
+    for fnum in range(1, 6):
+        fr = FakeFrame(fnum, W, H, rng, reach=50)
+        for r0, r1 in ((0, 128), (128, 256), (256, 320)):
+            req = halo_requests(fr, H, r0, r1)
+            for blk in fr.blocks:
+                if not (r0 <= blk["ypos"] < r1):
+                    continue
+                lo, hi = req[int(blk["ref0"])]
+                for q in range(4):
+                    mvy = int(blk["mv0"][2 * q + 1])
+                    for s_ in (1, -1):
+                        dy = (s_ * mvy) >> 2
+                        a = max(0, int(blk["ypos"]) + dy - 2)
+                        b_ = min(H, int(blk["ypos"]) + int(blk["bheight"]) + dy + 3)
+                        assert lo <= a and b_ <= hi, (fnum, r0, lo, hi, a, b_)
+                        cdy = (s_ * mvy) >> 3  # chroma rows, in luma units
+                        assert lo <= max(0, 2 * ((int(blk["ypos"]) >> 1) + cdy - 1))
+                        assert min(H, 2 * ((int(blk["ypos"]) + int(blk["bheight"])) // 2 + cdy + 2)) <= hi
+
+
+def _halo_worker(rank, world, port, W, H, q):
+    import torch.distributed as dist
+
+    from thor_amd.shard import RowShard
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(7)  # same frames on every rank
+        nf = 5
+        truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
+                     rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(nf)}
+        frames = {f: FakeFrame(f, W, H, rng, reach=40) for f in range(nf)}
+        ctx = NumpyContext(W, H, truth)
+        ctx.halo = True
+        ctx.frames = frames
+        sh = RowShard(ctx, dist, W, H, device_exchange=False, band_local=True, halo=True)
+        for f in range(nf):
+            sh.decode(f, f, frames[f])
+        assert sh.halo_bytes[0] == 0 and sum(sh.halo_bytes) > 0, sh.halo_bytes
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-600:]))
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 192, 320), (3, 128, 448)])
+def test_row_shard_halo_exchange_gloo(world, W, H):
+    """Halo mode: no second all-gather; before each frame every rank fetches the
+    reference rows its band's vectors reach from their owners, and those rows
+    must be final (NumpyContext.begin checks them against the truth)."""
+    import random
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, W, H, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -877,6 +877,48 @@ int thor_dec_read_frame(thor_dec_t *d, int frame_num, uint8_t *y, uint8_t *u, ui
   return THOR_OK;
 }
 
+int thor_dec_put_ref_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const void *src) {
+  if (!d || !src || y0 < 0 || nrows <= 0 || (y0 & 1) || (nrows & 1)) return THOR_ERR_ARG;
+  const int s = find_slot_host(d, frame_num);  // a resident reference, not the frame being decoded
+  if (s < 0) return THOR_ERR_REF;
+  const int W = d->seq.width, H = d->seq.height;
+  const int n = y0 + nrows > H ? H - y0 : nrows;
+  if (n <= 0) return THOR_OK;
+  uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  const uint8_t *i = (const uint8_t *)src;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipMemcpy2DAsync(base + d->offy + (long long)y0 * d->sy, d->sy, i, W, W, n, hipMemcpyDeviceToDevice, d->stream));
+  i += (long long)nrows * W;
+  for (int c = 0; c < 2; c++) {
+    const long long off = (c ? d->offv : d->offu) + (long long)(y0 / 2) * d->sc;
+    HIPCHK(hipMemcpy2DAsync(base + off, d->sc, i, W / 2, W / 2, n / 2, hipMemcpyDeviceToDevice, d->stream));
+    i += (long long)(nrows / 2) * (W / 2);
+  }
+  return THOR_OK;
+}
+
+int thor_dec_pad_frame(thor_dec_t *d, int frame_num) {
+  if (!d) return THOR_ERR_ARG;
+  const int s = find_slot_host(d, frame_num);
+  if (s < 0) return THOR_ERR_REF;
+  const int W = d->seq.width, H = d->seq.height;
+  uint8_t *base = d->slots + (long long)s * d->slot_bytes;
+  FrameBatch fb;
+  memset(&fb, 0, sizeof(fb));
+  FrameCtx *hp = fb.f;
+  hp->cy = base + d->offy;
+  hp->cu = base + d->offu;
+  hp->cv = base + d->offv;
+  hp->sy = d->sy;
+  hp->sc = d->sc;
+  hp->W = W;
+  hp->H = H;
+  HIPCHK(hipSetDevice(d->device));
+  k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(fb);
+  HIPCHK(hipGetLastError());
+  return THOR_OK;
+}
+
 int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const uint8_t *u, const uint8_t *v) {
   if (!d || !y || !u || !v || d->pending) return THOR_ERR_ARG;
   HIPCHK(hipSetDevice(d->device));

@@ -169,6 +169,12 @@ class GpuDecoder:
     def put_rows(self, frame_num: int, y0: int, nrows: int, src_ptr):
         L.check(self.lib.thor_dec_put_rows(self.h, frame_num, y0, nrows, src_ptr), "thor_dec_put_rows")
 
+    def put_ref_rows(self, frame_num: int, y0: int, nrows: int, src_ptr):
+        L.check(self.lib.thor_dec_put_ref_rows(self.h, frame_num, y0, nrows, src_ptr), "thor_dec_put_ref_rows")
+
+    def pad_frame(self, frame_num: int):
+        L.check(self.lib.thor_dec_pad_frame(self.h, frame_num), "thor_dec_pad_frame")
+
     def scratch(self, nbytes: int) -> int:
         return self._buf(np.zeros(max(nbytes, 16), np.uint8)).ptr
 
