@@ -493,6 +493,9 @@ def main():
     ap.add_argument("--clips", type=int, default=8, help="distinct seeded clips the streams are drawn from (<= 8)")
     ap.add_argument("--band-local", action="store_true",
                     help="--shard rows: each rank deblocks / CLPFs only its band, then a second all-gather of final rows")
+    ap.add_argument("--halo", action="store_true",
+                    help="--shard rows, band-local: no second all-gather; each rank fetches the reference rows its "
+                         "band's vectors reach (MV-reach halo exchange, thor_amd/shard.py)")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
                     help="streams: independent enc+dec streams per GPU (default); rows: decode-only, ONE "
                          "stream's SB rows split across the ranks with an RCCL all-gather before intra/deblock")
@@ -888,11 +891,12 @@ def rows_mode(a, torch, dist, rank, world, local):
     seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
     dec = GpuDecoder(seq, device=local)
     devs = [dec.upload(fr) for fr in frames]
-    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=a.band_local)
+    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=a.band_local or a.halo,
+                  halo=a.halo)
 
     def step():
         for d, fr in zip(devs, frames):
-            sh.decode(d, fr.frame_num)
+            sh.decode(d, fr.frame_num, fr)
 
     for _ in range(max(1, a.warmup)):
         step()
@@ -911,6 +915,8 @@ def rows_mode(a, torch, dist, rank, world, local):
     okt = torch.tensor([1 if ok else 0], device="cuda")
     dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     elapsed, ok = float(t.item()), bool(okt.item())
+    if a.halo and world > 1:  # each rank holds only its band final: not checked here (tests/test_gpu_shard.py is)
+        ok = None
     px_step = seq.width * seq.height * len(frames)
     if rank == 0:
         print(json.dumps({
@@ -921,8 +927,9 @@ def rows_mode(a, torch, dist, rank, world, local):
             "bit_exact": ok,
             "config": {"workload": "ONE 4K 8-frame LDB-low stream, SB rows sharded across %d GPU(s): band k_recon, "
                                    "RCCL all-gather of pre-deblock bands, whole-frame intra, %s" % (
-                                   world, "band-local deblock/CLPF + all-gather of final bands, pad" if a.band_local
-                                   else "whole-frame deblock/CLPF/pad"),
+                                   world, "band-local deblock/CLPF, pad, MV-reach halo exchange of reference rows"
+                                   if a.halo else "band-local deblock/CLPF + all-gather of final bands, pad"
+                                   if a.band_local else "whole-frame deblock/CLPF/pad"),
                        "parallelism": "rows%d" % world, "frames": len(frames)},
         }), flush=True)
     dec.close()
