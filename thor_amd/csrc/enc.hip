@@ -218,6 +218,11 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
   if (threadIdx.x == 0) *J.out_bits = (int)total;
 }
 
+// Every job's coded-bit count into one array (one readback per batch).
+__global__ __launch_bounds__(512) void k_enc_nbits(const TeJob *__restrict__ jobs, int n, int *__restrict__ out) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = *jobs[i].out_bits;
+}
+
 // ============================================================================
 // Host side
 // ============================================================================
@@ -310,6 +315,13 @@ struct EncPool {
   TeJob *jobs = nullptr;
   long long *scan = nullptr;
   size_t scan_n = 0;
+  // per batch: every context's frame-header words (one upload) and coded-bit
+  // counts (one readback), and pinned staging for the coded words (async
+  // readbacks, one synchronisation)
+  uint32_t *hdr_all = nullptr;
+  int *nb_all = nullptr;
+  uint8_t *rb_host = nullptr;
+  size_t rb_cap = 0;
 };
 static std::mutex g_pools_mu;
 static std::map<int, EncPool *> g_pools;
@@ -328,6 +340,8 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n) {
     EHIP(hipMalloc(&P.err, 64));
     EHIP(hipMemset(P.err, 0, 64));
     EHIP(hipMalloc(&P.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
+    EHIP(hipMalloc(&P.hdr_all, THOR_ENC_MAX_BATCH * 64 * sizeof(uint32_t)));
+    EHIP(hipMalloc(&P.nb_all, THOR_ENC_MAX_BATCH * sizeof(int)));
   }
   if (nwork > P.nwork) {
     if (P.scratch) (void)hipFree(P.scratch);
@@ -416,7 +430,11 @@ int thor_enc_next_input(const thor_enc_t *e) {
 }
 void *thor_enc_stream(thor_enc_t *e) { return e ? (void *)e->stream : nullptr; }
 
-static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob &J, TeFramePlan &pl, int &cur_slot) {
+// One context's frame job.  Its device setup (cell and progress resets) is
+// enqueued on the batch stream `st`; its header words go to `hw` (host), which
+// the caller uploads with every context's in one copy to `hdr_dev`.
+static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob &J, TeFramePlan &pl, int &cur_slot,
+                       hipStream_t st, uint32_t *hw, uint32_t *hdr_dev) {
   pl = e->gop->plans[e->pos];
   // the frame being coded takes a slot no window entry holds
   std::vector<int> held(e->nslots, 0);
@@ -487,7 +505,6 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   J.clpf_bits = e->clpf_bits;
   J.clpf_flags = e->clpf_flags;
   J.cellinfo = e->cellinfo;
-  J.hdr_words = e->hdr_words;
   J.out_words = e->out_words;
   J.out_bits = e->out_bits;
   J.nsbh = e->nsbh;
@@ -497,13 +514,14 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   TeHostBits hb;
   if (e->first) te_seq_header(hb, P);
   te_frame_header(hb, pl);
-  std::vector<uint32_t> hw(64, 0);
+  for (int i = 0; i < 64; i++) hw[i] = 0;
+  if (hb.nbits > 64 * 32) return THOR_ERR_ARG;
   for (uint64_t i = 0; i < hb.nbits; i++)
     if (hb.bytes[i >> 3] & (0x80 >> (i & 7))) hw[i >> 5] |= 0x80000000u >> (i & 31);
   J.hdr_bits = (int)hb.nbits;
-  EHIP(hipMemcpyAsync(e->hdr_words, hw.data(), 64 * 4, hipMemcpyHostToDevice, e->stream));
-  EHIP(hipMemsetAsync(e->cells, 0, (size_t)(W / 4) * (H / 4) * sizeof(TeCell), e->stream));
-  EHIP(hipMemsetAsync(e->progress, 0, (size_t)e->nsbv * sizeof(unsigned), e->stream));
+  J.hdr_words = hdr_dev;
+  EHIP(hipMemsetAsync(e->cells, 0, (size_t)(W / 4) * (H / 4) * sizeof(TeCell), st));
+  EHIP(hipMemsetAsync(e->progress, 0, (size_t)e->nsbv * sizeof(unsigned), st));
   return THOR_OK;
 }
 
@@ -565,15 +583,18 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   std::vector<TeJob> jobs(n);
   std::vector<TeFramePlan> plans(n);
   std::vector<int> cur(n);
+  std::vector<uint32_t> hdr((size_t)n * 64);
   for (int i = 0; i < n; i++) {
     thor_enc *e = es[i];
     if (e->stream != st) {  // the members' earlier work on their own streams comes first
       EHIP(hipStreamSynchronize(e->stream));
     }
     const int s = orig_stride ? orig_stride[i] : W;
-    if ((rc = enc_prepare(e, orig[i], s, jobs[i], plans[i], cur[i])) != THOR_OK) return rc;
-    EHIP(hipStreamSynchronize(e->stream));  // per-context header / memsets (tiny) before the shared stream
+    if ((rc = enc_prepare(e, orig[i], s, jobs[i], plans[i], cur[i], st, &hdr[(size_t)i * 64], P.hdr_all + i * 64)) !=
+        THOR_OK)
+      return rc;
   }
+  EHIP(hipMemcpyAsync(P.hdr_all, hdr.data(), hdr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   // interpolated references: each context's on its own stream (they overlap), all done before the RD loop
   bool any_interp = false;
   for (int i = 0; i < n; i++)
@@ -641,9 +662,12 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   }
   k_enc_pack<<<n, 256, 0, st>>>(P.jobs, P.scan, lead->out_cap_words);
   EHIP(hipGetLastError());
-  // read back every stream's frame
+  // read back every stream's frame: the bit counts in one copy, then every
+  // stream's words into pinned staging, asynchronously, one synchronisation
+  k_enc_nbits<<<1, 512, 0, st>>>(P.jobs, n, P.nb_all);
+  EHIP(hipGetLastError());
   std::vector<int> nbits(n);
-  for (int i = 0; i < n; i++) EHIP(hipMemcpyAsync(&nbits[i], es[i]->out_bits, sizeof(int), hipMemcpyDeviceToHost, st));
+  EHIP(hipMemcpyAsync(nbits.data(), P.nb_all, n * sizeof(int), hipMemcpyDeviceToHost, st));
   EHIP(hipStreamSynchronize(st));
   unsigned err = 0;
   EHIP(hipMemcpy(&err, P.err, sizeof(unsigned), hipMemcpyDeviceToHost));
@@ -652,13 +676,26 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
     EHIP(hipMemset(P.err, 0, 4));
     return THOR_ERR_HIP;
   }
+  std::vector<size_t> woff(n + 1, 0);
+  for (int i = 0; i < n; i++) {
+    if (nbits[i] < 0) return THOR_ERR_NOMEM;
+    woff[i + 1] = woff[i] + ((((size_t)nbits[i] + 7) / 8 + 3) / 4) * 4;
+  }
+  if (woff[n] > P.rb_cap) {
+    if (P.rb_host) (void)hipHostFree(P.rb_host);
+    P.rb_host = nullptr;
+    P.rb_cap = 0;
+    EHIP(hipHostMalloc((void **)&P.rb_host, woff[n] * 2 + 4096, hipHostMallocDefault));
+    P.rb_cap = woff[n] * 2 + 4096;
+  }
+  for (int i = 0; i < n; i++)
+    if (woff[i + 1] > woff[i])
+      EHIP(hipMemcpyAsync(P.rb_host + woff[i], es[i]->out_words, woff[i + 1] - woff[i], hipMemcpyDeviceToHost, st));
+  EHIP(hipStreamSynchronize(st));
   for (int i = 0; i < n; i++) {
     thor_enc *e = es[i];
-    if (nbits[i] < 0) return THOR_ERR_NOMEM;
-    const size_t nb = ((size_t)nbits[i] + 7) / 8, nw = (nb + 3) / 4;
-    std::vector<uint32_t> w(nw + 1);
-    EHIP(hipMemcpyAsync(w.data(), e->out_words, nw * 4, hipMemcpyDeviceToHost, st));
-    EHIP(hipStreamSynchronize(st));
+    const size_t nb = ((size_t)nbits[i] + 7) / 8;
+    const uint32_t *w = (const uint32_t *)(P.rb_host + woff[i]);
     e->chunk.resize(4 + nb);
     e->chunk[0] = (uint8_t)(nb >> 24);
     e->chunk[1] = (uint8_t)(nb >> 16);
