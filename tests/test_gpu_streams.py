@@ -150,3 +150,54 @@ def test_missing_reference_is_an_error():
         assert dec.lib.thor_dec_sync(dec.h) == 0
     finally:
         dec.close()
+
+
+def _parsed(name):
+    import os
+
+    from conftest import GOLD
+
+    bit = os.path.join(GOLD, name + ".bit")
+    if name.endswith(("hdbi", "hdbi_high")) and os.path.exists(bit):  # the interpolated-reference headers
+        from thor_amd.bitstream import parse_stream
+
+        return parse_stream(open(bit, "rb").read())
+    return load_trace(trace_path(name))
+
+
+@pytest.mark.parametrize("name", STREAMS + ["cif_hdbi"])
+def test_ring_sized_from_stream(name, streams):
+    """A ring of ring_slots(frames) slots (decode-order reach + 1) decodes the
+    stream bit-exactly; one slot fewer evicts a reference some frame still
+    needs, and the decoder reports it (THOR_ERR_REF) instead of predicting
+    from stale pixels."""
+    from thor_amd.decoder import GpuDecoder, ring_slots
+
+    meta = streams[name]
+    seq, frames = _parsed(name)
+    n = ring_slots(frames)
+    dec = GpuDecoder(seq, slots=n)
+    try:
+        for fr in frames:
+            dec.decode(dec.upload(fr))
+            assert dec.lib.thor_dec_sync(dec.h) == 0, (name, fr.decode_order)
+            assert _md5(dec.read_i420(fr.frame_num)) == meta["stage_md5"][fr.decode_order]["final"], (
+                name, fr.decode_order, n)
+    finally:
+        dec.close()
+    if n <= 2:
+        return
+    dec = GpuDecoder(seq, slots=n - 1)
+    try:
+        rcs = []
+        for fr in frames:
+            try:  # an evicted interpolation source is caught on the host, at enqueue
+                dec.decode(dec.upload(fr))
+            except RuntimeError as e:
+                assert "status -4" in str(e), e
+                rcs.append(-4)
+                break
+            rcs.append(dec.lib.thor_dec_sync(dec.h))
+        assert -4 in rcs, (name, n, rcs)
+    finally:
+        dec.close()

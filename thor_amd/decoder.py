@@ -60,8 +60,43 @@ class DeviceBuffer:
             self.ptr = None
 
 
+MAX_SLOTS = 34  # MAX_REF_FRAMES (33, common/global.h:67) references + the frame being decoded
+
+
+def ring_slots(frames, hold: int = 0) -> int:
+    """Reference-ring slots a stream needs: 1 + the longest decode-order
+    distance from a frame to a picture it predicts from (its blocks' ref0 /
+    ref1 and the interpolated reference's two sources), or `hold` if more of
+    the most recently decoded frames must stay readable.  The sequence header
+    cannot bound this: it carries max_num_ref (dec/maindec.c:137) but a
+    reference index reaches up to 32 pictures back (ref_array, 6 bits,
+    dec/decode_frame.c:68; HDB16 uses 2 * sub_gop - 1 = 31 with max_num_ref 2,
+    enc/mainenc.c:302), so the ring is sized from the parsed frame headers.
+    The ring evicts the slot decoded longest ago (thor_dec_create)."""
+    order = {}
+    reach = 0
+    for d, fr in enumerate(frames):
+        refs = set()
+        b = fr.blocks
+        if len(b):
+            refs.update(int(r) for r in np.unique(np.concatenate([b["ref0"], b["ref1"]])) if r >= 0)
+        if getattr(fr, "interp_ratio", 0):
+            refs.update(r for r in fr.interp_refs if r >= 0)
+        for r in refs:
+            if r not in order:
+                raise ValueError("frame %d references frame %d, not decoded before it" % (fr.frame_num, r))
+            reach = max(reach, d - order[r])
+        order[fr.frame_num] = d
+    n = max(reach + 1, hold, 2)
+    if n > MAX_SLOTS:
+        raise ValueError("stream reaches %d frames back, the ring holds at most %d" % (reach, MAX_SLOTS - 1))
+    return n
+
+
 class GpuDecoder:
-    def __init__(self, seq, device: int = 0, slots: int = 34):
+    def __init__(self, seq, device: int = 0, slots: int = MAX_SLOTS):
+        """slots: reference-ring size; ring_slots(frames) sizes it to a parsed
+        stream (the default holds any stream the reference can produce)."""
         self.lib = L.load()
         if self.lib.thor_device_count() <= 0:
             raise RuntimeError("no HIP device visible: the GPU decode path has no CPU fallback")
