@@ -699,7 +699,6 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
 TE_FN uint32_t te_search_inter(const TeFrame &F, TeSB &sb, int r, const uint8_t *org, int os,
                                const TeBlockInfo &bi, TeMv mvc, TeMv mvp, TeMv *mv_arr, int part, int sign,
                                int enable_bipred) {
-  const TeScratch S = te_here();
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, rs = F.rsy;
   const uint8_t *ref_y = F.refy[r] + ypos * rs + xpos;
   TeMv mv, mvp2 = mvp;
@@ -948,7 +947,6 @@ TE_FN uint32_t te_bi_joint_sad(const TeFrame &F, const uint8_t *org, const uint8
 TE_NOINL void te_search_bipred_joint(const TeFrame &F_, TeSB &sb_, const TeBlockInfo &bi_,
                                      const TeMv *mv_center, TeMv mvp, int *ref_idx0, int *ref_idx1, TeMv *mv_out) {
   const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
   const TeBlockInfo &bi = *te_lds(&bi_);
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos;
@@ -1474,7 +1472,6 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeSB &sb_, int ypos, int x
 // search when max_delta_qp is set (trials leave their candidates behind, as
 // there).  Returns the SB's bit count in sb.bits.
 TE_FN void te_encode_sb(const TeFrame &F, TeSB &sb, int k, int l) {
-  const TeScratch S = te_here();
   TE_P(TP_SB);
   const int ypos = k * 64, xpos = l * 64;
   for (int r = 0; r < F.num_ref; r++) {

@@ -109,10 +109,12 @@ __device__ __forceinline__ uint32_t pack_lo16(int lo, int hi) {  // (lo & 0xffff
   return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
 }
 // packed int16 pairs of a 6-tap word (t0,t1), (t2,t3), (t4,t5)
-__device__ __forceinline__ void tap_pairs6(int w0, int w1, int &p01, int &p23, int &p45) {
-  p01 = (tap8(w0, 0) & 0xffff) | (tap8(w0, 1) << 16);
-  p23 = (tap8(w0, 2) & 0xffff) | (tap8(w0, 3) << 16);
-  p45 = (tap8(w1, 0) & 0xffff) | (tap8(w1, 1) << 16);
+// (the fast path scales them: m = 16, |tap| x 16 <= 944 stays an int16)
+__device__ __forceinline__ int tap_pair(int a, int b, int m) { return ((a * m) & 0xffff) | ((b * m) << 16); }
+__device__ __forceinline__ void tap_pairs6(int w0, int w1, int &p01, int &p23, int &p45, int m = 1) {
+  p01 = tap_pair(tap8(w0, 0), tap8(w0, 1), m);
+  p23 = tap_pair(tap8(w0, 2), tap8(w0, 3), m);
+  p45 = tap_pair(tap8(w1, 0), tap8(w1, 1), m);
 }
 
 // Four horizontal 6-tap sums from the 12 bytes d0..d2 (window bytes are stored ^ 0x80),
@@ -141,6 +143,20 @@ __device__ __forceinline__ uint32_t sat_u8x2(int a, int b) {
 }
 __device__ __forceinline__ uint32_t pack4_u8(int a, int b, int c, int d) {
   return __builtin_amdgcn_perm(sat_u8x2(c, d), sat_u8x2(a, b), 0x05040100u);
+}
+// clip255(s >> 16) of four sums packed as bytes: the high halves of (a, b)
+// and (c, d) as int16 pairs (one byte permute each), then v_sat_pk_u8_i16.
+// The fast path scales its vertical taps by 16 so that the >> 12 of the 2-D
+// filters is this >> 16 (5 instructions per 4 px instead of 9).
+__device__ __forceinline__ uint32_t sat_u8x2_pk(uint32_t p) {
+  uint32_t r;
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(p));
+  return r;
+}
+__device__ __forceinline__ uint32_t pack4_hi16_u8(int a, int b, int c, int d) {
+  const uint32_t ab = __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x07060302u);
+  const uint32_t cd = __builtin_amdgcn_perm((uint32_t)d, (uint32_t)c, 0x07060302u);
+  return __builtin_amdgcn_perm(sat_u8x2_pk(cd), sat_u8x2_pk(ab), 0x05040100u);
 }
 __device__ __forceinline__ uint32_t avg_bytes(uint32_t a, uint32_t b) {  // (p0 + p1) >> 1 per byte
   return (a & b) + (((a ^ b) >> 1) & 0x7f7f7f7fu);
@@ -387,8 +403,12 @@ __device__ __forceinline__ Key make_key(int mv, int slot) {
 // or (past the ring) zeros through the buffer descriptor -- never out of bounds.
 struct WinLoad {
   uint4 v[WIN_LOADS];
-  int dst[WIN_LOADS];
 };
+// Chunk q (16 bytes) of the window is LDS bytes [16q, 16q + 16): RefWin is
+// contiguous, luma rows of WL_P = 6 chunks, then U and V rows of WC_P = 4.
+// Its ring offset is its row's start + 16 x its column, i.e. 16q plus
+// (row x (stride - pitch)): per load a reciprocal multiply (q / 6) or a shift
+// and one multiply-add; loads 0-2 are all luma, 4-5 all chroma.
 __device__ __forceinline__ void win_issue(WinLoad &W, const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, const Key &K,
                                           int x0, int y0) {
   const int lane = threadIdx.x;
@@ -396,32 +416,32 @@ __device__ __forceinline__ void win_issue(WinLoad &W, const FrameCtx &f, __amdgp
   const int cx0 = x0 >> 1, cy0 = y0 >> 1;
   const int ly = (int)(sbase + f.offy + (long long)(y0 - 2 + K.dy) * f.sy + ((x0 - 2 + K.dx) & ~15));
   const int cu = (int)(sbase + f.offu + (long long)(cy0 - 1 + K.cdy) * f.sc + ((cx0 - 1 + K.cdx) & ~15));
-  const int uvd = (int)(f.offv - f.offu);
+  const int uvd = (int)(f.offv - f.offu) - WC_R * WC_P;  // V rows follow U's in the window
+  const int syd = f.sy - WL_P, scd = f.sc - WC_P;
 #pragma unroll
   for (int i = 0; i < WIN_LOADS; i++) {
     const int q = lane + 64 * i;
-    int off, d;
-    if (q < WL_CH) {
-      const int r = q / (WL_P / 16), c = q - r * (WL_P / 16);
-      off = ly + r * f.sy + 16 * c;
-      d = r * WL_P + 16 * c;
-    } else {
-      const int q2 = q - WL_CH, pl = q2 >= WC_CH, q3 = q2 - pl * WC_CH;
-      const int r = q3 / (WC_P / 16), c = q3 - r * (WC_P / 16);
-      off = cu + pl * uvd + r * f.sc + 16 * c;
-      d = WL_R * WL_P + pl * (WC_R * WC_P) + r * WC_P + 16 * c;
+    int offl = 0, offc = 0;
+    if (64 * i < WL_CH) offl = ly + 16 * q + ((q * 171) >> 10) * syd;  // q / 6, exact for q < 256
+    if (64 * i + 63 >= WL_CH) {
+      const int q2 = q - WL_CH;  // chroma chunk: U 0..75, V 76..151
+      const bool pv = q2 >= WC_CH;
+      const int q3 = pv ? q2 - WC_CH : q2;
+      offc = cu + 16 * q2 + (pv ? uvd : 0) + (q3 >> 2) * scd;
     }
-    W.dst[i] = q < WL_CH + 2 * WC_CH ? d : -1;
+    const int off = 64 * i + 63 < WL_CH ? offl : (64 * i >= WL_CH ? offc : (q < WL_CH ? offl : offc));
     W.v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ring, off, 0, 0));
   }
 }
 __device__ __forceinline__ void win_commit(const WinLoad &W, RefWin &w) {
+  static_assert(sizeof(RefWin) == 16 * (WL_CH + 2 * WC_CH), "window chunks are contiguous");
+  const int lane = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < WIN_LOADS; i++)
-    if (W.dst[i] >= 0) {
+    if (64 * i + 63 < WL_CH + 2 * WC_CH || lane + 64 * i < WL_CH + 2 * WC_CH) {
       uint4 v = W.v[i];
       v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
-      *(uint4 *)(w.y + W.dst[i]) = v;
+      *(uint4 *)(w.y + 16 * (lane + 64 * i)) = v;
     }
 }
 
@@ -527,11 +547,16 @@ __device__ __forceinline__ void shifted_taps(unsigned long long t48, int o, int 
 // byte offset of column -2 in it (uniform).  Horizontal: three dot4 per pixel
 // on the unshifted dwords with per-pixel shifted tap words (no v_alignbyte);
 // vertical: three dot2 per pixel on (H'[r], H'[r+1]) pairs.
-__device__ __forceinline__ void luma8_fast(const uint8_t *base, int sh, unsigned long long th48, int v01, int v23,
+// SH (the uniform byte offset, a template argument: the dispatcher switches on
+// it) tells which tap words are zero: pixel j's taps cover window bytes
+// SH + j .. SH + j + 5, so d0 is read only for SH + j <= 3 and d2 only for
+// SH + j >= 3 -- 9 dot4 per row of 4 px instead of 12.
+template <int SH>
+__device__ __forceinline__ void luma8_fast(const uint8_t *base, unsigned long long th48, int v01, int v23,
                                            int v45, uint32_t out[8], bool acc, bool k0 = true, bool k1 = true) {
   int T[4][3];
 #pragma unroll
-  for (int j = 0; j < 4; j++) shifted_taps(th48, sh + j, T[j][0], T[j][1], T[j][2]);
+  for (int j = 0; j < 4; j++) shifted_taps(th48, SH + j, T[j][0], T[j][1], T[j][2]);
   const int hb = HB;  // in a VGPR: the chains' seed (one scalar operand per instruction)
   int hp[4];
   uint32_t pa[6][4];
@@ -540,7 +565,13 @@ __device__ __forceinline__ void luma8_fast(const uint8_t *base, int sh, unsigned
     const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
     int hc[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) hc[j] = vdot4(d0, T[j][0], vdot4(d1, T[j][1], vdot4(d2, T[j][2], hb)));
+    for (int j = 0; j < 4; j++) {
+      int a = hb;
+      if (SH + j >= 3) a = vdot4(d2, T[j][2], a);
+      a = vdot4(d1, T[j][1], a);
+      if (SH + j <= 3) a = vdot4(d0, T[j][0], a);
+      hc[j] = a;
+    }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (r > -2) pa[(r + 5) % 6][j] = pack_lo16(hp[j], hc[j]);
@@ -555,9 +586,8 @@ __device__ __forceinline__ void luma8_fast(const uint8_t *base, int sh, unsigned
     int v[4];
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      v[j] = vdot2(pa[(i + 2 + 6) % 6][j], v45, vdot2(pa[(i + 6) % 6][j], v23, vdot2_0(pa[(i - 2 + 6) % 6][j], v01))) >>
-             12;
-    const uint32_t o = pack4_u8(v[0], v[1], v[2], v[3]);
+      v[j] = vdot2(pa[(i + 2 + 6) % 6][j], v45, vdot2(pa[(i + 6) % 6][j], v23, vdot2_0(pa[(i - 2 + 6) % 6][j], v01)));
+    const uint32_t o = pack4_hi16_u8(v[0], v[1], v[2], v[3]);  // vertical taps x 16
     if (i < 4 ? k0 : k1) out[i] = acc ? avg_bytes(out[i], o) : o;  // k0 / k1: the segment's key matches
   }
 }
@@ -604,10 +634,10 @@ __device__ __forceinline__ void chroma4_fast(const uint8_t *bu, const uint8_t *b
     int au[2], av[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
-      au[j] = vdot2(pu[(i + 1) % 4][j], v23, vdot2_0(pu[(i + 3) % 4][j], v01)) >> 12;
-      av[j] = vdot2(pv[(i + 1) % 4][j], v23, vdot2_0(pv[(i + 3) % 4][j], v01)) >> 12;
+      au[j] = vdot2(pu[(i + 1) % 4][j], v23, vdot2_0(pu[(i + 3) % 4][j], v01));
+      av[j] = vdot2(pv[(i + 1) % 4][j], v23, vdot2_0(pv[(i + 3) % 4][j], v01));
     }
-    const uint32_t uv = pack4_u8(au[0], au[1], av[0], av[1]);
+    const uint32_t uv = pack4_hi16_u8(au[0], au[1], av[0], av[1]);  // vertical taps x 16
     if (i < 2 ? k0 : k1) out[i] = acc ? avg_bytes(out[i], uv) : uv;
   }
 }
@@ -633,15 +663,21 @@ __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bi
     }
   } else {
     int v01, v23, v45;
-    tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45);
+    tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45, 16);
     const unsigned long long th48 = (unsigned long long)(uint32_t)g_taps.luma[bipred][K.fx][0] |
                                     ((unsigned long long)(uint32_t)(g_taps.luma[bipred][K.fx][1] & 0xffff) << 32);
-    luma8_fast(w.y + 8 * gr * WL_P + (lwb & ~3), lwb & 3, th48, v01, v23, v45, ty, acc, k0, k1);
+    const uint8_t *lb = w.y + 8 * gr * WL_P + (lwb & ~3);
+    switch (lwb & 3) {  // uniform
+      case 0: luma8_fast<0>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
+      case 1: luma8_fast<1>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
+      case 2: luma8_fast<2>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
+      default: luma8_fast<3>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
+    }
   }
   const int cvt = g_taps.chroma[K.cfy];
   chroma4_fast(w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3), cwb & 3,
-               (unsigned long long)(uint32_t)g_taps.chroma[K.cfx], (tap8(cvt, 0) & 0xffff) | (tap8(cvt, 1) << 16),
-               (tap8(cvt, 2) & 0xffff) | (tap8(cvt, 3) << 16), tc, acc, k0, k1);
+               (unsigned long long)(uint32_t)g_taps.chroma[K.cfx], tap_pair(tap8(cvt, 0), tap8(cvt, 1), 16),
+               tap_pair(tap8(cvt, 2), tap8(cvt, 3), 16), tc, acc, k0, k1);  // vertical taps x 16
   (void)l;
   (void)c;
 }
@@ -750,29 +786,31 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
       const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
       const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
       const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
-      // a half at the frame's bottom / right edge stores only its pixels inside
-      // (W, H multiples of 8: a lane's 4 luma / 2 chroma columns are all in or all out)
+      // Stores through a descriptor over the current slot: one lane offset per
+      // plane, the row in the scalar offset.  A half at the frame's bottom /
+      // right edge stores its rows / columns past the edge into the slot's
+      // padding, which k_pad rewrites (W, H multiples of 8; padding >= 48).
+      const __amdgpu_buffer_rsrc_t cur =
+          __builtin_amdgcn_make_buffer_rsrc((void *)(f.cy - f.offy), 0, (int)f.slot_bytes, 0x00020000);
       const bool xin = x < f.W;
+      const int oy = (int)f.offy + yb * f.sy + x, ou = (int)f.offu + ycb * f.sc + xc, uvd = (int)(f.offv - f.offu);
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        const int y = yb + i;
-        if (!xin || y >= f.H) continue;
         uint32_t v = ly[i];
-        if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
-        *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
-        if (i == 7 && h == 1 && gr == 3)  // SB row 63: the edge row k_intra's next SB row reads
+        if ((meta & CELL_RES(0)) && xin && yb + i < f.H) v = add_res4(v, rY + (long long)(yb + i) * f.W + x);
+        __builtin_amdgcn_raw_buffer_store_b32(v, cur, oy, i * f.sy, 0);
+        if (i == 7 && h == 1 && gr == 3 && yb + i < f.H)  // SB row 63: the edge row k_intra's next SB row reads
           *(uint32_t *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + x) = v;
       }
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int y = ycb + i;
-        if (!xin || y >= (f.H >> 1)) continue;
         uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
-        if (meta & CELL_RES(1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
-        if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
-        *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
-        *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
-        if (i == 3 && h == 1 && gr == 3) {  // chroma SB row 31
+        if ((meta & CELL_RES(1)) && xin && y < (f.H >> 1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
+        if ((meta & CELL_RES(2)) && xin && y < (f.H >> 1)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)vu, cur, ou, i * f.sc, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)vv, cur, ou + uvd, i * f.sc, 0);
+        if (i == 3 && h == 1 && gr == 3 && y < (f.H >> 1)) {  // chroma SB row 31
           uint8_t *e = f.edge + (long long)f.nsbrows * f.ewy + (long long)sby * f.ewc + EDGE_MARGIN + xc;
           *(uint16_t *)e = (uint16_t)vu;
           *(uint16_t *)(e + (long long)f.nsbrows * f.ewc) = (uint16_t)vv;
