@@ -13,6 +13,12 @@ SOURCES = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result", "-Wno-bitwise-instead-of-logical"]
+# Integer dot products as the three-operand VOP3P forms (v_dot4_i32_i8, v_dot2_i32_i16):
+# with the accumulate-in-place VOP2 forms (v_dot4c / v_dot2c) available hipcc seeds every
+# chain with a v_mov (k_recon: ~3 700 of them).  The host pass ignores these (it warns).
+FLAGS += ["-Xclang", "-target-feature", "-Xclang", "-dot6-insts", "-Xclang", "-target-feature", "-Xclang", "-dot4-insts"]
+# k_recon: 5 waves per SIMD (96 VGPRs; a few spills on the per-cell path only)
+FLAGS += ["-DRECON_WPE=5"]
 
 
 def _stale() -> bool:

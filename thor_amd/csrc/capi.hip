@@ -15,7 +15,7 @@
 
 // kernels (intra.hip, inter.hip, loopfilter.hip): the frame batch by value, first argument
 __global__ void k_frame_prep(const FrameBatch);
-__global__ void k_recon(const FrameBatch, unsigned long long *);
+__global__ void k_recon(const FrameBatch, int, unsigned long long *);
 __global__ void k_intra(const FrameBatch, unsigned long long *, int);
 __global__ void k_deblock_v(const FrameBatch, int, int);
 __global__ void k_deblock_h(const FrameBatch, int, int);
@@ -157,15 +157,21 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->seq = *seq;
   d->device = device;
   int W = seq->width, H = seq->height;
-  d->sy = (W + 2 * THOR_PAD_Y + 15) & ~15;       // common/common_frame.c:331
-  d->sc = (W / 2 + 2 * THOR_PAD_C + 15) & ~15;   // :332
-  long long ybytes = (long long)(H + 2 * THOR_PAD_Y) * d->sy;
-  long long cbytes = (long long)(H / 2 + 2 * THOR_PAD_C) * d->sc;
+  // The padding of create_yuv_frame (common/common_frame.c:324-351: 96 luma / 48
+  // chroma on every side), laid out so that every row's pixel 0 sits on a 128-byte
+  // line boundary: strides are multiples of 128 and each plane starts 32 / 80
+  // bytes into its 256-aligned block.  k_recon's 128-pixel units then store whole
+  // luma lines (inter.hip).
+  d->sy = (W + 2 * THOR_PAD_Y + 127) & ~127;
+  d->sc = (W / 2 + 2 * THOR_PAD_C + 127) & ~127;
+  const int ylead = (128 - THOR_PAD_Y % 128) % 128, clead = (128 - THOR_PAD_C % 128) % 128;
+  long long ybytes = ylead + (long long)(H + 2 * THOR_PAD_Y) * d->sy;
+  long long cbytes = clead + (long long)(H / 2 + 2 * THOR_PAD_C) * d->sc;
   ybytes = (ybytes + 255) & ~255LL;
   cbytes = (cbytes + 255) & ~255LL;
-  d->offy = (long long)THOR_PAD_Y * d->sy + THOR_PAD_Y;
-  d->offu = ybytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
-  d->offv = ybytes + cbytes + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
+  d->offy = ylead + (long long)THOR_PAD_Y * d->sy + THOR_PAD_Y;
+  d->offu = ybytes + clead + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
+  d->offv = ybytes + cbytes + clead + (long long)THOR_PAD_C * d->sc + THOR_PAD_C;
   d->slot_bytes = ybytes + 2 * cbytes + 256;
   if (d->slot_bytes * (num_slots + (seq->interp_ref ? 1 : 0)) >= (1LL << 31)) {  // k_recon addresses the ring with 32-bit buffer offsets
     create_fail(THOR_ERR_ARG, (size_t)(d->slot_bytes * (num_slots + (seq->interp_ref ? 1 : 0))),
@@ -217,9 +223,9 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->ewy = (W + 2 * EDGE_MARGIN + 15) & ~15;
   d->ewc = (W / 2 + 2 * EDGE_MARGIN + 15) & ~15;
   ok = ok && dev_alloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc), "thor_dec_create: edge rows");
-  const size_t nhalf = 2 * (size_t)((W + 63) / 64) * ((H + 63) / 64);
-  ok = ok && dev_alloc(&d->hplan, nhalf * sizeof(uint4), "thor_dec_create: half-SB plans");
-  ok = ok && hipMemset(d->hplan, 0, nhalf * sizeof(uint4)) == hipSuccess;  // tag 0: no plan (gen starts at 1)
+  const size_t nplan = hplan_entries(W, H);  // plans, then the slow list (common.h)
+  ok = ok && dev_alloc(&d->hplan, nplan * sizeof(uint4), "thor_dec_create: half-SB plans");
+  ok = ok && hipMemset(d->hplan, 0, nplan * sizeof(uint4)) == hipSuccess;  // tag 0: no plan (gen starts at 1)
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
   for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&d->xev[i], hipEventDisableTiming) == hipSuccess;
   {  // k_intra stages a row's CU words in LDS (up to (W/8) x 8 CUs)
@@ -520,7 +526,6 @@ static int batch_interp(thor_dec_t *const *ds, const Batch &b) {
 static int batch_phase_a(thor_dec *lead, const Batch &b) {
   const int W = lead->seq.width, H = lead->seq.height, n = b.n;
   hipStream_t st = lead->stream;
-  const int nsb = ((W + 63) / 64) * ((H + 63) / 64);
   {
     // side info + residuals of every coded transform block + intra chain setup
     StageMark m(lead, ST_PREP);
@@ -529,7 +534,10 @@ static int batch_phase_a(thor_dec *lead, const Batch &b) {
   }
   {
     StageMark m(lead, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
-    k_recon<<<dim3(8 * ((2 * nsb + 7) / 8), n), 64, recon_lds_pad(), st>>>(b.fb, lead->dbg_recon);
+    // one flat grid: every frame's slow-list slots first (frame-interleaved), then
+    // each frame's halves in XCD-major order (inter.hip)
+    k_recon<<<dim3(n * (SLOW_CAP + 8 * ((unit_count(W, H) + 7) / 8)), 1), 64, recon_lds_pad(), st>>>(b.fb, n,
+                                                                                               lead->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   return THOR_OK;

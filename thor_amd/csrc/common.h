@@ -117,8 +117,34 @@ struct FrameCtx {
 struct FrameBatch {
   FrameCtx f[THOR_MAX_BATCH];
 };
+static_assert(sizeof(FrameBatch) + 16 <= 4096, "the batch travels in the kernarg segment");
 #define FRAME_BATCH_CTX() ((const FrameCtx *)__builtin_amdgcn_kernarg_segment_ptr())
 #define EDGE_MARGIN 32
+
+// k_recon's work unit: 128 x 16 luma pixels (a quarter-SB row of two
+// horizontally adjacent SBs) + 2 x 64 x 8 chroma; unit u = slice row x pairs +
+// pair, slice row = 4 x SB row + quarter (inter.hip).
+__host__ __device__ __forceinline__ int half_count(int W, int H) { return 2 * ((W + 63) >> 6) * ((H + 63) >> 6); }
+__host__ __device__ __forceinline__ int unit_pairs(int W) { return (((W + 63) >> 6) + 1) >> 1; }
+__host__ __device__ __forceinline__ int unit_count(int W, int H) { return unit_pairs(W) * 4 * ((H + 63) >> 6); }
+
+// The slow list of a frame: the units with several (MV, reference) keys in a
+// half (k_frame_prep appends them; k_recon dispatches them ahead of the planned
+// units so their long per-cell path overlaps the rest of the launch instead of
+// forming its tail).  It lives behind the plans in the hplan allocation (uint4s):
+//   [0, nh)                 per-half plans, .w == gen: planned (FrameCtx::hplan)
+//   [nh]                    u64 {count, gen} (count valid iff the high word == gen)
+//   [nh + 1, +SLOW_CAP/4)   SLOW_CAP list entries (unit indices)
+//   then                    u64 per unit {list position, gen} (claimed iff the high word == gen)
+// A slow unit at list position >= SLOW_CAP is reconstructed by its own
+// (planned-order) workgroup.
+#define SLOW_CAP 128
+__host__ __device__ __forceinline__ size_t hplan_utag_off(int W, int H) {
+  return (size_t)half_count(W, H) + 1 + SLOW_CAP / 4;
+}
+__host__ __device__ __forceinline__ size_t hplan_entries(int W, int H) {
+  return hplan_utag_off(W, H) + (size_t)(unit_count(W, H) + 1) / 2;
+}
 
 // Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits
 // (replaces the 44-byte deblock_data_t, common/types.h:127-135):

@@ -38,28 +38,38 @@
 
 #include "common.h"
 
+#ifndef RECON_PROBE
+#define RECON_PROBE 0  // timing-only probe builds (tools/gpu_var.sh); 0 in the product
+#endif
+
 #define SB_CELLS 256
 
-// reference window for one (mv, slot) key and one half SB
-#define WL_P 96  // luma pitch: 64 + 5 taps + 15 alignment, rounded to 16 B
-#define WL_R 37  // 32 rows + 5
-#define WC_P 64  // chroma pitch: 32 + 3 + 15 -> 64
-#define WC_R 19  // 16 rows + 3
-#define WL_CH (WL_R * WL_P / 16)  // 16-byte chunks: 222
-#define WC_CH (WC_R * WC_P / 16)  // 76 per plane
-#define WIN_LOADS 6               // ceil((222 + 2 * 76) / 64)
+// The work unit (common.h): 128 x 16 luma + 2 x 64 x 8 chroma, two SBs side by
+// side.  Lane geometry: LCC = 4-px luma / 2-px chroma column (0..31), LGR = row
+// group (8 luma / 4 chroma rows, 0..1).
+#define LCC(lane) ((lane) & 31)
+#define LGR(lane) ((lane) >> 5)
+
+// reference window for one (mv, slot) key and one unit
+#define WL_P 160  // luma pitch: 128 + 5 taps + 15 alignment -> 160 B (10 chunks)
+#define WL_R 21   // 16 rows + 5
+#define WC_P 96   // chroma pitch: 64 + 3 + 15 -> 96 B (6 chunks)
+#define WC_R 11   // 8 rows + 3
+#define WL_CH (WL_R * WL_P / 16)  // 16-byte chunks: 210
+#define WC_CH (WC_R * WC_P / 16)  // 66 per plane
+#define WIN_LOADS 6               // ceil((210 + 2 * 66) / 64)
 struct RefWin {
   uint8_t y[WL_R * WL_P];
   uint8_t u[WC_R * WC_P];
   uint8_t v[WC_R * WC_P];
 };
 
-#define HALF_CELLS 128  // 8 cell rows x 16 cells: one half SB
+#define UNIT_CELLS 128  // 4 cell rows x 32 cells
 struct ReconLds {
   RefWin win;
-  int mv0[HALF_CELLS];        // per 4x4 cell: (mvx, mvy) int16 pair, sign applied
-  int mv1[HALF_CELLS];
-  unsigned meta[HALF_CELLS];  // slot0 | slot1 << 8 | ACT | BI | RES(c)
+  int mv0[UNIT_CELLS];        // per 4x4 cell: (mvx, mvy) int16 pair, sign applied
+  int mv1[UNIT_CELLS];
+  unsigned meta[UNIT_CELLS];  // slot0 | slot1 << 8 | ACT | BI | RES(c)
   int8_t lut[128];            // display frame number & 127 -> ring slot
 };
 
@@ -405,10 +415,10 @@ struct WinLoad {
   uint4 v[WIN_LOADS];
 };
 // Chunk q (16 bytes) of the window is LDS bytes [16q, 16q + 16): RefWin is
-// contiguous, luma rows of WL_P = 6 chunks, then U and V rows of WC_P = 4.
+// contiguous, luma rows of WL_P = 10 chunks, then U and V rows of WC_P = 6.
 // Its ring offset is its row's start + 16 x its column, i.e. 16q plus
-// (row x (stride - pitch)): per load a reciprocal multiply (q / 6) or a shift
-// and one multiply-add; loads 0-2 are all luma, 4-5 all chroma.
+// (row x (stride - pitch)): per load a reciprocal multiply for the row and one
+// multiply-add; loads 0-2 are all luma, 4-5 all chroma.
 __device__ __forceinline__ void win_issue(WinLoad &W, const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, const Key &K,
                                           int x0, int y0) {
   const int lane = threadIdx.x;
@@ -422,14 +432,22 @@ __device__ __forceinline__ void win_issue(WinLoad &W, const FrameCtx &f, __amdgp
   for (int i = 0; i < WIN_LOADS; i++) {
     const int q = lane + 64 * i;
     int offl = 0, offc = 0;
-    if (64 * i < WL_CH) offl = ly + 16 * q + ((q * 171) >> 10) * syd;  // q / 6, exact for q < 256
+    if (64 * i < WL_CH) offl = ly + 16 * q + ((q * 205) >> 11) * syd;  // q / 10, exact for q < 1029
     if (64 * i + 63 >= WL_CH) {
-      const int q2 = q - WL_CH;  // chroma chunk: U 0..75, V 76..151
+      const int q2 = q - WL_CH;  // chroma chunk: U 0..65, V 66..131
       const bool pv = q2 >= WC_CH;
       const int q3 = pv ? q2 - WC_CH : q2;
-      offc = cu + 16 * q2 + (pv ? uvd : 0) + (q3 >> 2) * scd;
+      offc = cu + 16 * q2 + (pv ? uvd : 0) + ((q3 * 171) >> 10) * scd;  // q3 / 6, exact for q3 < 256
     }
-    const int off = 64 * i + 63 < WL_CH ? offl : (64 * i >= WL_CH ? offc : (q < WL_CH ? offl : offc));
+    int off = 64 * i + 63 < WL_CH ? offl : (64 * i >= WL_CH ? offc : (q < WL_CH ? offl : offc));
+#if RECON_PROBE == 1  // timing probe: the same bytes as whole 128-B lines, 8 rows per load (wrong output)
+    off = (int)((ly & ~127) + (q >> 3) * f.sy + (q & 7) * 16);
+#elif RECON_PROBE == 2  // timing probe: no chroma window loads (wrong output)
+    if (64 * i >= WL_CH) continue;
+#elif RECON_PROBE == 4  // timing probe: every wave loads the same 6 KB (wrong output)
+    off = (int)(f.offy + 16 * q);
+#endif
+    if (64 * i + 63 >= WL_CH + 2 * WC_CH && q >= WL_CH + 2 * WC_CH) continue;  // past the window
     W.v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ring, off, 0, 0));
   }
 }
@@ -445,18 +463,18 @@ __device__ __forceinline__ void win_commit(const WinLoad &W, RefWin &w) {
     }
 }
 
-// A pass's items of this lane: segment s (cell row 2gr + s of the half).
+// A pass's items of this lane: segment s (cell row 2 LGR + s of the unit).
 struct Items {
   unsigned pend;
   int mv[2], slot[2];
 };
 __device__ __forceinline__ Items job_items(const ReconLds &L, int pass) {
-  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const int lane = threadIdx.x, cc = LCC(lane), gr = LGR(lane);
   Items it;
   it.pend = 0;
 #pragma unroll
   for (int s = 0; s < 2; s++) {
-    const int cell = (2 * gr + s) * 16 + cc;
+    const int cell = (2 * gr + s) * 32 + cc;
     const unsigned meta = L.meta[cell];
     const bool act = (meta & CELL_ACT) && (pass == 0 || (meta & CELL_BI));
     it.mv[s] = pass ? L.mv1[cell] : L.mv0[cell];
@@ -479,7 +497,7 @@ __device__ __forceinline__ bool first_key(const Items &it, Key &K) {
 // Filter every pending item whose key is K from the staged window; clears them.
 __device__ __forceinline__ void filter_key(const RefWin &w, const Key &K, int bipred, int x0, Items &it, uint32_t ty[8],
                                            uint32_t tc[4], bool acc) {
-  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const int lane = threadIdx.x, cc = LCC(lane), gr = LGR(lane);
   const bool m0 = (it.pend & 1) && it.mv[0] == K.mv && it.slot[0] == K.slot;
   const bool m1 = (it.pend & 2) && it.mv[1] == K.mv && it.slot[1] == K.slot;
   const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
@@ -646,7 +664,7 @@ __device__ __forceinline__ void chroma4_fast(const uint8_t *bu, const uint8_t *b
 // into the prediction registers (no per-segment key match).
 __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bipred, int x0, uint32_t ty[8],
                                            uint32_t tc[4], bool acc, bool k0 = true, bool k1 = true) {
-  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const int lane = threadIdx.x, cc = LCC(lane), gr = LGR(lane);
   const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
   const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
   const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
@@ -686,7 +704,7 @@ __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bi
 // per-lane keys (one pass, no per-key staging round trips).
 __device__ __forceinline__ void filter_direct(const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, int bipred, int x0,
                                               int y0, Items &it, uint32_t ty[8], uint32_t tc[4], bool acc) {
-  const int lane = threadIdx.x, cc = lane & 15, gr = lane >> 4;
+  const int lane = threadIdx.x, cc = LCC(lane), gr = LGR(lane);
   const Key K0 = make_key(it.mv[0], it.slot[0]), K1 = make_key(it.mv[1], it.slot[1]);
   const bool m0 = it.pend & 1, m1 = (it.pend >> 1) & 1;
   const bool same = it.mv[0] == it.mv[1] && it.slot[0] == it.slot[1];
@@ -721,16 +739,61 @@ __device__ __forceinline__ uint32_t add_res2(uint32_t p, const int16_t *__restri
          put_byte(clip255((int)((p >> 8) & 255) + (int)(int16_t)(a >> 16)), 1);
 }
 
-__global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned long long *__restrict__ dbg) {
+// Stage key K's window and filter it into (ty, tc): every lane filters, lanes
+// with `mine` keep the result (bi-pred pass 1: truncating average with pass 0).
+__device__ __forceinline__ void plan_pass(ReconLds &L, const FrameCtx &f, __amdgpu_buffer_rsrc_t ring, const Key &K,
+                                          int x0, int y0, uint32_t ty[8], uint32_t tc[4], bool acc, bool mine) {
+  WinLoad W;
+  win_issue(W, f, ring, K, x0, y0);
+  wave_lds_sync();  // the previous pass's reads of the window are done
+  win_commit(W, L.win);
+  wave_lds_sync();
+  filter_all(L.win, K, f.bipred, x0, ty, tc, acc, mine, mine);
+}
+
+#ifndef RECON_WPE
+#define RECON_WPE 1
+#endif
+__global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, int nfr, unsigned long long *__restrict__ dbg) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ ReconLds L;
-  const FrameCtx &f = F[blockIdx.y];
-  if (f.nblocks <= 0) return;
-  if (blockIdx.y) dbg = nullptr;
-  int16_t *__restrict__ resid = f.resid;
   const int lane = threadIdx.x;
-  // debug only (null in the product path): s_memrealtime stamps, 8 u64 per wave
-  unsigned long long *stamp = dbg ? dbg + blockIdx.x * 8 : nullptr;
+  // Flat grid (capi.hip): blocks [0, nfr x SLOW_CAP) take the frames' slow-list
+  // entries (frame-interleaved, so every frame's multi-key units start first);
+  // then each frame's NU blocks walk its units in XCD-major order --
+  // workgroup b runs on XCD b % 8 (round-robin dispatch), so each XCD gets a
+  // contiguous band of slice rows and vertical neighbours share their reference
+  // rows in that XCD's L2.  Speed only, never correctness.
+  const int W0 = F[0].W, H0 = F[0].H;
+  const int sbw = (W0 + 63) >> 6, np = unit_pairs(W0), nu = unit_count(W0, H0), NU = 8 * ((nu + 7) >> 3);
+  const int nh = half_count(W0, H0);
+  const int nslow = nfr * SLOW_CAP;
+  int fi, u;
+  bool listed = false;
+  if ((int)blockIdx.x < nslow) {
+    fi = blockIdx.x % nfr;
+    const int idx = blockIdx.x / nfr;
+    const FrameCtx &f = F[fi];
+    if (!f.hplan || f.nblocks <= 0) return;
+    const unsigned long long c = *(const unsigned long long *)(f.hplan + nh);
+    if ((unsigned)(c >> 32) != (unsigned)f.gen || idx >= (int)(unsigned)c) return;
+    u = (int)((const unsigned *)(f.hplan + nh + 1))[idx];
+    listed = true;
+  } else {
+    const int b = blockIdx.x - nslow;
+    fi = b / NU;
+    const int loc = b - fi * NU, per = NU >> 3;
+    u = (loc & 7) * per + (loc >> 3);
+    if (u >= nu) return;
+  }
+  u = __builtin_amdgcn_readfirstlane(u);  // uniform (the scalar loads below need it in SGPRs)
+  fi = __builtin_amdgcn_readfirstlane(fi);
+  const FrameCtx &f = F[fi];
+  if (f.nblocks <= 0) return;
+  if (fi) dbg = nullptr;
+  int16_t *__restrict__ resid = f.resid;
+  // debug only (null in the product path): s_memrealtime stamps, 8 u64 per unit of frame 0
+  unsigned long long *stamp = dbg ? dbg + u * 8 : nullptr;
 #define STAMP(i) \
   if (stamp && lane == 0) stamp[i] = __builtin_amdgcn_s_memrealtime();
   STAMP(0);
@@ -739,82 +802,127 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
     const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
     stamp[7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
   }
-  const int sbw = (f.W + 63) >> 6, sbh = (f.H + 63) >> 6, nh = 2 * sbw * sbh;
-  // XCD-major order of half SBs: workgroup b runs on XCD b % 8 (round-robin
-  // dispatch); each XCD gets a contiguous band.  Speed only, never correctness.
-  const int per = (nh + 7) >> 3;
-  const int hsb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (hsb >= nh) return;
-  const int sb = hsb >> 1, h = hsb & 1;
-  const int sby = sb / sbw, sbx = sb - sby * sbw;
+  const int srow = u / np, pr = u - srow * np;  // slice row (4 per SB row), SB pair
+  const int sby = srow >> 2, qtr = srow & 3, h = qtr >> 1;
   if (sby < f.band0 || sby >= f.band1) return;  // another shard's rows (row-band sharding)
   const int cs = f.W >> 2;
-  const int x0 = sbx * 64, y0 = sby * 64 + 32 * h, cc = lane & 15, gr = lane >> 4;
+  const int x0 = 128 * pr, y0 = 16 * srow, cc = LCC(lane), gr = LGR(lane);
+  const bool bex = 2 * pr + 1 < sbw;  // the pair's right SB exists
+  const bool last = qtr == 3;         // the unit holds SB row 63: the edge rows k_intra reads
 
-  // ---- fast path: the half's plan (k_frame_prep: one 64x64 inter CU, one key
-  // per pass) replaces the per-cell resolution (P0): one
-  // scalar load, then straight to the window staging ----
-  if (f.hplan) {
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 pv;  // a scalar (uniform) load through the constant cache
-    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(pv) : "s"(f.hplan + hsb) : "memory");
-    const uint4 pl = make_uint4(pv.x, pv.y, pv.z, pv.w);
-    if ((int)pl.w == f.gen) {
+  // ---- fast path: both halves planned (k_frame_prep: one 64x64 inter CU, one
+  // key per pass) -- no per-cell resolution (P0): scalar loads, then straight
+  // to the window staging ----
+  if (f.hplan && !listed) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u32x16 __attribute__((ext_vector_type(16)));
+    u32x2 tg;  // the unit's slow-list tag {position, gen}
+    u32x16 pv;  // plans of halves hsb and hsb + 2 (scalar, uniform loads through the constant cache)
+    const int hsb = 2 * (sby * sbw + 2 * pr) + h;
+    const unsigned long long *utag = (const unsigned long long *)(f.hplan + hplan_utag_off(W0, H0)) + u;
+    asm volatile("s_load_dwordx2 %0, %2, 0x0\n\ts_load_dwordx16 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(tg), "=&s"(pv)  // early clobber: the first load must not land in the second's address
+                 : "s"(utag), "s"(f.hplan + hsb)
+                 : "memory");
+    STAMP(1);
+    if (tg.y == (unsigned)f.gen && tg.x < SLOW_CAP) return;  // a slow-list block has it
+    const uint4 pa = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+    const uint4 pb = bex ? make_uint4(pv[8], pv[9], pv[10], pv[11]) : pa;
+    if ((int)pa.w == f.gen && (int)pb.w == f.gen) {
       const __amdgpu_buffer_rsrc_t ring =
           __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
-      const unsigned meta = pl.y;
+      const unsigned ma = pa.y, mb = pb.y;
+      const bool mine_a = cc < 16;  // filter lanes: columns of the left SB
       uint32_t ly[8], lc[4];
-      {
-        const Key K = make_key((int)pl.x, (int)(meta & 255));
-        WinLoad W;
-        win_issue(W, f, ring, K, x0, y0);
-        win_commit(W, L.win);
-        wave_lds_sync();
+      {  // pass 0: mv0 (one window when both SBs share the key, else one per SB)
+        const Key KA = make_key((int)pa.x, (int)(ma & 255)), KB = make_key((int)pb.x, (int)(mb & 255));
+        STAMP(2);
+        if (KA.mv == KB.mv && KA.slot == KB.slot) {
+          plan_pass(L, f, ring, KA, x0, y0, ly, lc, false, true);
+        } else {
+          plan_pass(L, f, ring, KA, x0, y0, ly, lc, false, mine_a);
+          plan_pass(L, f, ring, KB, x0, y0, ly, lc, false, !mine_a);
+        }
         STAMP(4);
-        filter_all(L.win, K, f.bipred, x0, ly, lc, false);
       }
-      if (meta & CELL_BI) {  // pass 1: mv1, truncating average with pass 0
-        const Key K = make_key((int)pl.z, (int)((meta >> 8) & 255));
-        wave_lds_sync();
-        WinLoad W;
-        win_issue(W, f, ring, K, x0, y0);
-        win_commit(W, L.win);
-        wave_lds_sync();
-        filter_all(L.win, K, f.bipred, x0, ly, lc, true);
+      const bool bia = ma & CELL_BI, bib = mb & CELL_BI;
+      if (bia || bib) {  // pass 1: mv1 of the bi-pred SB(s), truncating average with pass 0
+        const Key KA = make_key((int)pa.z, (int)((ma >> 8) & 255)), KB = make_key((int)pb.z, (int)((mb >> 8) & 255));
+        if (bia && bib && KA.mv == KB.mv && KA.slot == KB.slot) {
+          plan_pass(L, f, ring, KA, x0, y0, ly, lc, true, true);
+        } else {
+          if (bia) plan_pass(L, f, ring, KA, x0, y0, ly, lc, true, mine_a);
+          if (bib) plan_pass(L, f, ring, KB, x0, y0, ly, lc, true, !mine_a);
+        }
       }
       STAMP(3);
-      const int16_t *rY = resid, *rU = resid + (long long)f.W * f.H, *rV = rU + (long long)(f.W >> 1) * (f.H >> 1);
-      const int x = x0 + 4 * cc, yb = y0 + 8 * gr;
-      const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
-      // Stores through a descriptor over the current slot: one lane offset per
-      // plane, the row in the scalar offset.  A half at the frame's bottom /
-      // right edge stores its rows / columns past the edge into the slot's
-      // padding, which k_pad rewrites (W, H multiples of 8; padding >= 48).
-      const __amdgpu_buffer_rsrc_t cur =
-          __builtin_amdgcn_make_buffer_rsrc((void *)(f.cy - f.offy), 0, (int)f.slot_bytes, 0x00020000);
-      const bool xin = x < f.W;
-      const int oy = (int)f.offy + yb * f.sy + x, ou = (int)f.offu + ycb * f.sc + xc, uvd = (int)(f.offv - f.offu);
+      // ---- residual + stores: the prediction goes through LDS (the window is
+      // free now) so each lane holds 16 contiguous bytes of one row -- three
+      // 16-byte stores per lane: the luma rows as whole 128-B lines (row pixel 0
+      // is line-aligned, capi.hip), the chroma rows as 64-B segments.  The
+      // store tail is bound by store instructions and the lines they touch ----
+      wave_lds_sync();
+      uint8_t *const ty = L.win.y, *const tc = L.win.y + 2048;  // 16 x 128 B luma; 8 x 64 B U, then V
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        uint32_t v = ly[i];
-        if ((meta & CELL_RES(0)) && xin && yb + i < f.H) v = add_res4(v, rY + (long long)(yb + i) * f.W + x);
-        __builtin_amdgcn_raw_buffer_store_b32(v, cur, oy, i * f.sy, 0);
-        if (i == 7 && h == 1 && gr == 3 && yb + i < f.H)  // SB row 63: the edge row k_intra's next SB row reads
-          *(uint32_t *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + x) = v;
-      }
+      for (int i = 0; i < 8; i++) *(uint32_t *)(ty + (8 * gr + i) * 128 + 4 * cc) = ly[i];
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const int y = ycb + i;
-        uint32_t vu = lc[i] & 0xffff, vv = lc[i] >> 16;
-        if ((meta & CELL_RES(1)) && xin && y < (f.H >> 1)) vu = add_res2(vu, rU + (long long)y * (f.W >> 1) + xc);
-        if ((meta & CELL_RES(2)) && xin && y < (f.H >> 1)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
-        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)vu, cur, ou, i * f.sc, 0);
-        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)vv, cur, ou + uvd, i * f.sc, 0);
-        if (i == 3 && h == 1 && gr == 3 && y < (f.H >> 1)) {  // chroma SB row 31
-          uint8_t *e = f.edge + (long long)f.nsbrows * f.ewy + (long long)sby * f.ewc + EDGE_MARGIN + xc;
-          *(uint16_t *)e = (uint16_t)vu;
-          *(uint16_t *)(e + (long long)f.nsbrows * f.ewc) = (uint16_t)vv;
+        *(uint16_t *)(tc + (4 * gr + i) * 64 + 2 * cc) = (uint16_t)lc[i];
+        *(uint16_t *)(tc + 512 + (4 * gr + i) * 64 + 2 * cc) = (uint16_t)(lc[i] >> 16);
+      }
+      wave_lds_sync();
+      uint4 py0 = *(const uint4 *)(ty + 16 * lane), py1 = *(const uint4 *)(ty + 1024 + 16 * lane);
+      uint4 pc = *(const uint4 *)(tc + 16 * lane);
+      const int r = lane >> 3, xl = x0 + 16 * (lane & 7);  // luma: rows r and r + 8 of the unit
+      const int pl1 = lane >> 5, rc = (lane & 31) >> 2;     // chroma: plane U / V, row rc
+      const int xcl = (x0 >> 1) + 16 * (lane & 3), yc = (y0 >> 1) + rc;
+      const unsigned mly = (lane & 4) ? mb : ma, mlc = (lane & 2) ? mb : ma;  // the SB of the lane's chunk
+      if (mly & CELL_RES(0)) {
+        const int16_t *rY = resid;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const int y = y0 + r + 8 * k;
+          if (y >= f.H) continue;
+          uint4 &p = k ? py1 : py0;
+          const int16_t *q = rY + (long long)y * f.W + xl;
+          if (xl < f.W) p.x = add_res4(p.x, q);
+          if (xl + 4 < f.W) p.y = add_res4(p.y, q + 4);
+          if (xl + 8 < f.W) p.z = add_res4(p.z, q + 8);
+          if (xl + 12 < f.W) p.w = add_res4(p.w, q + 12);
         }
+      }
+      if ((mlc & CELL_RES(1 + pl1)) && yc < (f.H >> 1)) {
+        const int wc = f.W >> 1;
+        const int16_t *q = resid + (long long)f.W * f.H + (long long)pl1 * wc * (f.H >> 1) + (long long)yc * wc + xcl;
+        if (xcl < wc) pc.x = add_res4(pc.x, q);
+        if (xcl + 4 < wc) pc.y = add_res4(pc.y, q + 4);
+        if (xcl + 8 < wc) pc.z = add_res4(pc.z, q + 8);
+        if (xcl + 12 < wc) pc.w = add_res4(pc.w, q + 12);
+      }
+      // Stores through a descriptor over the current slot: one lane offset per
+      // plane, the second luma row set in the scalar offset.  A unit at the
+      // frame's bottom / right edge stores its rows / columns past the edge into
+      // the slot's padding, which k_pad rewrites (W, H multiples of 8; padding
+      // >= 48); the columns of a right SB past the last one are not stored.
+      const __amdgpu_buffer_rsrc_t cur =
+          __builtin_amdgcn_make_buffer_rsrc((void *)(f.cy - f.offy), 0, (int)f.slot_bytes, 0x00020000);
+      const int oy = (int)f.offy + (y0 + r) * f.sy + xl;
+      const int oc = (int)(pl1 ? f.offv : f.offu) + yc * f.sc + xcl;
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+#if RECON_PROBE == 3  // timing probe: no pixel stores (wrong output)
+      if (f.W > 0) return;
+#endif
+      if (bex || !(lane & 4)) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, py0), cur, oy, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, py1), cur, oy, 8 * f.sy, 0);
+      }
+      if (bex || !(lane & 2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pc), cur, oc, 0, 0);
+      if (last) {  // SB row 63 / chroma SB row 31: the edge rows k_intra's next SB row reads
+        if (r == 7 && y0 + 15 < f.H && xl < f.W)
+          *(uint4 *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + xl) = py1;
+        if (rc == 7 && yc < (f.H >> 1) && xcl < (f.W >> 1))
+          *(uint4 *)(f.edge + (long long)f.nsbrows * f.ewy + (long long)(pl1 * f.nsbrows + sby) * f.ewc + EDGE_MARGIN +
+                     xcl) = pc;
       }
       STAMP(5);
       return;
@@ -828,14 +936,14 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
     STAMP(1);
   }
 
-  // ---- P0: lane = cell row cr of 8x8 unit uu of the half: the two cells' MC
-  // words that k_frame_prep resolved (quarter MV with the `sign` negation,
+  // ---- P0: lane = cell row cr of 8x8 unit uu of the work unit: the two cells'
+  // MC words that k_frame_prep resolved (quarter MV with the `sign` negation,
   // inter_prediction.c:78-79 / :125-126, reference slots, bi-pred, coded
   // residual per component), one 16-byte load ----
   const int uu = lane >> 1, cr = lane & 1;
-  const int ur = uu >> 3, uc = uu & 7;
-  const int uy = sby * 64 + 32 * h + 8 * ur, ux = sbx * 64 + 8 * uc;
-  const int lrow = 2 * ur + cr;  // cell row inside the half
+  const int ur = uu >> 4, uc = uu & 15;
+  const int uy = y0 + 8 * ur, ux = x0 + 8 * uc;
+  const int lrow = 2 * ur + cr;  // cell row inside the unit
   uint4 mc = make_uint4(0, 0, 0, 0);
   const int cidx = ((uy >> 2) + cr) * cs + (ux >> 2);
   if (uy < f.H && ux < f.W) mc = *(const uint4 *)&f.cellmc[cidx];
@@ -843,7 +951,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
 #pragma unroll
   for (int c = 0; c < 2; c++) {
     const unsigned meta = c ? mc.w : mc.y;
-    const int cell = lrow * 16 + 2 * uc + c;
+    const int cell = lrow * 32 + 2 * uc + c;
     L.mv0[cell] = (int)(c ? mc.z : mc.x);
     L.mv1[cell] = (meta & CELL_BI) ? f.cellmv1[cidx + c] : 0;
     L.meta[cell] = meta;
@@ -890,7 +998,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
   const int xc = (x0 >> 1) + 2 * cc, ycb = (y0 >> 1) + 4 * gr;
 #pragma unroll
   for (int s = 0; s < 2; s++) {
-    const unsigned meta = L.meta[(2 * gr + s) * 16 + cc];
+    const unsigned meta = L.meta[(2 * gr + s) * 32 + cc];
     if (!(meta & CELL_ACT)) continue;
 #pragma unroll
     for (int i = 4 * s; i < 4 * s + 4; i++) {
@@ -898,7 +1006,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
       uint32_t v = ly[i];
       if (meta & CELL_RES(0)) v = add_res4(v, rY + (long long)y * f.W + x);
       *(uint32_t *)(f.cy + (long long)y * f.sy + x) = v;
-      if (i == 7 && h == 1 && gr == 3)  // SB row 63: the edge row k_intra's next SB row reads
+      if (i == 7 && last && gr == 1)  // SB row 63: the edge row k_intra's next SB row reads
         *(uint32_t *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + x) = v;
     }
 #pragma unroll
@@ -909,7 +1017,7 @@ __global__ __launch_bounds__(64) void k_recon(const FrameBatch fb_, unsigned lon
       if (meta & CELL_RES(2)) vv = add_res2(vv, rV + (long long)y * (f.W >> 1) + xc);
       *(uint16_t *)(f.cu + (long long)y * f.sc + xc) = (uint16_t)vu;
       *(uint16_t *)(f.cv + (long long)y * f.sc + xc) = (uint16_t)vv;
-      if (i == 3 && h == 1 && gr == 3) {  // chroma SB row 31
+      if (i == 3 && last && gr == 1) {  // chroma SB row 31
         uint8_t *e = f.edge + (long long)f.nsbrows * f.ewy + (long long)sby * f.ewc + EDGE_MARGIN + xc;
         *(uint16_t *)e = (uint16_t)vu;
         *(uint16_t *)(e + (long long)f.nsbrows * f.ewc) = (uint16_t)vv;

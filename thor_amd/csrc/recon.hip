@@ -12,6 +12,45 @@
 // the packed side-info that copy_deblock_data (dec/decode_block.c:122-156)
 // stores for deblocking/CLPF.
 // ---------------------------------------------------------------------------
+// A half with several (MV, reference) keys: its two k_recon units join the
+// frame's slow list (common.h).  The first claimant of a unit this frame tags it
+// and appends it (count and tags are generation-stamped, so nothing is cleared
+// between frames).
+__device__ __forceinline__ void slow_claim(const FrameCtx &f, int sbx, int sby, int h) {
+  const int nh = half_count(f.W, f.H), np = unit_pairs(f.W);
+  unsigned long long *cnt = (unsigned long long *)(f.hplan + nh);
+  unsigned long long *utag = (unsigned long long *)(f.hplan + hplan_utag_off(f.W, f.H));
+  const unsigned long long g = (unsigned long long)(unsigned)f.gen << 32;
+  for (int j = 0; j < 2; j++) {
+    const int u = (4 * sby + 2 * h + j) * np + (sbx >> 1);
+    unsigned long long o = __hip_atomic_load(&utag[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool won = false;
+    while ((o >> 32) != (g >> 32)) {
+      const unsigned long long r = atomicCAS(&utag[u], o, g | 0xffffffffull);
+      if (r == o) {
+        won = true;
+        break;
+      }
+      o = r;
+    }
+    if (!won) continue;  // another CU of this unit got there first
+    unsigned long long c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned idx;
+    for (;;) {
+      const bool cur = (c >> 32) == (g >> 32);
+      const unsigned long long nw = cur ? c + 1 : (g | 1ull);
+      const unsigned long long r = atomicCAS(cnt, c, nw);
+      if (r == c) {
+        idx = cur ? (unsigned)c : 0u;
+        break;
+      }
+      c = r;
+    }
+    if (idx < SLOW_CAP) ((unsigned *)(f.hplan + nh + 1))[idx] = (unsigned)u;
+    __hip_atomic_store(&utag[u], g | idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   const int b = bx * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -71,11 +110,16 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   // has rows inside the frame writes half h's record when quarters 2h and 2h+1 share their MVs
   // (always so for SKIP / MERGE, which use mv_arr[0]; INTER / BIPRED halves of
   // a horizontal split too).
+  // Every other half with inter work (smaller inter CUs, or a 64x64 INTER / BIPRED
+  // half whose two quarters differ) is multi-key: its first claimant appends it
+  // to the frame's slow list, which k_recon dispatches ahead of the planned halves.
+  if (f.hplan && S < 64 && lane == 0 && mode != M_INTRA) slow_claim(f, B.xpos >> 6, B.ypos >> 6, (B.ypos & 63) >= 32);
   if (f.hplan && S == 64 && lane < 2 && mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0)) {
     const int h = lane, q0 = quarters ? 2 * h : 0, q1 = quarters ? 2 * h + 1 : 0;
     const bool same = B.mv0[2 * q0] == B.mv0[2 * q1] && B.mv0[2 * q0 + 1] == B.mv0[2 * q1 + 1] &&
                       (!bi || (B.mv1[2 * q0] == B.mv1[2 * q1] && B.mv1[2 * q0 + 1] == B.mv1[2 * q1 + 1]));
     const bool inside = B.ypos + 32 * h < f.H;  // rows / columns past the frame edge are not stored (k_recon)
+    if (!same && inside) slow_claim(f, B.xpos >> 6, B.ypos >> 6, h);
     if (same && inside) {
       int m0x = B.mv0[2 * q0], m0y = B.mv0[2 * q0 + 1], m1x = B.mv1[2 * q0], m1y = B.mv1[2 * q0 + 1];
       if (sg0) { m0x = -m0x; m0y = -m0y; }

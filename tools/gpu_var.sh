@@ -6,7 +6,8 @@ mkdir -p gpurun_out
 for V in ${VARS:-A B B6 B7 B8}; do
   if [ $V = A ]; then LIBP=thor_amd/libthor_amd.so; else LIBP=var/lib_$V.so; fi
   for S in k4_low k4_med; do
-    echo "== $V $S"; THOR_AMD_LIB=$LIBP timeout -k 10 120 python3 tools/recon_batch.py $S 8 10 --time 2>&1 | grep -E "avg|Error|error" || exit 1
+    echo "== $V $S"; THOR_AMD_LIB=$LIBP timeout -k 10 120 python3 tools/recon_batch.py $S 8 10 --time > gpurun_out/var_time.log 2>&1 || { tail -8 gpurun_out/var_time.log; exit 1; }
+    grep -E "avg" gpurun_out/var_time.log
   done
 done
 for V in ${PVARS-B B8}; do

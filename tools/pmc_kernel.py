@@ -11,7 +11,7 @@ from collections import defaultdict
 d = sys.argv[1]
 kern = sys.argv[2] if len(sys.argv) > 2 else "k_recon"
 res = {}
-for p in ("sq1", "sq2", "fetch", "write"):
+for p in ("sq1", "sq2", "fetch", "write", "ta"):
     db = os.path.join(d, p, "run_results.db")
     if not os.path.exists(db):
         continue

@@ -16,5 +16,6 @@ timeout -s KILL 60 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAI
 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d $OUT/sq2 -o run -- $D > /dev/null 2> $OUT/sq2.err || { echo SQ2_FAIL; tail -20 $OUT/sq2.err; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run -- $D > /dev/null 2> $OUT/fetch.err || { echo FETCH_FAIL; tail -20 $OUT/fetch.err; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run -- $D > /dev/null 2> $OUT/write.err || { echo WRITE_FAIL; tail -20 $OUT/write.err; exit 1; }
+timeout -s KILL 60 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUFFER_WAVEFRONTS_sum GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d $OUT/ta -o run -- $D > /dev/null 2> $OUT/ta.err || echo TA_FAIL
 timeout -k 10 120 $P > $OUT/probe.txt 2>&1 || { echo PROBE_FAIL; tail $OUT/probe.txt; exit 1; }
 find $OUT -name '*.csv' | head -40

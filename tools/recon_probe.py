@@ -16,7 +16,7 @@ dec = GpuDecoder(seq)
 lib = L.load()
 lib.thor_dec_debug_recon.argtypes = [C.c_void_p, C.c_void_p]
 nsb = ((seq.width + 63) // 64) * ((seq.height + 63) // 64)
-nwg = 8 * ((2 * nsb + 7) // 8)
+nwg = 8 * (((((seq.width + 63) // 64 + 1) // 2) * 4 * ((seq.height + 63) // 64) + 7) // 8)  # k_recon units
 nbytes = nwg * 8 * 8
 buf = lib.thor_dev_alloc(nbytes)
 devs = [dec.upload(fr) for fr in frames]
@@ -42,7 +42,8 @@ for i, d in enumerate(devs):
     print("   init  dur  ", q(rel[:, 1] - rel[:, 0]))
     print("   P0    dur  ", q(rel[:, 2] - rel[:, 1]))
     print("   stage dur  ", q(rel[:, 4] - rel[:, 2]))
-    print("   filt+store ", q(rel[:, 3] - rel[:, 4]))
+    print("   filter     ", q(rel[:, 3] - rel[:, 4]))
+    print("   store      ", q(rel[:, 5] - rel[:, 3]))
     print("   end        ", q(rel[:, 5]))
     cu = ((hw >> 8) & 15) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 3) << 5)
     simd = (hw >> 4) & 3
@@ -59,8 +60,7 @@ for i, d in enumerate(devs):
     for n in sorted(set(load.tolist())):
         print("     simds with %d waves: end p50 %.2f max %.2f (%d waves)" % (n, np.median(rel[load == n, 5]), rel[load == n, 5].max(), (load == n).sum()))
     idx = np.nonzero(ok)[0]
-    per_x = (2 * nsb + 7) // 8
-    hsb = (idx & 7) * per_x + (idx >> 3)
+    hsb = idx  # stamps are indexed by half SB
     sbw = (seq.width + 63) // 64
     st = rel[:, 4] - rel[:, 2]
     order = np.argsort(-st)[:12]
