@@ -846,8 +846,8 @@ def main():
                 "avg_launch_us": round(recon_ms * 1e3, 2),
                 "frames_per_launch": B,
                 "launches": "batched P-frame decode launches of group 0 alone (streams of clips 0..7, the inter "
-                            "stage: k_recon + k_recon_multi for the half SBs with several keys); hipEvents on its "
-                            "stream",
+                            "stage: one k_recon launch -- 128x16 units, the frames' multi-key units first); "
+                            "hipEvents on its stream",
                 "dominant_kernel_note": "by GPU time the step is k_enc_rows, the encoder's superblock worker: "
                                         "integer RD search with negligible HBM traffic and no MFMA work, latency "
                                         "bound inside the wave (DESIGN.md 3b), so neither roofline bounds it; this "
@@ -901,7 +901,9 @@ def rows_mode(a, torch, dist, rank, world, local):
     for _ in range(max(1, a.warmup)):
         step()
     torch.cuda.synchronize(local)
-    got = {fr.frame_num: dec.read_i420(fr.frame_num) for fr in frames}
+    # halo mode: no rank holds every row final -- each frame is put together from
+    # its bands' owners (outside the timed region)
+    got = {fr.frame_num: sh.assemble(fr.frame_num) if a.halo else dec.read_i420(fr.frame_num) for fr in frames}
     ok = hashlib.md5(b"".join(got[k] for k in sorted(got))).hexdigest() == meta["dec_md5"]
     dist.barrier()
     torch.cuda.synchronize(local)
@@ -915,8 +917,6 @@ def rows_mode(a, torch, dist, rank, world, local):
     okt = torch.tensor([1 if ok else 0], device="cuda")
     dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     elapsed, ok = float(t.item()), bool(okt.item())
-    if a.halo and world > 1:  # each rank holds only its band final: not checked here (tests/test_gpu_shard.py is)
-        ok = None
     px_step = seq.width * seq.height * len(frames)
     if rank == 0:
         print(json.dumps({

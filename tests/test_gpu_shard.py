@@ -44,7 +44,7 @@ def _worker(rank, world, port, name, nframes, q, local=False, halo=False):
             sh.decode(dec.upload(fr), fr.frame_num, fr)
             # halo mode leaves only the band final on each rank: the check (not the protocol)
             # assembles the frame from every band's owner
-            got = hashlib.md5(_assembled(sh, dec, fr.frame_num) if halo else dec.read_i420(fr.frame_num)).hexdigest()
+            got = hashlib.md5(sh.assemble(fr.frame_num) if halo else dec.read_i420(fr.frame_num)).hexdigest()
             if got != meta["stage_md5"][fr.decode_order]["final"]:
                 bad.append(fr.decode_order)
         if halo:  # the halo bytes this rank received per frame vs one full-frame exchange
@@ -58,40 +58,6 @@ def _worker(rank, world, port, name, nframes, q, local=False, halo=False):
     finally:
         if dec is not None:
             dec.close()
-
-
-def _assembled(sh, dec, fnum):
-    """Test-only: the whole frame (I420 bytes) from the bands' owners."""
-    import numpy as np
-    import torch
-
-    from thor_amd.shard import rows_bytes
-
-    W, H, world = sh.W, sh.H, sh.world
-    mine = np.zeros(sh.nbytes, np.uint8)
-    lo, hi = sh.owned(sh.rank)
-    if hi > lo:
-        buf = dec.scratch(sh.nbytes)
-        dec.get_rows(fnum, lo, sh.rows, buf)
-        dec.d2h(mine, buf)
-    parts = [torch.empty(sh.nbytes, dtype=torch.uint8) for _ in range(world)]
-    sh.dist.all_gather(parts, torch.from_numpy(mine))
-    y = np.zeros((H, W), np.uint8)
-    u = np.zeros((H // 2, W // 2), np.uint8)
-    v = np.zeros((H // 2, W // 2), np.uint8)
-    for r in range(world):
-        a, b = sh.owned(r)
-        n = b - a
-        if n <= 0:
-            continue
-        p = parts[r].numpy()
-        y[a:b] = p[:n * W].reshape(n, W)
-        o = sh.rows * W
-        for pl in (u, v):
-            pl[a // 2:b // 2] = p[o:o + (n // 2) * (W // 2)].reshape(n // 2, W // 2)
-            o += (sh.rows // 2) * (W // 2)
-    assert rows_bytes(W, H) == y.nbytes + u.nbytes + v.nbytes
-    return y.tobytes() + u.tobytes() + v.tobytes()
 
 
 @pytest.mark.parametrize("name,nframes,world,local", [

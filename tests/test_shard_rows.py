@@ -273,3 +273,120 @@ def test_row_shard_halo_exchange_gloo(world, W, H):
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(r, "ok") for r in range(world)], res
+
+
+def test_missing_rows_tracking():
+    """RowShard.missing: only the requested rows a rank does not already hold
+    final are fetched (its own band, every halo fetched before)."""
+    from thor_amd.shard import RowShard
+
+    sh = object.__new__(RowShard)
+    sh.final = {}
+    sh._hold(5, 128, 256)
+    assert sh.missing({5: (100, 300)}) == [(5, 100, 128), (5, 256, 300)]
+    sh._hold(5, 256, 300)
+    sh._hold(5, 90, 130)
+    assert sh.final[5] == [(90, 300)]
+    assert sh.missing({5: (100, 300)}) == []
+    assert sh.missing({5: (0, 320), 6: (10, 20)}) == [(5, 0, 90), (5, 300, 320), (6, 10, 20)]
+
+
+def _halo_interp_worker(rank, world, port, W, H, q):
+    import torch.distributed as dist
+
+    from thor_amd.shard import RowShard, rows_bytes
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(11)
+        nf = 6
+        truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
+                     rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(nf)}
+        frames = {f: FakeFrame(f, W, H, rng, reach=8) for f in range(nf)}
+        for f in range(2, nf):  # temporal-interpolated reference built from frames 0 and 1 (both read whole)
+            frames[f].interp_refs, frames[f].interp_ratio = (0, 1), 2
+        ctx = NumpyContext(W, H, truth)
+        ctx.halo = True
+        ctx.frames = frames
+        sh = RowShard(ctx, dist, W, H, device_exchange=False, band_local=True, halo=True)
+        for f in range(nf):
+            sh.decode(f, f, frames[f])
+        full = rows_bytes(W, H)
+        # frame 2 fetches both interpolation sources whole (less this rank's own bands of them);
+        # frames 3.. hold them already: only their small MV halos of the previous frame move
+        assert sh.halo_bytes[2] > full // 2, sh.halo_bytes
+        assert all(b < full // 4 for b in sh.halo_bytes[3:]), sh.halo_bytes
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-600:]))
+
+
+def _halo_overflow_worker(rank, world, port, W, H, q):
+    import torch.distributed as dist
+
+    from thor_amd.shard import MAX_REQ, RowShard
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(5)
+        nf = MAX_REQ + 3
+        truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
+                     rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(nf)}
+        frames = {f: FakeFrame(f, W, H, rng, reach=2) for f in range(nf)}
+        last = frames[nf - 1]
+        last.blocks = np.repeat(last.blocks[:1], nf - 1)  # rank 0's first SB, once per older frame
+        last.blocks["ref0"] = np.arange(nf - 1)
+        last.blocks["mv0"][:] = 4 * 200  # reaching far below the band: rows it does not hold
+        ctx = NumpyContext(W, H, truth)
+        ctx.halo = True
+        sh = RowShard(ctx, dist, W, H, device_exchange=False, band_local=True, halo=True)
+        for f in range(nf - 1):
+            sh.decode(f, f, frames[f])
+        try:
+            sh.decode(nf - 1, nf - 1, last)
+            res = "no error"
+        except ValueError as e:
+            res = "raised" if "reference ranges" in str(e) else repr(e)
+        dist.barrier()  # every rank got here: nobody is stuck in a collective
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-600:]))
+
+
+def _run_world(target, world, W, H, want):
+    import random
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=target, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(r, want) for r in range(world)], res
+
+
+def test_row_shard_halo_interp_sources_fetched_once_gloo():
+    """Frames whose interpolated reference reads both sources whole fetch them
+    once; later frames over the same sources move only their MV halos."""
+    _run_world(_halo_interp_worker, 2, 192, 320, "ok")
+
+
+def test_row_shard_halo_request_overflow_raises_everywhere_gloo():
+    """A rank with more than MAX_REQ reference ranges flags the request table:
+    every rank raises after the all-gather instead of one rank raising before it
+    and the others blocking in the collective."""
+    _run_world(_halo_overflow_worker, 2, 192, 320, "raised")

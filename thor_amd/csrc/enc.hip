@@ -16,6 +16,8 @@
 //   k_clpf, k_pad   the decoder's CLPF and padding kernels
 //   k_enc_pack      frame header + SB bit strings + CLPF bits -> the frame's
 //                   bytes (putbits / flush_all_bits, enc/putbits.c:57-129)
+#include <atomic>
+
 #include "common.h"
 #include "enc_gop.h"
 #include "enc_rd.h"
@@ -361,8 +363,10 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n) {
 }
 
 // diagnostics (thor_enc_debug_stall): the WPP wait bound and a row that never publishes
-static unsigned long long g_spin_limit = 30000000000ULL;  // s_memrealtime ticks (100 MHz): 5 minutes
-static int g_stall_row = -1;
+// thor_enc_debug_stall's settings, read by every thor_enc_frames call: atomics,
+// so a call on another thread sees either the old or the new value, never a torn one
+static std::atomic<unsigned long long> g_spin_limit{30000000000ULL};  // s_memrealtime ticks (100 MHz): 5 minutes
+static std::atomic<int> g_stall_row{-1};
 
 extern "C" {
 
@@ -614,8 +618,8 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   // than the chip holds at once (one per SIMD at this kernel's register and LDS
   // use) would only start as the first ones run out of work
   k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(P.jobs, n, P.ticket, nrows,
-                                                                         P.scratch, P.err, g_spin_limit,
-                                                                         g_stall_row);
+                                                                         P.scratch, P.err, g_spin_limit.load(),
+                                                                         g_stall_row.load());
   EHIP(hipGetLastError());
   const int ncell = (W / 4) * (H / 4);
   k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(P.jobs);
@@ -730,8 +734,8 @@ int thor_enc_reset(thor_enc_t *e) {
 // (-1: off) and a WPP wait gives up after `spin_ms` (<= 0: the 5-minute
 // default), so the bounded-time failure path can be exercised.
 int thor_enc_debug_stall(int row, int spin_ms) {
-  g_stall_row = row;
-  g_spin_limit = spin_ms > 0 ? (unsigned long long)spin_ms * 100000ULL : 30000000000ULL;
+  g_stall_row.store(row);
+  g_spin_limit.store(spin_ms > 0 ? (unsigned long long)spin_ms * 100000ULL : 30000000000ULL);
   return THOR_OK;
 }
 

@@ -560,36 +560,68 @@ __device__ __forceinline__ void shifted_taps(unsigned long long t48, int o, int 
   w2 = o > 2 ? (int)(uint32_t)(t48 >> (64 - 8 * o)) : 0;
 }
 
-// Eight luma rows of the lane's 4-px column, generic 6x6 taps.  `base` = the
-// window byte of strip row -2, column -2 rounded down to a dword; sh = the
-// byte offset of column -2 in it (uniform).  Horizontal: three dot4 per pixel
-// on the unshifted dwords with per-pixel shifted tap words (no v_alignbyte);
-// vertical: three dot2 per pixel on (H'[r], H'[r+1]) pairs.
-// SH (the uniform byte offset, a template argument: the dispatcher switches on
-// it) tells which tap words are zero: pixel j's taps cover window bytes
-// SH + j .. SH + j + 5, so d0 is read only for SH + j <= 3 and d2 only for
-// SH + j >= 3 -- 9 dot4 per row of 4 px instead of 12.
-template <int SH>
+// clip255(x >> 6) of four sums packed as bytes (|x| < 2^15): int16 pairs, a
+// packed shift, saturation to u8 -- the one-dimensional filters' output (the
+// rounding 32 is in the sums' seed).
+typedef short i16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack4_sh6_u8(int a, int b, int c, int d) {
+  const i16x2v sh = {6, 6};
+  const i16x2v ab = __builtin_amdgcn_cvt_pk_i16(a, b) >> sh, cd = __builtin_amdgcn_cvt_pk_i16(c, d) >> sh;
+  return __builtin_amdgcn_perm(sat_u8x2_pk(__builtin_bit_cast(uint32_t, cd)),
+                               sat_u8x2_pk(__builtin_bit_cast(uint32_t, ab)), 0x05040100u);
+}
+
+// Eight luma rows of the lane's 4-px column, 6x6 taps.  `base` = the window
+// byte of strip row -2, column -2 rounded down to a dword; SH = the byte offset
+// of column -2 in it (uniform: the dispatcher switches on it).  Horizontal: dot4
+// per pixel on the unshifted dwords with per-pixel shifted tap words (no
+// v_alignbyte); pixel j's taps cover window bytes SH + j .. SH + j + 5, so d0 is
+// read only for SH + j <= 3 and d2 only for SH + j >= 3 -- 9 dot4 per row of 4 px
+// instead of 12.  Vertical: three dot2 per pixel on (H'[r], H'[r+1]) pairs.
+// FX0 / FY0: the horizontal / vertical fraction is 0, i.e. the taps are
+// {0, 0, 64, 0, 0, 0} (common/inter_prediction.c:47-59): one dot4 per pixel for
+// the horizontal pass / no vertical pass at all ((64 x 64 x p + 2048) >> 12 =
+// (64 x H + 2048) >> 12 = (H + 32) >> 6 exactly, so the one-dimensional forms
+// are the same integers as the two-dimensional filter).
+template <int SH, bool FX0, bool FY0>
 __device__ __forceinline__ void luma8_fast(const uint8_t *base, unsigned long long th48, int v01, int v23,
                                            int v45, uint32_t out[8], bool acc, bool k0 = true, bool k1 = true) {
   int T[4][3];
 #pragma unroll
   for (int j = 0; j < 4; j++) shifted_taps(th48, SH + j, T[j][0], T[j][1], T[j][2]);
   const int hb = HB;  // in a VGPR: the chains' seed (one scalar operand per instruction)
+  auto hsum = [&](int r, int hc[4]) {  // strip row r: H' + HB of the lane's 4 pixels
+    const uint32_t *q = (const uint32_t *)(base + (r + 2) * WL_P);
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (FX0) {  // the one non-zero tap (64) sits on window byte SH + j + 2
+        const int w = (SH + j + 2) >> 2;
+        hc[j] = vdot4(w == 0 ? d0 : (w == 1 ? d1 : d2), T[j][w], hb);
+      } else {
+        int a = hb;
+        if (SH + j >= 3) a = vdot4(d2, T[j][2], a);
+        a = vdot4(d1, T[j][1], a);
+        if (SH + j <= 3) a = vdot4(d0, T[j][0], a);
+        hc[j] = a;
+      }
+    }
+  };
+  if (FY0) {  // horizontal only: rows 0..7
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      int hc[4];
+      hsum(i, hc);
+      const uint32_t o = pack4_sh6_u8(hc[0], hc[1], hc[2], hc[3]);
+      if (i < 4 ? k0 : k1) out[i] = acc ? avg_bytes(out[i], o) : o;
+    }
+    return;
+  }
   int hp[4];
   uint32_t pa[6][4];
   auto hrow = [&](int r) {  // strip row r (-2 .. 10) -> P(r - 1)
-    const uint32_t *q = (const uint32_t *)(base + (r + 2) * WL_P);
-    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
     int hc[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      int a = hb;
-      if (SH + j >= 3) a = vdot4(d2, T[j][2], a);
-      a = vdot4(d1, T[j][1], a);
-      if (SH + j <= 3) a = vdot4(d0, T[j][0], a);
-      hc[j] = a;
-    }
+    hsum(r, hc);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (r > -2) pa[(r + 5) % 6][j] = pack_lo16(hp[j], hc[j]);
@@ -610,8 +642,66 @@ __device__ __forceinline__ void luma8_fast(const uint8_t *base, unsigned long lo
   }
 }
 
+// The (2,2) position (common/inter_prediction.c:145-157), fast form: the
+// kernel K[i][j] = u_i + u_j (rows / columns -1..2, u = [0 1 1 0]) is
+//   S(o) = H2(o-1) + H4(o) + H4(o+1) + H2(o+2),
+// H4 = the [1 2 2 1] and H2 = the [0 1 1 0] horizontal sums over columns -1..2
+// (dot4 with compile-time shifted tap words on the biased bytes: H4' = H4 - 768,
+// H2' = H2 - 256, and H2's seed 1028 carries the bias and the rounding:
+// 2 x (256 + 1028) + 2 x 768 ... = S + 8 exactly).  Output (S + 8) >> 4 with
+// the rows as int16 pairs of pixels: packed adds and shifts (|S| < 2^13).
+template <int SH>
+__device__ __forceinline__ void luma8_ctr(const uint8_t *base, uint32_t out[8], bool acc, bool k0 = true,
+                                          bool k1 = true) {
+  constexpr unsigned long long t4 = 0x0000010202010000ull >> 8;  // {0, 1, 2, 2, 1, 0} at window bytes 0..5
+  constexpr unsigned long long t2 = 0x0000000101000000ull >> 8;  // {0, 0, 1, 1, 0, 0}
+  auto word = [](unsigned long long t, int o, int w) -> int {
+    const unsigned long long lo = t << (8 * o);
+    return w == 0 ? (int)(uint32_t)lo : (w == 1 ? (int)(uint32_t)(lo >> 32) : (o > 2 ? (int)(uint32_t)(t >> (64 - 8 * o)) : 0));
+  };
+  i16x2v p4[4][2], p2[4][2];  // rows as (pixel 0, 1), (pixel 2, 3) pairs, ring by strip row
+  auto hrow = [&](int r) {  // strip row r (-1 .. 9)
+    const uint32_t *q = (const uint32_t *)(base + (r + 2) * WL_P);
+    const uint32_t d[3] = {q[0], q[1], q[2]};
+    int h4[4], h2[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int a = 0, c = 1028;
+#pragma unroll
+      for (int w = (SH + j + 1) >> 2; w <= (SH + j + 4) >> 2; w++) a = vdot4(d[w], word(t4, SH + j, w), a);
+#pragma unroll
+      for (int w = (SH + j + 2) >> 2; w <= (SH + j + 3) >> 2; w++) c = vdot4(d[w], word(t2, SH + j, w), c);
+      h4[j] = a;
+      h2[j] = c;
+    }
+    const int k = (r + 4) & 3;
+    p4[k][0] = __builtin_amdgcn_cvt_pk_i16(h4[0], h4[1]);
+    p4[k][1] = __builtin_amdgcn_cvt_pk_i16(h4[2], h4[3]);
+    p2[k][0] = __builtin_amdgcn_cvt_pk_i16(h2[0], h2[1]);
+    p2[k][1] = __builtin_amdgcn_cvt_pk_i16(h2[2], h2[3]);
+  };
+#pragma unroll
+  for (int r = -1; r <= 1; r++) hrow(r);
+  const i16x2v sh = {4, 4};
+#pragma unroll
+  for (int o = 0; o < 8; o++) {
+    hrow(o + 2);
+    uint32_t hv[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const i16x2v s = (p2[(o + 3) & 3][e] + p4[(o + 4) & 3][e]) + (p4[(o + 5) & 3][e] + p2[(o + 6) & 3][e]);
+      hv[e] = sat_u8x2_pk(__builtin_bit_cast(uint32_t, s >> sh));
+    }
+    const uint32_t v = __builtin_amdgcn_perm(hv[1], hv[0], 0x05040100u);
+    if (o < 4 ? k0 : k1) out[o] = acc ? avg_bytes(out[o], v) : v;
+  }
+}
+
 // Four chroma rows of the lane's 2-px column, U and V (4x4 taps).  sh = byte
 // offset of column -1 in the first dword (uniform).
+// CY0: the vertical fraction is 0 ({0, 64, 0, 0}): rows 0..3 only, no vertical
+// pass ((H + 32) >> 6, the same integers, as for luma).
+template <bool CY0>
 __device__ __forceinline__ void chroma4_fast(const uint8_t *bu, const uint8_t *bv, int sh, unsigned long long tc32,
                                              int v01, int v23, uint32_t out[4], bool acc, bool k0 = true,
                                              bool k1 = true) {
@@ -623,17 +713,30 @@ __device__ __forceinline__ void chroma4_fast(const uint8_t *bu, const uint8_t *b
     T[j][1] = (int)(uint32_t)(x >> 32);
   }
   const int hb = HB;
-  int pu_prev[2], pv_prev[2];
-  uint32_t pu[4][2], pv[4][2];
-  auto hrow = [&](int r) {  // strip row r (-1 .. 5)
+  auto hsum = [&](int r, int hu[2], int hv[2]) {  // strip row r: H' + HB of the lane's 2 U and 2 V pixels
     const uint32_t *qu = (const uint32_t *)(bu + (r + 1) * WC_P), *qv = (const uint32_t *)(bv + (r + 1) * WC_P);
     const uint32_t u0 = qu[0], u1 = qu[1], w0 = qv[0], w1 = qv[1];
-    int hu[2], hv[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       hu[j] = vdot4(u0, T[j][0], vdot4(u1, T[j][1], hb));
       hv[j] = vdot4(w0, T[j][0], vdot4(w1, T[j][1], hb));
     }
+  };
+  if (CY0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      int hu[2], hv[2];
+      hsum(i, hu, hv);
+      const uint32_t uv = pack4_sh6_u8(hu[0], hu[1], hv[0], hv[1]);
+      if (i < 2 ? k0 : k1) out[i] = acc ? avg_bytes(out[i], uv) : uv;
+    }
+    return;
+  }
+  int pu_prev[2], pv_prev[2];
+  uint32_t pu[4][2], pv[4][2];
+  auto hrow = [&](int r) {  // strip row r (-1 .. 5)
+    int hu[2], hv[2];
+    hsum(r, hu, hv);
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       if (r > -1) {
@@ -669,33 +772,48 @@ __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bi
   const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
   const LdsLuma l{w.y + 8 * gr * WL_P + (lwb & ~3)};
   const LdsChroma c{w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3)};
+  const uint8_t *lb = w.y + 8 * gr * WL_P + (lwb & ~3);
+  const int lsh = lwb & 3;  // uniform
   if (K.fx == 2 && K.fy == 2) {
-    if (k0 && k1) {
-      luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ty, acc);
-    } else {
-      uint32_t ny[8];
-      luma_rows_ctr<0, 8>(l, (uint32_t)(lwb & 3), ny, false);
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-        if (i < 4 ? k0 : k1) ty[i] = acc ? avg_bytes(ty[i], ny[i]) : ny[i];
+    switch (lsh) {
+      case 0: luma8_ctr<0>(lb, ty, acc, k0, k1); break;
+      case 1: luma8_ctr<1>(lb, ty, acc, k0, k1); break;
+      case 2: luma8_ctr<2>(lb, ty, acc, k0, k1); break;
+      default: luma8_ctr<3>(lb, ty, acc, k0, k1); break;
     }
   } else {
     int v01, v23, v45;
     tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45, 16);
     const unsigned long long th48 = (unsigned long long)(uint32_t)g_taps.luma[bipred][K.fx][0] |
                                     ((unsigned long long)(uint32_t)(g_taps.luma[bipred][K.fx][1] & 0xffff) << 32);
-    const uint8_t *lb = w.y + 8 * gr * WL_P + (lwb & ~3);
-    switch (lwb & 3) {  // uniform
-      case 0: luma8_fast<0>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
-      case 1: luma8_fast<1>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
-      case 2: luma8_fast<2>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
-      default: luma8_fast<3>(lb, th48, v01, v23, v45, ty, acc, k0, k1); break;
+#define LUMA8(SHv, X0, Y0) luma8_fast<SHv, X0, Y0>(lb, th48, v01, v23, v45, ty, acc, k0, k1)
+#define LUMA8_SH(X0, Y0)            \
+  switch (lsh) {                    \
+    case 0: LUMA8(0, X0, Y0); break; \
+    case 1: LUMA8(1, X0, Y0); break; \
+    case 2: LUMA8(2, X0, Y0); break; \
+    default: LUMA8(3, X0, Y0); break; \
+  }
+    if (K.fy == 0) {
+      if (K.fx == 0) {
+        LUMA8_SH(true, true)
+      } else {
+        LUMA8_SH(false, true)
+      }
+    } else if (K.fx == 0) {
+      LUMA8_SH(true, false)
+    } else {
+      LUMA8_SH(false, false)
     }
+#undef LUMA8_SH
+#undef LUMA8
   }
   const int cvt = g_taps.chroma[K.cfy];
-  chroma4_fast(w.u + 4 * gr * WC_P + (cwb & ~3), w.v + 4 * gr * WC_P + (cwb & ~3), cwb & 3,
-               (unsigned long long)(uint32_t)g_taps.chroma[K.cfx], tap_pair(tap8(cvt, 0), tap8(cvt, 1), 16),
-               tap_pair(tap8(cvt, 2), tap8(cvt, 3), 16), tc, acc, k0, k1);  // vertical taps x 16
+  const uint8_t *cu = w.u + 4 * gr * WC_P + (cwb & ~3), *cv = w.v + 4 * gr * WC_P + (cwb & ~3);
+  const unsigned long long tc32 = (unsigned long long)(uint32_t)g_taps.chroma[K.cfx];
+  const int c01 = tap_pair(tap8(cvt, 0), tap8(cvt, 1), 16), c23 = tap_pair(tap8(cvt, 2), tap8(cvt, 3), 16);
+  if (K.cfy == 0) chroma4_fast<true>(cu, cv, cwb & 3, tc32, c01, c23, tc, acc, k0, k1);
+  else chroma4_fast<false>(cu, cv, cwb & 3, tc32, c01, c23, tc, acc, k0, k1);  // vertical taps x 16
   (void)l;
   (void)c;
 }
@@ -929,6 +1047,9 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
     }
   }
 
+#ifdef RECON_PLAN_ONLY
+  if (f.W > 0) return;
+#endif
   // reference lookup table (packed by the host)
   if (lane < 32) *(int *)&L.lut[4 * lane] = f.slot_lut[lane];
   if (stamp) {  // debug: the frame context's scalar loads have returned

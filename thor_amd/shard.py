@@ -25,15 +25,17 @@ With halo=True (band-local only), step 4 is replaced by an MV-reach halo
 exchange at the start of the NEXT frames (variant 2): before
 a frame's step 1 every rank works out, from the frame's parse output, which
 rows of which reference frames the vectors of its band can reach (the 6-tap
-luma / 4-tap chroma footprints, both signs of each vector component), the
-requests are all-gathered, every owner sends the parts of them that lie in its
-band (point to point), and the receivers write them into their copies of the
-references (thor_dec_put_ref_rows) and re-pad those (thor_dec_pad_frame).  A
-rank then holds final pixels only for its band plus the halos its vectors
-need; per frame it moves one full-frame exchange (step 2: the whole-frame
-intra chains read across bands) plus its halos, instead of two full ones.
-Frames with a temporal-interpolated reference fetch both sources whole (the
-interpolation's motion search spans the frame).
+luma / 4-tap chroma footprints, both signs of each vector component), drops the
+rows it already holds final (its own band, and every halo it fetched before:
+RowShard.final), the remaining requests are all-gathered, every owner sends the
+parts of them that lie in its band (point to point, one grouped batch), and the
+receivers write them into their copies of the references
+(thor_dec_put_ref_rows) and re-pad those (thor_dec_pad_frame).  A rank then
+holds final pixels only for its band plus the halos its vectors need; per
+frame it moves one full-frame exchange (step 2: the whole-frame intra chains
+read across bands) plus the halo rows it does not hold yet.  Frames with a
+temporal-interpolated reference need both sources whole (the interpolation's
+motion search spans the frame) -- fetched once per source, not per frame.
 
 Band b covers SB rows [b*R, (b+1)*R), R = ceil(SB rows / world); the last band
 may run past the frame (those rows are not copied).
@@ -42,7 +44,8 @@ from __future__ import annotations
 
 import numpy as np
 
-MAX_REQ = 8  # reference ranges one rank may request per frame (4 references x 2 legs)
+MAX_REQ = 16  # reference ranges one rank may request per frame (MAX_REF_FRAMES-bounded lists: 4 references
+# x 2 legs + 2 interpolation sources fit with room); a rank over it flags the table and every rank raises
 
 
 
@@ -131,6 +134,7 @@ class RowShard:
             raise ValueError("the halo exchange replaces band-local phase B's second all-gather")
         self.halo = halo
         self.halo_bytes = []  # per frame: bytes this rank received in halo exchanges
+        self.final = {}  # halo mode: frame_num -> sorted disjoint luma row ranges this rank holds final
         self.dec, self.dist = dec, dist
         self.W, self.H = width, height
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
@@ -173,6 +177,10 @@ class RowShard:
         d = self.dec
         if self.halo:
             self._fetch_halo(frame)
+            self.final[int(frame_num)] = []  # (re)decoded: only this rank's band is final
+            lo, hi = self.owned(self.rank)
+            if hi > lo:
+                self._hold(frame_num, lo, hi)
         d.begin(devframe)
         self._exchange(frame_num)  # the bands' pre-deblock rows (inter reconstruction)
         d.end()
@@ -183,21 +191,26 @@ class RowShard:
 
     def _fetch_halo(self, frame):
         """Before `frame`'s band reconstruction: every rank's reference rows
-        within its vectors' reach, from their owners (point to point)."""
+        within its vectors' reach that it does not already hold final, from
+        their owners (point to point)."""
         import torch
 
         d, dist = self.dec, self.dist
         r0, r1 = self.owned(self.rank)
-        req = halo_requests(frame, self.H, r0, r1)
-        if len(req) > MAX_REQ:
-            raise ValueError("more than %d reference ranges in one frame" % MAX_REQ)
+        req = self.missing(halo_requests(frame, self.H, r0, r1))
         mine = np.full((MAX_REQ, 3), -1, np.int32)
-        for k, (f, (lo, hi)) in enumerate(sorted(req.items())):
-            mine[k] = (f, lo, hi)
+        if len(req) > MAX_REQ:  # flagged in the table: every rank raises after the all-gather, none blocks
+            mine[0] = (-2, len(req), 0)
+        else:
+            for k, (f, lo, hi) in enumerate(req):
+                mine[k] = (f, lo, hi)
         dev = torch.device("cuda", torch.cuda.current_device()) if self.device_exchange else None
         table = [torch.empty((MAX_REQ, 3), dtype=torch.int32, device=dev) for _ in range(self.world)]
         dist.all_gather(table, torch.from_numpy(mine).to(dev) if dev is not None else torch.from_numpy(mine))
         table = [t.cpu().numpy() for t in table]
+        over = [q for q in range(self.world) if table[q][0][0] == -2]
+        if over:
+            raise ValueError("rank(s) %s need more than %d reference ranges in one frame" % (over, MAX_REQ))
 
         def parts(q, p):  # the (frame, lo, hi) pieces rank q asked for that rank p owns
             plo, phi = self.owned(p)
@@ -210,12 +223,17 @@ class RowShard:
                     out.append((int(f), int(a), int(c)))
             return out
 
+        for p in range(self.world):  # what this rank receives is final from now on
+            if p != self.rank:
+                for f, a, c in parts(self.rank, p):
+                    self._hold(f, a, c)
         if self.device_exchange:
             self.halo_bytes.append(self._fetch_halo_device(parts, dev))
             return
         # host-staged point to point (gloo): sends from this rank's final rows, receives into
-        # numpy, then into the references in order (one staging buffer per peer, synchronised)
-        sends, recvs, got = [], [], 0
+        # numpy, one grouped batch, then into the references in order (one staging buffer per
+        # peer, synchronised)
+        ops, recvs, keep, got = [], [], [], 0
         for q in range(self.world):
             if q == self.rank:
                 continue
@@ -223,23 +241,25 @@ class RowShard:
                 buf = np.empty(rows_bytes(self.W, c - a), np.uint8)
                 d.get_rows(f, a, c - a, self.hbuf[q])
                 d.d2h(buf, self.hbuf[q])
-                sends.append((dist.isend(torch.from_numpy(buf), q), buf))
+                ops.append(dist.P2POp(dist.isend, torch.from_numpy(buf), q))
+                keep.append(buf)
         for p in range(self.world):
             if p == self.rank:
                 continue
             for f, a, c in parts(self.rank, p):
                 t = torch.empty(rows_bytes(self.W, c - a), dtype=torch.uint8)
-                recvs.append((dist.irecv(t, p), t, p, f, a, c))
+                ops.append(dist.P2POp(dist.irecv, t, p))
+                recvs.append((t, p, f, a, c))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
         padded = set()
-        for w, t, p, f, a, c in recvs:
-            w.wait()
+        for t, p, f, a, c in recvs:
             d.h2d(self.hbuf[p], t.numpy())
             d.put_ref_rows(f, a, c - a, self.hbuf[p])
             d.sync()  # the staging buffer is reused by the next piece from p
             padded.add(f)
             got += t.numel()
-        for w, _ in sends:
-            w.wait()
         for f in sorted(padded):
             d.pad_frame(f)
         self.halo_bytes.append(got)
@@ -275,47 +295,120 @@ class RowShard:
 
     def _fetch_halo_device(self, parts, dev):
         """_fetch_halo's data movement with device buffers (nccl = RCCL point
-        to point): get_rows on the decoder's stream -> event -> isend on
-        torch's stream; irecv -> event -> put_ref_rows on the decoder's
-        stream.  Returns the bytes received."""
+        to point): get_rows on the decoder's stream -> event -> one grouped
+        batch of every isend and irecv on torch's stream (dist.batch_isend_irecv,
+        i.e. one RCCL group: no send waits on a peer's unposted receive) ->
+        event -> put_ref_rows on the decoder's stream.  The staging tensors are
+        recorded on the decoder's stream, so the caching allocator keeps them
+        until its copies are done -- no host synchronisation.  Returns the
+        bytes received."""
         import torch
 
         d, dist = self.dec, self.dist
         cur = torch.cuda.current_stream()
-        sends, keep, got = [], [], 0
+        ops, recvs, keep, got = [], [], [], 0
         for q in range(self.world):
             if q == self.rank:
                 continue
             for f, a, c in parts(q, self.rank):
                 t = torch.empty(rows_bytes(self.W, c - a), dtype=torch.uint8, device=dev)
                 d.get_rows(f, a, c - a, t.data_ptr())
-                if self.dstream is not None:
-                    ev = torch.cuda.Event()
-                    ev.record(self.dstream)
-                    cur.wait_event(ev)
-                sends.append(dist.isend(t, q))
+                ops.append(dist.P2POp(dist.isend, t, q))
                 keep.append(t)
-        recvs = []
         for p in range(self.world):
             if p == self.rank:
                 continue
             for f, a, c in parts(self.rank, p):
                 t = torch.empty(rows_bytes(self.W, c - a), dtype=torch.uint8, device=dev)
-                recvs.append((dist.irecv(t, p), t, f, a, c))
-        padded = set()
-        for w, t, f, a, c in recvs:
+                ops.append(dist.P2POp(dist.irecv, t, p))
+                recvs.append((t, f, a, c))
+                keep.append(t)
+        if not ops:
+            return 0
+        if self.dstream is not None:  # the sent rows are staged before the group reads them
+            ev = torch.cuda.Event()
+            ev.record(self.dstream)
+            cur.wait_event(ev)
+        for w in dist.batch_isend_irecv(ops):
             w.wait()
-            if self.dstream is not None:
-                ev = torch.cuda.Event()
-                ev.record(cur)
-                self.dstream.wait_event(ev)
+        if self.dstream is not None:  # the received rows land before the decoder stream reads them
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.dstream.wait_event(ev)
+        padded = set()
+        for t, f, a, c in recvs:
             d.put_ref_rows(f, a, c - a, t.data_ptr())
-            keep.append(t)
             padded.add(f)
             got += t.numel()
-        for w in sends:
-            w.wait()
         for f in sorted(padded):
             d.pad_frame(f)
-        d.sync()  # the staging tensors may be freed
+        if self.dstream is not None:
+            for t in keep:  # freed only after the decoder stream's copies
+                t.record_stream(self.dstream)
+        else:
+            d.sync()  # no stream to record on: the staging tensors may be freed after this
         return got
+
+    # ---- which rows of which frames this rank holds final (halo mode) ----
+    def _hold(self, f: int, a: int, c: int):
+        iv = self.final.setdefault(int(f), [])
+        iv.append((int(a), int(c)))
+        iv.sort()
+        merged = []
+        for lo, hi in iv:
+            if merged and lo <= merged[-1][1]:
+                merged[-1] = (merged[-1][0], max(merged[-1][1], hi))
+            else:
+                merged.append((lo, hi))
+        self.final[int(f)] = merged
+
+    def missing(self, req):
+        """[(frame, lo, hi)]: the parts of the requested row ranges {frame: (lo,
+        hi)} this rank does not hold final yet (even-aligned, sorted)."""
+        out = []
+        for f, (lo, hi) in sorted(req.items()):
+            cur = lo
+            for a, c in self.final.get(int(f), []):
+                if c <= cur or a >= hi:
+                    continue
+                if a > cur:
+                    out.append((int(f), cur, min(a, hi)))
+                cur = max(cur, c)
+                if cur >= hi:
+                    break
+            if cur < hi:
+                out.append((int(f), cur, hi))
+        return [(f, a & ~1, (c + 1) & ~1) for f, a, c in out]
+
+    def assemble(self, frame_num: int) -> bytes:
+        """The whole frame (I420 bytes) from its bands' owners (one all-gather;
+        a check outside any timed region -- in halo mode no rank holds every
+        row final)."""
+        import torch
+
+        d, W, H, world = self.dec, self.W, self.H, self.world
+        mine = np.zeros(self.nbytes, np.uint8)
+        lo, hi = self.owned(self.rank)
+        if hi > lo:
+            buf = d.scratch(self.nbytes)
+            d.get_rows(frame_num, lo, self.rows, buf)
+            d.d2h(mine, buf)
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.device_exchange else None
+        src = torch.from_numpy(mine).to(dev) if dev is not None else torch.from_numpy(mine)
+        parts = [torch.empty(self.nbytes, dtype=torch.uint8, device=dev) for _ in range(world)]
+        self.dist.all_gather(parts, src)
+        y = np.zeros((H, W), np.uint8)
+        u = np.zeros((H // 2, W // 2), np.uint8)
+        v = np.zeros((H // 2, W // 2), np.uint8)
+        for r in range(world):
+            a, b = self.owned(r)
+            n = b - a
+            if n <= 0:
+                continue
+            p = parts[r].cpu().numpy()
+            y[a:b] = p[:n * W].reshape(n, W)
+            o = self.rows * W
+            for pl in (u, v):
+                pl[a // 2:b // 2] = p[o:o + (n // 2) * (W // 2)].reshape(n // 2, W // 2)
+                o += (self.rows // 2) * (W // 2)
+        return y.tobytes() + u.tobytes() + v.tobytes()

@@ -125,8 +125,13 @@ def synth_frames(width: int, height: int, frames: int, seed: int = 1, workers: i
         return np.stack([_i420(a) for a in args])
     import multiprocessing as mp
 
-    with mp.get_context("fork").Pool(min(workers, frames)) as pool:
-        return np.stack(pool.map(_i420, args))
+    pool = mp.get_context("fork").Pool(min(workers, frames))
+    try:
+        out = np.stack(pool.map(_i420, args))
+    finally:
+        pool.close()  # workers exit on their own (the `with` block's terminate() SIGTERMs them, which
+        pool.join()   # profilers log as aborts)
+    return out
 
 
 def synth_clip(width: int, height: int, frames: int, seed: int = 1) -> bytes:
