@@ -172,6 +172,51 @@ def encoder_leg(torch, lib, reps: int = 10):
             "note": "RD candidate evaluation throughput of the encoder TU chain; not part of `value`"}
 
 
+def config3_leg(torch, lib, streams: int = 64, nf: int = 2):
+    """BASELINE config 3 -- 1080p config_LDB_high_efficiency, the full encoder
+    RD loop on the GPU (encoder_speed 0: exact sub-pel ME, tb / pb split,
+    4 references, delta-QP RD) -- as a throughput leg beside `value`: `streams`
+    independent contexts coding the first `nf` frames (the I frame, then P) of
+    the seeded 1080p clip tests/golden/hd_high was encoded from, one
+    thor_enc_frames launch set per frame for all of them.  Every stream's .bit
+    must equal the reference Thorenc's (tests/golden/hd_high.bit) byte for byte.
+    The reference's own figure on this config (0.046 Mpx/s, one
+    core, 17 frames) is quoted beside it, with 16 cores taken as 16x that."""
+    from thor_amd import synth
+    from thor_amd.encoder import GpuEncoder, encode_batch, params_for
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold, "streams.json")))["hd_high"]
+    w, h = meta["width"], meta["height"]
+    clip = synth.synth_frames(w, h, nf, meta["seed"], workers=1)  # serial: this process owns the GPU
+    want = open(os.path.join(gold, "hd_high.bit"), "rb").read()
+    encs = [GpuEncoder(params_for(meta["config"], w, h, nf, meta["extra"])) for _ in range(streams)]
+    try:
+        for e in encs:
+            e.upload_sequence(clip)
+        torch.cuda.synchronize()
+        out = [b""] * streams
+        frame_s = []
+        for _ in range(nf):
+            t0 = time.perf_counter()
+            ch = encode_batch(encs)
+            frame_s.append(time.perf_counter() - t0)
+            for k in range(streams):
+                out[k] += ch[k]
+        ok = all(want.startswith(o) and len(o) > 0 for o in out) and len(set(out)) == 1
+    finally:
+        for e in encs:
+            e.close()
+    t = sum(frame_s)
+    mpx = streams * w * h * nf / t / 1e6
+    ref1 = 0.046  # BASELINE.md, config_LDB_high_efficiency 1080p x 17, SIMD build, one core
+    return {"workload": "%d streams x %d frames of 1080p config_LDB_high_efficiency (I + P, encoder_speed 0), "
+                        "encode only, thor_enc_frames batches" % (streams, nf),
+            "mpx_s": round(mpx, 3), "seconds": round(t, 3), "frame_s": [round(x, 3) for x in frame_s],
+            "bit_exact": ok, "reference_single_core_mpx_s": ref1, "reference_16_core_mpx_s": round(16 * ref1, 3),
+            "x_16_reference_cores": round(mpx / (16 * ref1), 2)}
+
+
 def pyramid_leg(torch, lib, reps: int = 50):
     """Temporal-interpolation luma pyramid (thor_scale_pyramid2, the chains of
     scale_frame_down2x2_simd calls of common/temporal_interp.c:1011-1019) on
@@ -483,6 +528,11 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config3-streams", type=int, default=64,
+                    help="streams of the BASELINE config-3 encoder leg (1080p LDB high efficiency)")
+    ap.add_argument("--drop-in", nargs="?", const="hd_low", default=None, metavar="STREAM",
+                    help="time the reference decoder's host C on this library's per-call surface "
+                         "(oracle/_ref/thordec_amd) beside the reference Thordec on a golden .bit (default hd_low)")
     ap.add_argument("--no-legs", action="store_true", help="skip the kernel legs reported beside `value`")
     ap.add_argument("--dec-slots", type=int, default=10,
                     help="reference ring slots per decoder context (LDB: up to 4 references + the current frame)")
@@ -509,6 +559,8 @@ def main():
         sys.exit(launch_ranks(a.gpus))
     if a.launcher_selftest:
         return launcher_selftest(a)
+    if a.drop_in:
+        return dropin_mode(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -731,6 +783,10 @@ def main():
     for _ in range(max(1, a.warmup)):
         _, bits, devs = step_pipe(allk)
     bit_exact = bits_ok(allk, bits) and decoded_ok(allk)
+    rf_early = None
+    if os.environ.get("THOR_BENCH_RF_EARLY"):  # diagnostic: the roofline pass before the timed steps too
+        _, rf_early, _, _ = roofline_pass(lib, decs, [groups[0]], devs, [parse_stream(bits[k])[1] for k in groups[0]],
+                                          seq, 3)
 
     if dist is not None:
         dist.barrier()
@@ -844,6 +900,7 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": round(alg),
                 "avg_launch_us": round(recon_ms * 1e3, 2),
+                **({"avg_launch_us_before_steps": round(rf_early * 1e3, 2)} if rf_early is not None else {}),
                 "frames_per_launch": B,
                 "launches": "batched P-frame decode launches of group 0 alone (streams of clips 0..7, the inter "
                             "stage: one k_recon launch -- 128x16 units, the frames' multi-key units first); "
@@ -859,6 +916,7 @@ def main():
             out["temporal_pyramid"] = pyramid_leg(torch, lib)
             out["temporal_interp_comp"] = interp_leg(torch, lib)
             out["temporal_interp_frame"] = interp_frames_leg(torch, lib, clips[0])
+            out["config3_encoder"] = config3_leg(torch, lib, a.config3_streams)
         if not a.no_cpu_baseline and world == 1:
             cb = cpu_baseline(bc, clips_meta, clips)
             if cb is not None:
@@ -869,6 +927,44 @@ def main():
         x.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def dropin_mode(a):
+    """--drop-in: the reference decoder's own host C linked against this
+    library's SIMD-surface / L2 entry points (oracle/_ref/thordec_amd: every
+    per-block kernel call of dec/decode_block.c:48-453 and the frame deblock
+    runs on the GPU, one small launch per call) timed beside the reference
+    Thordec (SIMD build, one core) on the same .bit; both outputs md5-checked
+    against the reference decoder's.  The per-call surface exists for drop-in
+    compatibility; the batched decoder (thor_dec_frames) is the throughput API."""
+    gold = os.path.join(ROOT, "tests", "golden")
+    name = a.drop_in
+    meta = json.load(open(os.path.join(gold, "streams.json")))[name]
+    bit = os.path.join(gold, name + ".bit")
+    out = {"metric": "Mpixels/s decode, %s (%dx%d x %d frames) through the reference decoder host C" % (
+        name, meta["width"], meta["height"], meta["frames"]), "unit": "Mpixels/s", "higher_is_better": True}
+    px = meta["width"] * meta["height"] * meta["frames"]
+    import tempfile
+
+    for key, exe in (("reference_thordec_simd_1core", "Thordec"), ("thordec_amd_gpu_surface", "thordec_amd")):
+        path = os.path.join(ROOT, "oracle", "_ref", exe)
+        if not os.path.exists(path):
+            out[key] = None
+            continue
+        with tempfile.TemporaryDirectory() as td:
+            dec = os.path.join(td, "dec.yuv")
+            best = None
+            for _ in range(a.steps):
+                t0 = time.perf_counter()
+                subprocess.run([path, bit, dec], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            ok = hashlib.md5(open(dec, "rb").read()).hexdigest() == meta["dec_md5"]
+        out[key] = {"seconds": round(best, 3), "mpx_s": round(px / best / 1e6, 3), "bit_exact": ok}
+    r, g = out.get("reference_thordec_simd_1core"), out.get("thordec_amd_gpu_surface")
+    if r and g:
+        out["gpu_surface_vs_reference"] = round(r["seconds"] / g["seconds"], 4)
+    print(json.dumps(out), flush=True)
 
 
 def rows_mode(a, torch, dist, rank, world, local):

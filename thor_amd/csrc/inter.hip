@@ -97,6 +97,19 @@ struct TapTables {
   }
 };
 __constant__ TapTables g_taps = TapTables();
+// The same words as scalar selects of compile-time constants (no table load on
+// the fast path: a load there is one more dependent round trip before the
+// window staging can start).
+constexpr TapTables k_taps = TapTables();
+__device__ __forceinline__ int luma_word(int bipred, int f, int w) {
+  const int u = f == 1 ? k_taps.luma[0][1][w] : f == 2 ? k_taps.luma[0][2][w] : f == 3 ? k_taps.luma[0][3][w] : k_taps.luma[0][0][w];
+  const int b = f == 1 ? k_taps.luma[1][1][w] : f == 2 ? k_taps.luma[1][2][w] : f == 3 ? k_taps.luma[1][3][w] : k_taps.luma[1][0][w];
+  return bipred ? b : u;
+}
+__device__ __forceinline__ int chroma_word(int f) {
+  return f == 1 ? k_taps.chroma[1] : f == 2 ? k_taps.chroma[2] : f == 3 ? k_taps.chroma[3] : f == 4 ? k_taps.chroma[4]
+       : f == 5 ? k_taps.chroma[5] : f == 6 ? k_taps.chroma[6] : f == 7 ? k_taps.chroma[7] : k_taps.chroma[0];
+}
 
 // Rounding constant of the 2-D filters with the (p - 128) bias folded in:
 // 2048 + 128 * 64 * 64 (every tap set sums to 64).
@@ -432,12 +445,12 @@ __device__ __forceinline__ void win_issue(WinLoad &W, const FrameCtx &f, __amdgp
   for (int i = 0; i < WIN_LOADS; i++) {
     const int q = lane + 64 * i;
     int offl = 0, offc = 0;
-    if (64 * i < WL_CH) offl = ly + 16 * q + ((q * 205) >> 11) * syd;  // q / 10, exact for q < 1029
+    if (64 * i < WL_CH) offl = ly + 16 * q + __mul24((q * 205) >> 11, syd);  // q / 10, exact for q < 1029 (24-bit mad)
     if (64 * i + 63 >= WL_CH) {
       const int q2 = q - WL_CH;  // chroma chunk: U 0..65, V 66..131
       const bool pv = q2 >= WC_CH;
       const int q3 = pv ? q2 - WC_CH : q2;
-      offc = cu + 16 * q2 + (pv ? uvd : 0) + ((q3 * 171) >> 10) * scd;  // q3 / 6, exact for q3 < 256
+      offc = cu + 16 * q2 + (pv ? uvd : 0) + __mul24((q3 * 171) >> 10, scd);  // q3 / 6, exact for q3 < 256
     }
     int off = 64 * i + 63 < WL_CH ? offl : (64 * i >= WL_CH ? offc : (q < WL_CH ? offl : offc));
 #if RECON_PROBE == 1  // timing probe: the same bytes as whole 128-B lines, 8 rows per load (wrong output)
@@ -783,9 +796,9 @@ __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bi
     }
   } else {
     int v01, v23, v45;
-    tap_pairs6(g_taps.luma[bipred][K.fy][0], g_taps.luma[bipred][K.fy][1], v01, v23, v45, 16);
-    const unsigned long long th48 = (unsigned long long)(uint32_t)g_taps.luma[bipred][K.fx][0] |
-                                    ((unsigned long long)(uint32_t)(g_taps.luma[bipred][K.fx][1] & 0xffff) << 32);
+    tap_pairs6(luma_word(bipred, K.fy, 0), luma_word(bipred, K.fy, 1), v01, v23, v45, 16);
+    const unsigned long long th48 = (unsigned long long)(uint32_t)luma_word(bipred, K.fx, 0) |
+                                    ((unsigned long long)(uint32_t)(luma_word(bipred, K.fx, 1) & 0xffff) << 32);
 #define LUMA8(SHv, X0, Y0) luma8_fast<SHv, X0, Y0>(lb, th48, v01, v23, v45, ty, acc, k0, k1)
 #define LUMA8_SH(X0, Y0)            \
   switch (lsh) {                    \
@@ -808,9 +821,9 @@ __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bi
 #undef LUMA8_SH
 #undef LUMA8
   }
-  const int cvt = g_taps.chroma[K.cfy];
+  const int cvt = chroma_word(K.cfy);
   const uint8_t *cu = w.u + 4 * gr * WC_P + (cwb & ~3), *cv = w.v + 4 * gr * WC_P + (cwb & ~3);
-  const unsigned long long tc32 = (unsigned long long)(uint32_t)g_taps.chroma[K.cfx];
+  const unsigned long long tc32 = (unsigned long long)(uint32_t)chroma_word(K.cfx);
   const int c01 = tap_pair(tap8(cvt, 0), tap8(cvt, 1), 16), c23 = tap_pair(tap8(cvt, 2), tap8(cvt, 3), 16);
   if (K.cfy == 0) chroma4_fast<true>(cu, cv, cwb & 3, tc32, c01, c23, tc, acc, k0, k1);
   else chroma4_fast<false>(cu, cv, cwb & 3, tc32, c01, c23, tc, acc, k0, k1);  // vertical taps x 16
@@ -907,6 +920,18 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
   u = __builtin_amdgcn_readfirstlane(u);  // uniform (the scalar loads below need it in SGPRs)
   fi = __builtin_amdgcn_readfirstlane(fi);
   const FrameCtx &f = F[fi];
+  {  // every frame-context word the kernel reads, fetched together: one scalar-load round trip
+     // instead of a chain of them spread over the branches below (the empty asm needs them all)
+    const uint8_t *a0 = f.slots, *a1 = f.cy, *a2 = f.edge;
+    const uint4 *a3 = f.hplan;
+    const int16_t *a4 = f.resid;
+    const long long b0 = f.slot_bytes, b1 = f.ring_bytes, b2 = f.offy, b3 = f.offu, b4 = f.offv;
+    const int c0 = f.nblocks, c1 = f.band0, c2 = f.band1, c3 = f.gen, c4 = f.sy, c5 = f.sc, c6 = f.bipred, c7 = f.W,
+              c8 = f.H, c9 = f.ewy, c10 = f.ewc, c11 = f.nsbrows;
+    asm volatile("" ::"s"(a0), "s"(a1), "s"(a2), "s"(a3), "s"(a4), "s"(b0), "s"(b1), "s"(b2), "s"(b3), "s"(b4), "s"(c0),
+                 "s"(c1), "s"(c2), "s"(c3), "s"(c4), "s"(c5), "s"(c6), "s"(c7), "s"(c8), "s"(c9), "s"(c10), "s"(c11),
+                 "s"(dbg));
+  }
   if (f.nblocks <= 0) return;
   if (fi) dbg = nullptr;
   int16_t *__restrict__ resid = f.resid;
@@ -1025,7 +1050,8 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
       const __amdgpu_buffer_rsrc_t cur =
           __builtin_amdgcn_make_buffer_rsrc((void *)(f.cy - f.offy), 0, (int)f.slot_bytes, 0x00020000);
       const int oy = (int)f.offy + (y0 + r) * f.sy + xl;
-      const int oc = (int)(pl1 ? f.offv : f.offu) + yc * f.sc + xcl;
+      const int offu = __builtin_amdgcn_readfirstlane((int)f.offu), offv = __builtin_amdgcn_readfirstlane((int)f.offv);
+      const int oc = (pl1 ? offv : offu) + yc * f.sc + xcl;  // (a select of scalars, not a per-lane load of the field)
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #if RECON_PROBE == 3  // timing probe: no pixel stores (wrong output)
       if (f.W > 0) return;

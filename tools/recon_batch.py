@@ -24,6 +24,8 @@ B = int(args[1]) if len(args) > 1 else 8
 reps = int(args[2]) if len(args) > 2 else 2
 timing = "--time" in sys.argv
 seq, frames = load_trace(os.path.join(ROOT, "tests", "golden", name + ".trc.z"))
+# RB_EXTRA=N: N more (idle) decoder contexts allocated first -- the bench's memory footprint
+extra = [GpuDecoder(seq, slots=10) for _ in range(int(os.environ.get("RB_EXTRA", "0")))]
 decs = [GpuDecoder(seq, slots=10) for _ in range(B)]
 for d in decs[1:]:
     d.set_stream(C.c_void_p(decs[0].stream()))
