@@ -546,6 +546,9 @@ def main():
     ap.add_argument("--halo", action="store_true",
                     help="--shard rows, band-local: no second all-gather; each rank fetches the reference rows its "
                          "band's vectors reach (MV-reach halo exchange, thor_amd/shard.py)")
+    ap.add_argument("--boundary", action="store_true",
+                    help="--shard rows with the halo exchange and no pre-deblock all-gather either: edge rows for "
+                         "each band's intra chains from the band above, 8 deblocking halo rows either side")
     ap.add_argument("--shard", choices=["streams", "rows"], default="streams",
                     help="streams: independent enc+dec streams per GPU (default); rows: decode-only, ONE "
                          "stream's SB rows split across the ranks with an RCCL all-gather before intra/deblock")
@@ -987,8 +990,8 @@ def rows_mode(a, torch, dist, rank, world, local):
     seq, frames = load_trace(os.path.join(gold, "k4_low.trc.z"))
     dec = GpuDecoder(seq, device=local)
     devs = [dec.upload(fr) for fr in frames]
-    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=a.band_local or a.halo,
-                  halo=a.halo)
+    sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True,
+                  band_local=a.band_local or a.halo or a.boundary, halo=a.halo or a.boundary, boundary=a.boundary)
 
     def step():
         for d, fr in zip(devs, frames):
@@ -999,7 +1002,8 @@ def rows_mode(a, torch, dist, rank, world, local):
     torch.cuda.synchronize(local)
     # halo mode: no rank holds every row final -- each frame is put together from
     # its bands' owners (outside the timed region)
-    got = {fr.frame_num: sh.assemble(fr.frame_num) if a.halo else dec.read_i420(fr.frame_num) for fr in frames}
+    got = {fr.frame_num: sh.assemble(fr.frame_num) if (a.halo or a.boundary) else dec.read_i420(fr.frame_num)
+           for fr in frames}
     ok = hashlib.md5(b"".join(got[k] for k in sorted(got))).hexdigest() == meta["dec_md5"]
     dist.barrier()
     torch.cuda.synchronize(local)
@@ -1021,11 +1025,14 @@ def rows_mode(a, torch, dist, rank, world, local):
             "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u8/i16", "data": "synthetic (seeded clip) encoded by the reference Thorenc",
             "bit_exact": ok,
-            "config": {"workload": "ONE 4K 8-frame LDB-low stream, SB rows sharded across %d GPU(s): band k_recon, "
-                                   "RCCL all-gather of pre-deblock bands, whole-frame intra, %s" % (
-                                   world, "band-local deblock/CLPF, pad, MV-reach halo exchange of reference rows"
-                                   if a.halo else "band-local deblock/CLPF + all-gather of final bands, pad"
-                                   if a.band_local else "whole-frame deblock/CLPF/pad"),
+            "config": {"workload": "ONE 4K 8-frame LDB-low stream, SB rows sharded across %d GPU(s): band k_recon, %s" % (
+                                   world, "band intra, boundary exchange (edge rows for the intra chains, 8-row "
+                                   "deblocking halos; no all-gather), band-local deblock/CLPF, MV-reach halo exchange "
+                                   "of reference rows" if a.boundary
+                                   else "RCCL all-gather of pre-deblock bands, whole-frame intra, " + (
+                                       "band-local deblock/CLPF, pad, MV-reach halo exchange of reference rows"
+                                       if a.halo else "band-local deblock/CLPF + all-gather of final bands, pad"
+                                       if a.band_local else "whole-frame deblock/CLPF/pad")),
                        "parallelism": "rows%d" % world, "frames": len(frames)},
         }), flush=True)
     dec.close()

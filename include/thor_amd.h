@@ -165,9 +165,9 @@ int thor_dec_frames(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, 
  * bands (thor_dec_get_rows / thor_dec_put_rows on DEVICE buffers, e.g. an RCCL
  * all-gather on the same stream); thor_dec_frame_end enqueues intra, deblock,
  * CLPF and padding of the whole frame.  Rows are packed Y (nrows x W) | U |
- * V (nrows/2 x W/2 each); put_rows needs y0 on an SB row and also refreshes
- * the SB-row edge rows the intra chains read.  Rows past the frame are
- * skipped. */
+ * V (nrows/2 x W/2 each); put_rows (y0, nrows even) also refreshes the
+ * SB-row edge rows the intra chains read for every SB row whose bottom row it
+ * carries.  Rows past the frame are skipped. */
 int thor_dec_set_band(thor_dec_t *d, int sb_row0, int sb_row1);
 int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_frame_in_t *in);
 int thor_dec_frame_end(thor_dec_t *d);
@@ -182,6 +182,17 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
  * rank's loop filters then cover 1/N of the frame instead of all of it. */
 int thor_dec_set_band_local(thor_dec_t *d, int on);
 int thor_dec_frame_finish(thor_dec_t *d);
+/* Band-local intra (on = 1, with a band set; the boundary exchange of
+ * thor_amd/shard.py, which replaces the pre-deblock all-gather): the intra
+ * chains of the band's SB rows only, the first of them reading the row above
+ * from the edge rows (thor_dec_put_rows of the two luma rows ending the SB row
+ * above, from the rank that owns it) instead of waiting for it.
+ * thor_dec_frame_intra enqueues that intra stage between thor_dec_frame_begin
+ * and thor_dec_frame_end (which then skips it), so the caller can hand the
+ * band's bottom edge rows to the rank below and exchange the deblocking halo
+ * rows (8 above, 8 below the band) after it. */
+int thor_dec_set_band_intra(thor_dec_t *d, int on);
+int thor_dec_frame_intra(thor_dec_t *d);
 /* MV-reach halo exchange (band-local contexts, thor_amd/shard.py halo mode):
  * instead of all-gathering every band's final rows, each rank fetches, before
  * a frame's thor_dec_frame_begin, only the rows of its references that the

@@ -14,7 +14,7 @@ from conftest import GOLD
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, name, nframes, q, local=False, halo=False):
+def _worker(rank, world, port, name, nframes, q, local=False, halo=False, boundary=False):
     import hashlib
 
     import torch.distributed as dist
@@ -38,7 +38,8 @@ def _worker(rank, world, port, name, nframes, q, local=False, halo=False):
             seq, frames = load_trace(trace_path(name))
         frames = frames[:nframes]
         dec = GpuDecoder(seq)
-        sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=False, band_local=local, halo=halo)
+        sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=False, band_local=local, halo=halo,
+                      boundary=boundary)
         bad = []
         for fr in frames:
             sh.decode(dec.upload(fr), fr.frame_num, fr)
@@ -50,6 +51,8 @@ def _worker(rank, world, port, name, nframes, q, local=False, halo=False):
         if halo:  # the halo bytes this rank received per frame vs one full-frame exchange
             print("rank %d halo bytes per frame %s (full frame %d)" % (
                 rank, sh.halo_bytes, seq.width * seq.height * 3 // 2), flush=True)
+        if boundary:
+            print("rank %d boundary bytes per frame %s" % (rank, sh.boundary_bytes), flush=True)
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, bad))
@@ -77,7 +80,15 @@ def test_row_sharded_halo_exchange_matches_reference(name, nframes, world):
     _run_sharded(name, nframes, world, True, True)
 
 
-def _run_sharded(name, nframes, world, local, halo):
+# Boundary exchange (no pre-deblock all-gather either): edge rows for the band's intra
+# chains from the band above, 8 deblocking halo rows either side (thor_amd/shard.py)
+@pytest.mark.parametrize("name,nframes,world", [("k4_med", 8, 2), ("k4_med", 8, 3), ("cif_high", 10, 3),
+                                                ("hd_low", 6, 2), ("cif_hdbi", 9, 2), ("k4_hdbi", 9, 3)])
+def test_row_sharded_boundary_exchange_matches_reference(name, nframes, world):
+    _run_sharded(name, nframes, world, True, True, True)
+
+
+def _run_sharded(name, nframes, world, local, halo, boundary=False):
     import random
     import sys
 
@@ -87,7 +98,8 @@ def _run_sharded(name, nframes, world, local, halo):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, nframes, q, local, halo)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, nframes, q, local, halo, boundary))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=110) for _ in procs)

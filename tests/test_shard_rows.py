@@ -37,6 +37,25 @@ class NumpyContext:
         self.bufs = {}
         self.refs = {}
         self.frames = {}  # halo mode: parse-output stand-ins, to check the fetched rows
+        self.band_intra = False  # boundary mode: intra of the band only, rows above via the edge exchange
+        self.intra_done = False
+
+    def set_band_intra(self, on):
+        self.band_intra = on
+
+    def intra(self):
+        """The band's intra chains: the first one reads the two rows above the
+        band, which must be final by now when the band holds intra CUs."""
+        fnum, planes = self.cur
+        r0 = 64 * self.band[0]
+        fr = self.frames.get(fnum)
+        if fr is not None and r0 > 0 and len(fr.blocks):
+            rows = fr.blocks["ypos"][fr.blocks["mode"] == 1].astype(np.int64) >> 6
+            if np.any((rows >= self.band[0]) & (rows < self.band[1])):
+                assert np.array_equal(planes[0][r0 - 2:r0], self.truth[fnum][0][r0 - 2:r0]), (fnum, "edge rows")
+                for k in (1, 2):
+                    assert np.array_equal(planes[k][r0 // 2 - 1], self.truth[fnum][k][r0 // 2 - 1]), (fnum, k)
+        self.intra_done = True
 
     def set_band(self, b0, b1):
         self.band = (b0, b1)
@@ -77,7 +96,7 @@ class NumpyContext:
             o += (n // 2) * (W // 2)
 
     def put_rows(self, fnum, y0, n, key):
-        assert fnum == self.cur[0] and y0 % 64 == 0
+        assert fnum == self.cur[0] and y0 % 2 == 0
         buf, (y, u, v) = self.bufs[key], self.cur[1]
         m = max(0, min(n, self.H - y0))
         W = self.W
@@ -95,8 +114,16 @@ class NumpyContext:
 
     def end(self):
         fnum, planes = self.cur
-        for got, want in zip(planes, self.truth[fnum]):
-            assert np.array_equal(got, want), fnum
+        if self.band_intra:  # boundary mode: the band, its intra done, and 8 halo rows either side are final
+            assert self.intra_done
+            self.intra_done = False
+            r0, r1 = max(0, 64 * self.band[0] - 8), min(self.H, 64 * self.band[1] + 8)
+            for k, (got, want) in enumerate(zip(planes, self.truth[fnum])):
+                a, b = (r0, r1) if k == 0 else (r0 // 2, r1 // 2)
+                assert np.array_equal(got[a:b], want[a:b]), (fnum, k, a, b)
+        else:
+            for got, want in zip(planes, self.truth[fnum]):
+                assert np.array_equal(got, want), fnum
         if self.local:  # band-local phase B: only the band's rows are final, model the rest as stale
             r0, r1 = 64 * self.band[0], min(64 * self.band[1], self.H)
             for k, p in enumerate(planes):
@@ -390,3 +417,75 @@ def test_row_shard_halo_request_overflow_raises_everywhere_gloo():
     every rank raises after the all-gather instead of one rank raising before it
     and the others blocking in the collective."""
     _run_world(_halo_overflow_worker, 2, 192, 320, "raised")
+
+
+def _boundary_worker(rank, world, port, W, H, q):
+    import torch.distributed as dist
+
+    from thor_amd.shard import RowShard, rows_bytes
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(13)
+        nf = 6
+        truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
+                     rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(nf)}
+        frames = {f: FakeFrame(f, W, H, rng, reach=6) for f in range(nf)}
+        # intra CUs: every SB row of frame 0 (an I frame's serial chain across the bands), then
+        # frame-dependent rows -- some bands' last rows ("late" edge), some first rows only ("early")
+        for f in range(nf):
+            b = frames[f].blocks
+            if len(b) == 0:
+                continue
+            rows = b["ypos"].astype(np.int64) >> 6
+            pick = np.isin(rows, [(f + k) % ((H + 63) // 64) for k in (0, 2)])
+            b["mode"][pick & (np.arange(len(b)) % 2 == 0)] = 1
+        ctx = NumpyContext(W, H, truth)
+        ctx.halo = True
+        ctx.frames = frames
+        sh = RowShard(ctx, dist, W, H, device_exchange=False, band_local=True, halo=True, boundary=True)
+        for f in range(nf):
+            sh.decode(f, f, frames[f])
+        full = rows_bytes(W, H)
+        assert max(sh.boundary_bytes) < full // 4, (sh.boundary_bytes, full)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-800:]))
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 192, 320), (3, 128, 448)])
+def test_row_shard_boundary_exchange_gloo(world, W, H):
+    """Boundary mode: no pre-deblock all-gather -- the band below gets the two
+    edge rows of the band above (after that band's intra chains when its last
+    SB row holds intra CUs) before its own intra, then 8 deblocking halo rows
+    either side; NumpyContext checks the edge rows at intra time and the band
+    plus halos at deblocking time."""
+    _run_world(_boundary_worker, world, W, H, "ok")
+
+
+def test_boundary_plan():
+    from thor_amd.shard import RowShard
+
+    class D:
+        def get_rank(self):
+            return 1
+
+        def get_world_size(self):
+            return 3
+
+    sh = object.__new__(RowShard)
+    sh.H, sh.world, sh.rank = 448, 3, 1  # 7 SB rows, bands of 3: [0,3) [3,6) [6,7)
+    fr = FakeFrame(1, 128, 448, np.random.default_rng(0), reach=2)
+    fr.blocks["mode"][:] = 2
+    assert sh.boundary_plan(fr) == {}
+    rows = fr.blocks["ypos"] >> 6
+    fr.blocks["mode"][np.flatnonzero(rows == 3)[:1]] = 1  # band 1's first row: band 0 hands over early
+    assert sh.boundary_plan(fr) == {0: "early"}
+    fr.blocks["mode"][np.flatnonzero(rows == 2)[:1]] = 1  # band 0's last row has intra: late
+    fr.blocks["mode"][np.flatnonzero(rows == 6)[:1]] = 1  # band 2 has intra; band 1's last row (5) none
+    assert sh.boundary_plan(fr) == {0: "late", 1: "early"}

@@ -66,6 +66,7 @@ struct thor_dec {
   int stop_stage;
   hipEvent_t xev[2];  // cross-stream ordering when a batch mixes contexts on different streams
   int band0, band1;    // SB rows k_recon reconstructs (row sharding); band1 0 = all
+  int band_intra;      // row sharding: the intra chains of the band's rows only (thor_dec_set_band_intra)
   int band_local;      // phase B filters only the band's rows (thor_dec_set_band_local)
   void *pending;       // Batch of a thor_dec_frame_begin awaiting its _end (or, band-local, its _finish)
   int pending_ended;   // band-local: _end done, _finish (pad + commit) due
@@ -200,6 +201,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->xev[0] = d->xev[1] = nullptr;
   d->band0 = d->band1 = 0;
   d->band_local = 0;
+  d->band_intra = 0;
   d->pending_ended = 0;
   d->pending = nullptr;
   d->ev_used = 0;
@@ -399,6 +401,7 @@ struct Batch {
   // interpolated reference per frame: source slots (-1: none) and interpolate_frames' (ratio, pos)
   int ia[THOR_MAX_BATCH], ib[THOR_MAX_BATCH], iratio[THOR_MAX_BATCH], ipos[THOR_MAX_BATCH];
   int max_prep, any_intra, any_clpf, any_deblock, clpf_grid, max_intra;
+  int intra_done;  // thor_dec_frame_intra ran the intra stage already
 };
 
 static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *hdrs, const thor_frame_in_t *ins,
@@ -417,6 +420,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
   }
   memset(&b.fb, 0, sizeof(b.fb));
   b.n = n;
+  b.intra_done = 0;
   b.max_prep = 1;
   b.any_intra = b.any_clpf = b.any_deblock = 0;
   b.clpf_grid = 0;
@@ -462,6 +466,13 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.band0 = d->band0;
     f.band1 = d->band1 > 0 ? d->band1 : f.nsbrows;
     f.pb0 = f.pb1 = 0;
+    f.ir0 = 0;
+    f.ir1 = 0;
+    if (d->band_intra && d->band1 > 0) {
+      f.ir0 = d->band0;
+      f.ir1 = d->band1 > d->band0 ? d->band1 : d->band0;
+      if (f.ir1 == f.ir0) f.nintra = 0;  // an empty band: no chains
+    }
     if (d->band_local && d->band1 > 0) {
       f.pb0 = d->band0 * 64;
       f.pb1 = d->band1 * 64 < H ? d->band1 * 64 : H;
@@ -545,17 +556,24 @@ static int batch_phase_a(thor_dec *lead, const Batch &b) {
 
 // Phase B: intra, deblock, CLPF, reference padding (pad = 0: the band-local
 // form, padded by thor_dec_frame_finish after the final-rows exchange).
-static int batch_phase_b(thor_dec *lead, const Batch &b, int pad = 1) {
+static int batch_intra(thor_dec *lead, const Batch &b) {
   const int W = lead->seq.width, H = lead->seq.height, n = b.n;
-  hipStream_t st = lead->stream;
   const int nrows = (H + 63) / 64;
-  if (b.any_intra) {
+  if (b.any_intra && !b.intra_done) {
     StageMark m(lead, ST_INTRA);
     // one single-wave chain per (SB row, component); LDS holds the row's CU words
     size_t lds = (size_t)((W + 7) / 8) * 8 * sizeof(uint2);
-    k_intra<<<dim3(3 * nrows, n), 64, lds, st>>>(b.fb, lead->dbg, lead->dbg_flags);
+    k_intra<<<dim3(3 * nrows, n), 64, lds, lead->stream>>>(b.fb, lead->dbg, lead->dbg_flags);
     HIPCHK(hipGetLastError());
   }
+  return THOR_OK;
+}
+
+static int batch_phase_b(thor_dec *lead, const Batch &b, int pad = 1) {
+  const int W = lead->seq.width, H = lead->seq.height, n = b.n;
+  hipStream_t st = lead->stream;
+  const int rc = batch_intra(lead, b);
+  if (rc != THOR_OK) return rc;
   if (b.any_deblock) {
     StageMark m(lead, ST_DEBLOCK);
     int nv = ((W >> 3) - 1) * (H >> 3);
@@ -634,6 +652,21 @@ int thor_dec_set_band_local(thor_dec_t *d, int on) {
   if (!d || d->pending) return THOR_ERR_ARG;
   d->band_local = on != 0;
   return THOR_OK;
+}
+
+int thor_dec_set_band_intra(thor_dec_t *d, int on) {
+  if (!d || d->pending) return THOR_ERR_ARG;
+  d->band_intra = on != 0;
+  return THOR_OK;
+}
+
+int thor_dec_frame_intra(thor_dec_t *d) {
+  if (!d || !d->pending || d->pending_ended) return THOR_ERR_ARG;
+  Batch *b = (Batch *)d->pending;
+  HIPCHK(hipSetDevice(d->device));
+  const int rc = batch_intra(d, *b);
+  if (rc == THOR_OK) b->intra_done = 1;
+  return rc;
 }
 
 int thor_dec_frame_begin(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_frame_in_t *in) {
@@ -721,7 +754,7 @@ int thor_dec_get_rows(thor_dec_t *d, int frame_num, int y0, int nrows, void *dst
 }
 
 int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const void *src) {
-  if (!d || !src || y0 < 0 || nrows <= 0 || (y0 & 63) || (nrows & 1)) return THOR_ERR_ARG;
+  if (!d || !src || y0 < 0 || nrows <= 0 || (y0 & 1) || (nrows & 1)) return THOR_ERR_ARG;
   const int s = band_slot(d, frame_num);
   if (s < 0) return THOR_ERR_REF;
   const int W = d->seq.width, H = d->seq.height;
@@ -735,9 +768,10 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
   // writes the inter pixels there for its own band): refresh every SB row
   // whose bottom row this band carries
   const int sb0 = y0 / 64, sb1 = (y0 + n) / 64;  // SB rows whose row 63 lies inside [y0, y0 + n)
+  const long long r63 = 64LL * sb0 + 63 - y0;     // that row of SB row sb0, in the source
   if (sb1 > sb0)
-    HIPCHK(hipMemcpy2DAsync(d->edge + (long long)sb0 * d->ewy + EDGE_MARGIN, d->ewy, i + (long long)(63) * W, 64LL * W,
-                            W, sb1 - sb0, hipMemcpyDeviceToDevice, d->stream));
+    HIPCHK(hipMemcpy2DAsync(d->edge + (long long)sb0 * d->ewy + EDGE_MARGIN, d->ewy, i + r63 * W, 64LL * W, W,
+                            sb1 - sb0, hipMemcpyDeviceToDevice, d->stream));
   i += (long long)nrows * W;
   const int nsbrows = (H + 63) / 64;
   for (int c = 0; c < 2; c++) {
@@ -746,7 +780,7 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
     if (sb1 > sb0)
       HIPCHK(hipMemcpy2DAsync(d->edge + (long long)nsbrows * d->ewy + (long long)c * nsbrows * d->ewc +
                                   (long long)sb0 * d->ewc + EDGE_MARGIN,
-                              d->ewc, i + 31LL * (W / 2), 32LL * (W / 2), W / 2, sb1 - sb0, hipMemcpyDeviceToDevice,
+                              d->ewc, i + (r63 / 2) * (W / 2), 32LL * (W / 2), W / 2, sb1 - sb0, hipMemcpyDeviceToDevice,
                               d->stream));
     i += (long long)(nrows / 2) * (W / 2);
   }

@@ -96,6 +96,7 @@ struct FrameCtx {
   int band0, band1;  // SB rows k_recon reconstructs (row-band sharding); all by default
   int islot;         // slot of the frame's temporal-interpolated reference (blocks' ref -2), -1 none
   int pb0, pb1;      // band-local phase B: luma rows [pb0, pb1) deblocked / CLPF'd here; pb1 = 0: whole frame
+  int ir0, ir1;      // SB rows whose intra chains run here (band-local intra); ir1 = 0: every row
   // Per half SB (64x32 luma) prediction plan, written by k_frame_prep for the
   // halves one 64x64 inter CU covers with a single (MV, reference) key per
   // prediction pass: (mv0, MC meta word, mv1, tag).  A record is this frame's

@@ -563,7 +563,7 @@ __device__ __forceinline__ unsigned long long intra_chain(IntraChain &L, const F
   k.ctl = ctl;
   k.above = progress + 3 * (row - 1) + comp;
   const int iw = ch ? CompGeom<1>::IW : CompGeom<0>::IW, sz = 64 >> ch;
-  int seen = row == 0 ? 0x7fffffff : 0, cur_sb = -2;
+  int seen = row == f.ir0 ? 0x7fffffff : 0, cur_sb = -2;  // the first row (of the frame / band) waits on nothing
   uint2 wn = ncu > 0 ? g_cuw[0] : make_uint2(0, 0);
   for (int it = 0; it < ncu; it++) {
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(wn.x), w1 = __builtin_amdgcn_readfirstlane(wn.y);
@@ -662,10 +662,14 @@ __global__ __launch_bounds__(64) void k_intra(const FrameBatch fb_, unsigned lon
   const int nrows = f.nsbrows, full_sb = f.full_sb;
   const int16_t *__restrict__ resid = f.resid;
   const int lane = threadIdx.x;
+  // SB rows [ir0, ir1): the whole frame, or (band-local intra, row sharding) the
+  // band's rows, whose first chain reads the row above from the edge buffer
+  // (the rank above hands it over) instead of waiting for it
+  const int ir0 = f.ir0, ir1 = f.ir1 > 0 ? f.ir1 : nrows;
   for (;;) {
     const int task = (int)__builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&ctl[0], 1u) : 0u);
-    if (task >= 3 * nrows) return;
-    const int row = task / 3, c = task - 3 * row;
+    if (task >= 3 * (ir1 - ir0)) return;
+    const int row = ir0 + task / 3, c = task - 3 * (row - ir0);
     const int i0 = rowstart[row], ncu = rowstart[row + 1] - i0;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     // stage the row's CU words (lane-parallel, four batches of loads in flight)

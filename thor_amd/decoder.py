@@ -195,6 +195,13 @@ class GpuDecoder:
     def set_band_local(self, on: bool):
         L.check(self.lib.thor_dec_set_band_local(self.h, 1 if on else 0), "thor_dec_set_band_local")
 
+    def set_band_intra(self, on: bool):
+        L.check(self.lib.thor_dec_set_band_intra(self.h, 1 if on else 0), "thor_dec_set_band_intra")
+
+    def intra(self):
+        """The pending frame's intra stage now (band-local intra: the band's rows)."""
+        L.check(self.lib.thor_dec_frame_intra(self.h), "thor_dec_frame_intra")
+
     def finish(self):
         L.check(self.lib.thor_dec_frame_finish(self.h), "thor_dec_frame_finish")
 

@@ -129,9 +129,13 @@ class RowShard:
     (nccl/RCCL) or host staging (gloo)."""
 
     def __init__(self, dec, dist, width: int, height: int, device_exchange: bool, band_local: bool = False,
-                 halo: bool = False):
+                 halo: bool = False, boundary: bool = False):
         if halo and not band_local:
             raise ValueError("the halo exchange replaces band-local phase B's second all-gather")
+        if boundary and not halo:
+            raise ValueError("the boundary exchange replaces the first all-gather of the halo mode")
+        self.boundary = boundary
+        self.boundary_bytes = []  # per frame: bytes this rank received in the boundary exchange
         self.halo = halo
         self.halo_bytes = []  # per frame: bytes this rank received in halo exchanges
         self.final = {}  # halo mode: frame_num -> sorted disjoint luma row ranges this rank holds final
@@ -146,6 +150,10 @@ class RowShard:
         self.band_local = band_local
         if band_local:
             dec.set_band_local(True)
+        if boundary:
+            if any(self.owned(q)[1] - self.owned(q)[0] < 8 for q in range(self.world)):
+                raise ValueError("the boundary exchange needs every band at least 8 rows high")
+            dec.set_band_intra(True)
         import torch
 
         self.dstream = None
@@ -164,6 +172,8 @@ class RowShard:
         if halo:  # one full-frame staging buffer per peer (a halo may be a whole reference)
             self.fbytes = rows_bytes(width, height + (height & 1))
             self.hbuf = [dec.scratch(self.fbytes) for _ in range(self.world)]
+        if boundary and not device_exchange:  # host staging of the boundary pieces (edge, 4 halo pieces)
+            self.bscratch = [dec.scratch(rows_bytes(width, self.HALO_ROWS)) for _ in range(6)]
 
     def owned(self, rank: int):
         """Luma rows [lo, hi) of the frame `rank` holds final."""
@@ -182,7 +192,10 @@ class RowShard:
             if hi > lo:
                 self._hold(frame_num, lo, hi)
         d.begin(devframe)
-        self._exchange(frame_num)  # the bands' pre-deblock rows (inter reconstruction)
+        if self.boundary:
+            self._boundary(frame_num, frame)  # edge rows for the intra chains, deblocking halos
+        else:
+            self._exchange(frame_num)  # the bands' pre-deblock rows (inter reconstruction)
         d.end()
         if self.band_local:
             if not self.halo:
@@ -263,6 +276,140 @@ class RowShard:
         for f in sorted(padded):
             d.pad_frame(f)
         self.halo_bytes.append(got)
+
+    # ---- boundary exchange (replaces the pre-deblock all-gather) ----
+    HALO_ROWS = 8  # pre-deblock rows either side of a band its deblocking reads (3 needed, 8-row groups)
+
+    def boundary_plan(self, frame):
+        """Which ranks hand their band's bottom edge rows to the rank below this
+        frame, and when: {rank: "early" | "late"} -- "early" (right after the
+        band's inter reconstruction) when the band's last SB row holds no intra
+        CU, "late" (after its intra chains) otherwise; only toward a band that
+        has intra CUs (its first chain reads the row above).  Every rank derives
+        the same plan from the frame's parse output."""
+        b = frame.blocks
+        intra_rows = set((b["ypos"][b["mode"] == 1].astype(np.int64) >> 6).tolist()) if len(b) else set()
+        plan = {}
+        for r in range(self.world - 1):
+            a0, a1 = band_of(self.H, self.world, r)
+            c0, c1 = band_of(self.H, self.world, r + 1)
+            if a1 <= a0 or c1 <= c0 or not any(c0 <= y < c1 for y in intra_rows):
+                continue
+            plan[r] = "late" if (a1 - 1) in intra_rows else "early"
+        return plan
+
+    def _boundary(self, frame_num: int, frame):
+        """Between the band's inter reconstruction and its deblocking: (1) the
+        edge rows -- the two luma rows ending the band above (and their chroma
+        row) -- from the rank above, whose intra chains may write them, before
+        this band's intra chains (thor_dec_frame_intra, the band's rows only);
+        (2) after intra, HALO_ROWS pre-deblock rows either side of the band,
+        grouped both ways, for the band-local deblocking.  Bytes per rank and
+        frame: 3W per edge + 2 x 1.5 x HALO_ROWS x W, against a whole frame in
+        the all-gather."""
+        d, r = self.dec, self.rank
+        plan = self.boundary_plan(frame)
+        got = 0
+        lo, hi = self.owned(r)
+        if r in plan and plan[r] == "early":
+            self._send_rows(frame_num, hi - 2, 2, r + 1)
+        if (r - 1) in plan:
+            got += self._recv_rows(frame_num, lo - 2, 2, r - 1)
+        d.intra()
+        if r in plan and plan[r] == "late":
+            self._send_rows(frame_num, hi - 2, 2, r + 1)
+        h = self.HALO_ROWS
+        pieces = []  # (peer, y0, n, send?)
+        if r > 0 and hi > lo:
+            pieces += [(r - 1, lo, min(h, self.H - lo), True), (r - 1, lo - h, h, False)]
+        if r + 1 < self.world and hi > lo and hi < self.H:
+            pieces += [(r + 1, hi - h, h, True), (r + 1, hi, min(h, self.H - hi), False)]
+        got += self._swap_rows(frame_num, pieces)
+        self.boundary_bytes.append(got)
+
+    def _stage(self, nbytes):
+        import torch
+
+        if self.device_exchange:
+            return torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
+        return torch.empty(nbytes, dtype=torch.uint8)
+
+    def _rows_out(self, frame_num, y0, n, t, k):
+        """Rows [y0, y0 + n) of the frame into staging tensor t (host path: via scratch k)."""
+        d = self.dec
+        if self.device_exchange:
+            d.get_rows(frame_num, y0, n, t.data_ptr())
+        else:
+            d.get_rows(frame_num, y0, n, self.bscratch[k])
+            d.d2h(t.numpy(), self.bscratch[k])
+
+    def _rows_in(self, frame_num, y0, n, t, k):
+        d = self.dec
+        if self.device_exchange:
+            d.put_rows(frame_num, y0, n, t.data_ptr())
+        else:
+            d.h2d(self.bscratch[k], t.numpy())
+            d.put_rows(frame_num, y0, n, self.bscratch[k])
+            d.sync()  # the scratch buffer is reused
+
+    def _order(self, to_torch: bool):
+        """Order the decoder stream's copies before (to_torch) or after torch's stream (device path)."""
+        if self.device_exchange and self.dstream is not None:
+            import torch
+
+            cur = torch.cuda.current_stream()
+            ev = torch.cuda.Event()
+            if to_torch:
+                ev.record(self.dstream)
+                cur.wait_event(ev)
+            else:
+                ev.record(cur)
+                self.dstream.wait_event(ev)
+
+    def _keep(self, ts):
+        if self.device_exchange and self.dstream is not None:
+            for t in ts:
+                t.record_stream(self.dstream)
+
+    def _send_rows(self, frame_num, y0, n, peer):
+        t = self._stage(rows_bytes(self.W, n))
+        self._rows_out(frame_num, y0, n, t, 0)
+        self._order(True)
+        self.dist.send(t, peer)
+        self._keep([t])
+
+    def _recv_rows(self, frame_num, y0, n, peer):
+        t = self._stage(rows_bytes(self.W, n))
+        self.dist.recv(t, peer)
+        self._order(False)
+        self._rows_in(frame_num, y0, n, t, 1)
+        self._keep([t])
+        return t.numel()
+
+    def _swap_rows(self, frame_num, pieces):
+        """One grouped batch of sends and receives of row ranges: [(peer, y0, n, is_send)]."""
+        if not pieces:
+            return 0
+        ops, recvs, keep = [], [], []
+        for k, (peer, y0, n, snd) in enumerate(pieces):
+            t = self._stage(rows_bytes(self.W, n))
+            if snd:
+                self._rows_out(frame_num, y0, n, t, 2 + k)
+                ops.append(self.dist.P2POp(self.dist.isend, t, peer))
+            else:
+                ops.append(self.dist.P2POp(self.dist.irecv, t, peer))
+                recvs.append((y0, n, t, 2 + k))
+            keep.append(t)
+        self._order(True)
+        for w in self.dist.batch_isend_irecv(ops):
+            w.wait()
+        self._order(False)
+        got = 0
+        for y0, n, t, k in recvs:
+            self._rows_in(frame_num, y0, n, t, k)
+            got += t.numel()
+        self._keep(keep)
+        return got
 
     def _exchange(self, frame_num: int):
         d = self.dec
