@@ -32,12 +32,7 @@ __global__ void k_pad(const FrameBatch);
     }                                                                                           \
   } while (0)
 
-static int chroma_qp_host(int q) {
-  static const int t[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
-                            18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33,
-                            34, 34, 35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45};
-  return t[q < 0 ? 0 : (q > 51 ? 51 : q)];
-}
+#include "host_lists.h"
 
 struct thor_dec {
   thor_seq_t seq;
@@ -845,59 +840,6 @@ int thor_dec_stage_marks(thor_dec_t *d, int *stage, double *ms, int cap) {
   }
   d->ev_marks.clear();
   d->ev_used = 0;
-  return n;
-}
-
-int thor_build_clpf_list(const uint8_t *host_flags, int nsb, uint32_t *out) {
-  if (nsb < 0 || (nsb > 0 && !host_flags)) return THOR_ERR_ARG;
-  int n = 0;
-  for (int i = 0; i < nsb; i++)
-    if (host_flags[i]) {
-      if (out) out[n] = (uint32_t)i;
-      n++;
-    }
-  return n;
-}
-
-int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, thor_tu_t *out) {
-  if (nblocks < 0 || (nblocks > 0 && !host_blocks)) return THOR_ERR_ARG;
-  int n = 0;
-  for (int b = 0; b < nblocks; b++) {
-    const thor_block_t &B = host_blocks[b];
-    if (B.mode == M_SKIP) continue;  // SKIP carries no residual (dec/decode_block.c:213-242)
-    for (int c = 0; c < 3; c++) {
-      if (!((B.coeff_mask >> c) & 1)) continue;
-      // tb-split gives 4 quarters; chroma of an 8x8 CU is not split (dec/decode_block.c:449-450)
-      const int split = B.tb_split && (c == 0 || B.size > 8);
-      const int size = c ? B.size >> 1 : B.size, ntu = split ? size >> 1 : size;
-      const int nt = ntu == 64 ? 32 : ntu, q = nt < 16 ? nt : 16;
-      const int py = c ? B.ypos >> 1 : B.ypos, px = c ? B.xpos >> 1 : B.xpos;
-      for (int t = 0; t < (split ? 4 : 1); t++) {  // quarters in raster order, :101-102
-        if (out) {
-          thor_tu_t &T = out[n];
-          T.coeff_off = B.coeff_off[c] + (uint32_t)(t * q * q);
-          T.y = (uint16_t)(py + (t >> 1) * ntu);
-          T.x = (uint16_t)(px + (t & 1) * ntu);
-          T.size = (uint8_t)ntu;
-          T.comp = (uint8_t)c;
-          T.qp = (uint8_t)(c ? chroma_qp_host(B.qp) : B.qp);
-          T.rsv = 0;
-        }
-        n++;
-      }
-    }
-  }
-  return n;
-}
-
-int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t *out) {
-  if (nblocks < 0 || (nblocks > 0 && !host_blocks)) return THOR_ERR_ARG;
-  int n = 0;
-  for (int b = 0; b < nblocks; b++)
-    if (host_blocks[b].mode == M_INTRA) {
-      if (out) out[n] = (uint32_t)b;
-      n++;
-    }
   return n;
 }
 

@@ -375,10 +375,26 @@ static inline int te_set_param(thor_enc_params_t *p, const char *k, const char *
 
 // What this device encoder supports (and check_parameters, enc/strings.c:431-479)
 static inline int te_check_params(const thor_enc_params_t *p) {
+  // check_parameters (enc/strings.c:431-479); its fatalerror() is THOR_ERR_ARG here
+  if (p->num_frames <= 0) return THOR_ERR_ARG;
   if (p->width <= 0 || p->height <= 0 || (p->width & 7) || (p->height & 7)) return THOR_ERR_ARG;
-  if (p->qp < 0 || p->qp > 51 || p->max_num_ref < 1 || p->max_num_ref > 4 || p->HQperiod < 1) return THOR_ERR_ARG;
-  if (p->rdoq) return THOR_ERR_ARG;          // full RDOQ is not implemented
-  if (p->sync) return THOR_ERR_ARG;
-  if (p->num_reorder_pics + 1 > 16) return THOR_ERR_ARG;
+  if (p->max_num_ref < 1 || p->max_num_ref > 4) return THOR_ERR_ARG;
+  if (p->max_delta_qp >= 8) return THOR_ERR_ARG;
+  if (p->HQperiod >= 33) return THOR_ERR_ARG;  // MAX_REF_FRAMES, common/global.h:67
+  const int nrp1 = p->num_reorder_pics + 1;
+  if (p->num_reorder_pics > 0 && p->HQperiod > 1 && p->HQperiod % nrp1) return THOR_ERR_ARG;
+  if (p->dyadic_coding && (nrp1 < 1 || (nrp1 & (nrp1 - 1)))) return THOR_ERR_ARG;
+  if (p->num_reorder_pics > 0 && p->max_num_ref < 2) return THOR_ERR_ARG;
+  if (nrp1 != 0 && p->intra_period % nrp1) return THOR_ERR_ARG;
+  // what the reference leaves to the user but this encoder needs: the header
+  // field widths (16-bit sizes, 3-bit max_delta_qp), a sub-GOP of at most 16
+  // (the coding-order tables), a QP trial loop that ends, a window of one
+  // HQ period at least
+  if (p->width > 65535 || p->height > 65535 || p->qp < 0 || p->qp > 51 || p->HQperiod < 1) return THOR_ERR_ARG;
+  if (p->num_reorder_pics < 0 || nrp1 > 16 || p->max_delta_qp < 0) return THOR_ERR_ARG;
+  if (p->max_delta_qp > 0 && p->delta_qp_step < 1) return THOR_ERR_ARG;
+  if (p->skip < 0) return THOR_ERR_ARG;
+  if (p->rdoq) return THOR_ERR_ARG;  // full RDOQ is not implemented
+  if (p->sync) return THOR_ERR_ARG;  // WPP row sync (requires encoder_speed 2 in the reference) is not implemented
   return THOR_OK;
 }
