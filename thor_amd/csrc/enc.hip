@@ -59,11 +59,15 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 
 // WPP worker: grid of persistent single-wave workgroups; ticket t -> stream
 // t % n, SB row t / n.
-#if defined(THOR_ENC_WPE)  // experiments: minimum waves per SIMD the register budget must allow
-#define TE_WPE __attribute__((amdgpu_waves_per_eu(THOR_ENC_WPE)))
-#else
-#define TE_WPE
+// Two workers per SIMD: the RD loop is a latency-bound chain of small
+// dependent steps (LDS round trips, VALU -> SALU hand-offs), so a second wave
+// hides part of it -- 15 % off the 4K I frame at 240 streams.
+// That needs <= 20 KB of LDS per worker (the small levels live in global
+// memory, TeSmallLv) and <= 256 registers.  THOR_ENC_WPE overrides (experiments).
+#if !defined(THOR_ENC_WPE)
+#define THOR_ENC_WPE 2
 #endif
+#define TE_WPE __attribute__((amdgpu_waves_per_eu(THOR_ENC_WPE)))
 __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
                                                  TeScratchMem *scratch, unsigned *err, unsigned long long spin_limit,
                                                  int stall_row) {
@@ -615,7 +619,7 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   EHIP(hipMemcpyAsync(P.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
   EHIP(hipMemsetAsync(P.ticket, 0, 4, st));
   // persistent workers take row tickets until none are left: more workgroups
-  // than the chip holds at once (one per SIMD at this kernel's register and LDS
+  // than the chip holds at once (two per SIMD at this kernel's register and LDS
   // use) would only start as the first ones run out of work
   k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(P.jobs, n, P.ticket, nrows,
                                                                          P.scratch, P.err, g_spin_limit.load(),

@@ -94,9 +94,18 @@ template <typename T>
 __device__ __forceinline__ T *te_lds(T *p) {
   return (T *)(__attribute__((address_space(3))) T *)p;
 }
+// te_glb(p): p points into global memory (the worker's TeScratchMem)
+template <typename T>
+__device__ __forceinline__ T *te_glb(T *p) {
+  return (T *)(__attribute__((address_space(1))) T *)p;
+}
 #else
 template <typename T>
 static inline T *te_lds(T *p) {
+  return p;
+}
+template <typename T>
+static inline T *te_glb(T *p) {
   return p;
 }
 #endif
@@ -343,11 +352,10 @@ static const TeZigzag te_zig_h = TeZigzag();  // host copy (the parser)
 // LDS copy for the encoder worker (k_enc_rows loads it once: te_load_zig); the
 // per-lane lookups of quantize / write_coeff then cost an LDS read, not a
 // divergent global load
-__shared__ uint8_t te_zig_lds[2][3][256];
+__shared__ uint8_t te_zig_lds[1][3][256];  // te_zz only: te_izz (write_coeff's scan) reads the constant table
 __device__ __forceinline__ void te_load_zig() {
   for (int e = threadIdx.x; e < 768; e += 64) {
     te_zig_lds[0][e >> 8][e & 255] = te_zig.zz[e >> 8][e & 255];
-    te_zig_lds[1][e >> 8][e & 255] = te_zig.iz[e >> 8][e & 255];
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -361,11 +369,7 @@ TE_HD int te_zz(int q, int r) {
 #endif
 }
 TE_FN int te_izz(int q, int pos) {
-#if defined(TE_HOST)
   return te_zig.iz[q == 4 ? 0 : (q == 8 ? 1 : 2)][pos];
-#else
-  return te_zig_lds[1][q == 4 ? 0 : (q == 8 ? 1 : 2)][pos];
-#endif
 }
 
 // ---- bit writer (enc/putbits.c:112-146) -------------------------------------

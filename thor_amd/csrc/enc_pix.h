@@ -666,7 +666,7 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
 // ---- transform chain -----------------------------------------------------------
 // Scratch of one transform block (compact, q = min(N, 16)).
 struct TeTx {
-  int16_t R[64 * 64];  // residual (N x N), reconstructed residual
+  int16_t R[32 * 32];  // residual (N x N, N <= 32), reconstructed residual (64: the 32-point output)
   int16_t A[32 * 32];  // pre-summed input of the 32 / 64 paths
   int16_t T[32 * 32];  // pass-1 output
   int16_t C[256];      // q x q coefficients / levels (raster; every value fits 16 bits)
@@ -733,7 +733,7 @@ TE_FN void te_fwd_gen(TeTx &X, const int16_t *in, int sh1, int sh2) {
 }
 
 // transform, common/transform.c:249-330 (SIMD transform_simd for the 8x8
-// butterfly wrap): X.R (size x size, stride size) -> X.C (q x q raster).
+// butterfly wrap): X.R (size x size, stride size; 64: X.A, te_residual64) -> X.C (q x q raster).
 TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
   TE_P(TP_FWD);
   const int lg = te_log2(size);
@@ -752,28 +752,22 @@ TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
     te_sync();
     return;
   }
+  // size 64: X.A already holds the pre-summed residual (te_residual64)
   if (size > 16 && fast) {  // 2x2 / 4x4 pre-sum into a 16-point transform, :273-293
     N = 16;
     sh1 += 1 + (size == 64);
     sh2 = 9;
-    const int f = size / 16;
-    for (int e = TE_LANE; e < 256; e += TE_NL) {
-      const int i = e >> 4, j = e & 15;
-      int s = 0;
-      for (int a = 0; a < f; a++)
-        for (int b = 0; b < f; b++) s += X.R[(i * f + a) * size + j * f + b];
-      X.A[e] = (int16_t)te_wrap16(s);
-    }
+    if (size == 32)
+      for (int e = TE_LANE; e < 256; e += TE_NL) {
+        const int i = e >> 4, j = e & 15;
+        const int16_t *r = &X.R[(2 * i) * 32 + 2 * j];
+        X.A[e] = (int16_t)te_wrap16(r[0] + r[1] + r[32] + r[33]);
+      }
     in = X.A;
   } else if (size == 64) {  // 2x2 pre-sum into a 32-point transform, :294-307
     N = 32;
     sh1 = 7;
     sh2 = 10;
-    for (int e = TE_LANE; e < 1024; e += TE_NL) {
-      const int i = e >> 5, j = e & 31;
-      const int16_t *r = &X.R[(2 * i) * 64 + 2 * j];
-      X.A[e] = (int16_t)te_wrap16(r[0] + r[1] + r[64] + r[65]);
-    }
     in = X.A;
   }
   te_sync();

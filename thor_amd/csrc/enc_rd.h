@@ -14,10 +14,11 @@ struct TeLevel {             // one quadtree level (64, 32, 16, 8)
   uint32_t bbits[TE_BEST_WORDS];      // the best candidate's syntax bits (TeBlockInfo::best_bits)
 };
 // The 32 / 16 / 8 levels' reconstruction buffers and the 16 / 8 levels'
-// coefficient sets and kept syntax bits (80 of an SB's 85 CUs): LDS on the
-// device (k_enc_rows), so a candidate's levels and pixels make no global
-// memory round trips.  Capacity of the kept bits: overflow falls back to
-// running write_block again (te_keep_best_bits).
+// coefficient sets and kept syntax bits (80 of an SB's 85 CUs): global
+// memory (TeScratchMem::sl), L2-resident -- in LDS they would hold
+// k_enc_rows to one worker per SIMD.  Capacity of the
+// kept bits: overflow falls back to running write_block again
+// (te_keep_best_bits).
 struct TeSmallLv {
   uint8_t rec1[2][32 * 32 * 3 / 2], rec2[2][16 * 16 * 3 / 2], rec3[2][8 * 8 * 3 / 2];
   int16_t cf2[2][3 * 256], cf3[2][3 * 64];
@@ -25,7 +26,7 @@ struct TeSmallLv {
 };
 struct TeScratchMem {         // global memory, one per worker wave
   TeLevel lv[4];
-  TeSmallLv sl;                      // (host build; LDS on the device)
+  TeSmallLv sl;
   TeBlockInfo bi[4];                 // (host build: the per-level block state; LDS on the device)
   TeParam tmp;                       // (host build: the candidate parameters; LDS on the device)
   uint8_t pb0[TE_BLK], pb1[TE_BLK];  // bi-pred legs (Y | U | V, compact)
@@ -69,7 +70,7 @@ TE_FN TeScratch te_local(TeScratch S) {
   S.nb = te_lds(S.nb);
   S.bi = te_lds(S.bi);
   S.tmp = te_lds(S.tmp);
-  S.sl = te_lds(S.sl);
+  S.sl = te_glb(S.sl);  // global: the LDS budget of two workers per SIMD (k_enc_rows)
   return S;
 }
 // The worker's buffer table, rebuilt where it is needed instead of passed
@@ -84,13 +85,13 @@ static inline TeScratch te_here() { return g_te_scratch; }
 #else
 __shared__ TeTx g_te_tx;
 __shared__ TeNbr g_te_nb;
-__shared__ uint8_t g_te_pb[TE_BLK];
 __shared__ TeBlockInfo g_te_bi[4];
 __shared__ TeParam g_te_tmp;
-__shared__ TeSmallLv g_te_sl;
 __shared__ TeScratchMem *g_te_mem;
+__shared__ uint8_t g_te_pb[TE_BLK];
 __device__ __forceinline__ TeScratch te_here() {
-  return te_local(te_scratch(*g_te_mem, &g_te_tx, &g_te_nb, g_te_pb, g_te_bi, &g_te_tmp, &g_te_sl));
+  TeScratchMem &M = *g_te_mem;
+  return te_local(te_scratch(M, &g_te_tx, &g_te_nb, g_te_pb, g_te_bi, &g_te_tmp, &M.sl));
 }
 #endif
 // State of the superblock being encoded (frame_info mvcand / best_ref are
@@ -168,6 +169,42 @@ TE_FN void te_residual(int16_t *R, const uint8_t *o, int os, const uint8_t *p, i
     }
   }
   te_sync();
+}
+
+// A 64 x 64 residual straight into the pre-summed input of its transform
+// (te_fwd_tx's 64 path, common/transform.c:273-307): X.A = f x f sums of
+// o - p, f = 4 (fast: 16 x 16) or 2 (32 x 32), int16 wrap.  The sums are
+// exact, so this equals summing a materialised residual; X.R then only ever
+// holds up to 32 x 32.
+TE_FN void te_residual64(TeTx &X, const uint8_t *o, int os, const uint8_t *p, int ps, int fast) {
+  if (fast) {
+    for (int e = TE_LANE; e < 256; e += TE_NL) {
+      const int i = e >> 4, j = (e & 15) * 4;
+      int s = 0;
+      for (int a = 0; a < 4; a++) {
+        const uint32_t x = te_ld4(o + (4 * i + a) * os + j), y = te_ld4(p + (4 * i + a) * ps + j);
+        s += te_b(x, 0) + te_b(x, 1) + te_b(x, 2) + te_b(x, 3) - te_b(y, 0) - te_b(y, 1) - te_b(y, 2) - te_b(y, 3);
+      }
+      X.A[e] = (int16_t)te_wrap16(s);
+    }
+  } else {
+    for (int g = TE_LANE; g < 512; g += TE_NL) {  // two outputs per lane: 4 columns x 2 rows
+      const int i = g >> 4, j = (g & 15) * 4;
+      const uint32_t o0 = te_ld4(o + (2 * i) * os + j), o1 = te_ld4(o + (2 * i + 1) * os + j);
+      const uint32_t p0 = te_ld4(p + (2 * i) * ps + j), p1 = te_ld4(p + (2 * i + 1) * ps + j);
+      for (int k = 0; k < 2; k++) {
+        const int s = te_b(o0, 2 * k) + te_b(o0, 2 * k + 1) + te_b(o1, 2 * k) + te_b(o1, 2 * k + 1) - te_b(p0, 2 * k) -
+                      te_b(p0, 2 * k + 1) - te_b(p1, 2 * k) - te_b(p1, 2 * k + 1);
+        X.A[i * 32 + (j >> 1) + k] = (int16_t)te_wrap16(s);
+      }
+    }
+  }
+  te_sync();
+}
+// the residual of an N x N transform block into its transform's input
+TE_FN void te_residual_tx(TeTx &X, const uint8_t *o, int os, const uint8_t *p, int ps, int n, int fast) {
+  if (n == 64) te_residual64(X, o, os, p, ps, fast);
+  else te_residual(X.R, o, os, p, ps, n);
 }
 
 // clip_mv, enc/encode_block.c:816-828 (C division by 4; the right-edge test
@@ -270,7 +307,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, in
     // running copy of pred + residual (reconstruct_block after the loop, :1510)
     for (int t = 0; t < 4; t++) {
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
-      te_residual(X.R, org + i * os + j, os, pb + i * size + j, size, s2);
+      te_residual_tx(X, org + i * os + j, os, pb + i * size + j, size, s2, fast);
       te_fwd_tx(X, s2, fast);
       const int bit = te_quant(X, qp, s2, type);
       const int q = TE_MIN(s2, 16);
@@ -285,7 +322,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, in
     return cbp;
   }
   const int fast = (size == 64 && F.speed > 0) || F.speed > 1;
-  te_residual(X.R, org, os, pb, size, size);
+  te_residual_tx(X, org, os, pb, size, size, fast);
   te_fwd_tx(X, size, fast);
   cbp = te_quant(X, qp, size, type);
   const int q = TE_MIN(size, 16);
@@ -316,7 +353,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, co
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
       te_make_top_and_left(*S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
       te_intra_pred(*S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
-      te_residual(X.R, org + i * os + j, os, pb, s2, s2);
+      te_residual_tx(X, org + i * os + j, os, pb, s2, s2, fast);
       te_fwd_tx(X, s2, fast);
       const int bit = te_quant(X, qp, s2, type);
       for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * ts + e] = (int16_t)X.C[e];
@@ -331,7 +368,7 @@ TE_NOINL int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, co
   }
   te_make_top_and_left(*S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
   te_intra_pred(*S.nb, ypos, xpos, size, pb, mode, 0);
-  te_residual(X.R, org, os, pb, size, size);
+  te_residual_tx(X, org, os, pb, size, size, fast);
   te_fwd_tx(X, size, fast);
   const int cbp = te_quant(X, qp, size, type);
   const int q = TE_MIN(size, 16);
