@@ -172,7 +172,7 @@ def encoder_leg(torch, lib, reps: int = 10):
             "note": "RD candidate evaluation throughput of the encoder TU chain; not part of `value`"}
 
 
-def config3_leg(torch, lib, streams: int = 64, nf: int = 2):
+def config3_leg(torch, lib, streams: int = 128, nf: int = 2):
     """BASELINE config 3 -- 1080p config_LDB_high_efficiency, the full encoder
     RD loop on the GPU (encoder_speed 0: exact sub-pel ME, tb / pb split,
     4 references, delta-QP RD) -- as a throughput leg beside `value`: `streams`
@@ -528,7 +528,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config3-streams", type=int, default=64,
+    ap.add_argument("--config3-streams", type=int, default=128,
                     help="streams of the BASELINE config-3 encoder leg (1080p LDB high efficiency)")
     ap.add_argument("--drop-in", nargs="?", const="hd_low", default=None, metavar="STREAM",
                     help="time the reference decoder's host C on this library's per-call surface "
