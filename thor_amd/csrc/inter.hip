@@ -58,7 +58,7 @@
 #define WL_CH (WL_R * WL_P / 16)  // 16-byte chunks: 210
 #define WC_CH (WC_R * WC_P / 16)  // 66 per plane
 #define WIN_LOADS 6               // ceil((210 + 2 * 66) / 64)
-struct RefWin {
+struct alignas(16) RefWin {  // 16-B aligned: window chunks and the store transposes move as ds_*_b128
   uint8_t y[WL_R * WL_P];
   uint8_t u[WC_R * WC_P];
   uint8_t v[WC_R * WC_P];
