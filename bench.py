@@ -537,6 +537,9 @@ def main():
     ap.add_argument("--dec-slots", type=int, default=10,
                     help="reference ring slots per decoder context (LDB: up to 4 references + the current frame)")
     ap.add_argument("--streams", type=int, default=240, help="independent streams (encoder + decoder) per GPU")
+    ap.add_argument("--enc-cu-exclude", type=int, default=0, metavar="N",
+                    help="experiment: keep the encoder's kernels off N of every 32 CUs (hipExtStreamCreateWithCUMask), "
+                         "so concurrent decode launches always find free CUs")
     ap.add_argument("--dec-priority", type=int, default=0,
                     help="1: decoder groups on high-priority HIP streams (their launches dispatch ahead of the "
                          "encoder's queued workgroups); 0: default priority")
@@ -613,6 +616,13 @@ def main():
     for k in range(K):
         e = GpuEncoder(params_for(bc["config"], W, H, nf, bc["extra"]), device=local)
         e.use_device_sequence(inbuf[k].data_ptr(), nf)
+        if a.enc_cu_exclude and k == 0:  # the batch runs on its first member's stream (one masked queue, not K)
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            words = [0] * ((ncu + 31) // 32)
+            for c in range(ncu):
+                if c % 32 < 32 - a.enc_cu_exclude:
+                    words[c // 32] |= 1 << (c % 32)
+            e.set_cu_mask(words)
         encs.append(e)
     want_bit = [None] * nclip  # the reference Thorenc's .bit per clip: md5 in bench_clips.json
     seq, _ = parse_stream(open(os.path.join(gold, "k4_low.bit"), "rb").read())  # sequence header (all clips share it)
@@ -892,6 +902,7 @@ def main():
                 "stage_ms_per_stream_pass": {k: round(v, 4) for k, v in zip(STAGES + ["interp"], stage_ms)},
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "decoder_stream_priority": "high" if a.dec_priority else "default",
+                "enc_cu_exclude_per_32": a.enc_cu_exclude,
             },
             "roofline": {
                 "bound": "hbm",

@@ -338,6 +338,10 @@ int thor_enc_num_frames(const thor_enc_t *e);
  * -1 when every frame is coded */
 int thor_enc_next_input(const thor_enc_t *e);
 void *thor_enc_stream(thor_enc_t *e);
+/* Re-create the context's stream restricted to the CUs whose bits are set in
+ * mask[0..nwords) (bit c % 32 of word c / 32 = CU c; hipExtStreamCreateWithCUMask).
+ * A scheduling knob: CUs left out stay free for concurrent decode launches. */
+int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords);
 /* Code the next frame of each of `n` DIFFERENT contexts (same device and
  * size, n <= 512) with one launch per stage.  Thread-safe: calls on the same
  * device are serialised (they share that device's work pool); a context must

@@ -437,6 +437,24 @@ int thor_enc_next_input(const thor_enc_t *e) {
   return e->pos < e->gop->plans.size() ? e->gop->plans[e->pos].input_index : -1;
 }
 void *thor_enc_stream(thor_enc_t *e) { return e ? (void *)e->stream : nullptr; }
+// Re-create the context's stream restricted to a set of CUs
+// (hipExtStreamCreateWithCUMask: bit c % 32 of word c / 32 = CU c may run the
+// context's kernels).  A scheduling experiment (bench.py --enc-cu-exclude):
+// CUs the encoder's persistent row workers cannot hold stay free for
+// concurrent decode launches.
+int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords) {
+  if (!e || !mask || nwords <= 0) return THOR_ERR_ARG;
+  (void)hipSetDevice(e->device);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask) != hipSuccess) {
+    (void)hipGetLastError();
+    return THOR_ERR_HIP;
+  }
+  EHIP(hipStreamSynchronize(e->stream));
+  EHIP(hipStreamDestroy(e->stream));
+  e->stream = s;
+  return THOR_OK;
+}
 
 // One context's frame job.  Its device setup (cell and progress resets) is
 // enqueued on the batch stream `st`; its header words go to `hw` (host), which

@@ -97,6 +97,12 @@ class GpuEncoder:
             raise IndexError("input frame %d not uploaded" % k)
         return self.seq_dev + k * self.fsize
 
+    def set_cu_mask(self, words):
+        """Restrict this context's kernels to the CUs whose bits are set
+        (thor_enc_set_cu_mask; bit c % 32 of words[c // 32] = CU c)."""
+        arr = (C.c_uint32 * len(words))(*words)
+        L.check(self.lib.thor_enc_set_cu_mask(self.h, arr, len(words)), "thor_enc_set_cu_mask")
+
     def stream(self) -> int:
         """The context's HIP stream (thor_enc_stream): a batch runs on its first member's."""
         return self.lib.thor_enc_stream(self.h) or 0
