@@ -121,33 +121,12 @@ int thor_dev_free(void *p) {
   HIPCHK(hipFree(p));
   return THOR_OK;
 }
-// thor_h2d / thor_d2h copy on a per-thread non-blocking stream, never the
-// null stream: a null-stream copy would also wait for every blocking stream of
-// the device (a CU-masked encoder stream is one, thor_enc_set_cu_mask) and so
-// stall a decode upload behind the encoder.
-static hipStream_t copy_stream() {
-  thread_local int dev = -1;
-  thread_local hipStream_t s = nullptr;
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess) return nullptr;
-  if (!s || d != dev) {
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return s = nullptr;
-    dev = d;
-  }
-  return s;
-}
 int thor_h2d(void *dst, const void *src, size_t bytes) {
-  hipStream_t s = copy_stream();
-  if (!s) return THOR_ERR_HIP;
-  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
   return THOR_OK;
 }
 int thor_d2h(void *dst, const void *src, size_t bytes) {
-  hipStream_t s = copy_stream();
-  if (!s) return THOR_ERR_HIP;
-  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
   return THOR_OK;
 }
 

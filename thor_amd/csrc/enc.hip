@@ -441,7 +441,8 @@ void *thor_enc_stream(thor_enc_t *e) { return e ? (void *)e->stream : nullptr; }
 // (hipExtStreamCreateWithCUMask: bit c % 32 of word c / 32 = CU c may run the
 // context's kernels).  A scheduling experiment (bench.py --enc-cu-exclude):
 // CUs the encoder's persistent row workers cannot hold stay free for
-// concurrent decode launches.
+// concurrent decode launches.  The masked stream is a blocking stream (the HIP
+// call takes no flags): null-stream copies (thor_h2d / thor_d2h) wait for it.
 int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords) {
   if (!e || !mask || nwords <= 0) return THOR_ERR_ARG;
   (void)hipSetDevice(e->device);

@@ -51,20 +51,38 @@ TE_FN void te_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #endif
 }
+// Wave reductions (every call site is wave-uniform control flow, all 64
+// lanes active): DPP within each 16-lane row -- quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror, each lane then holds its row's result -- and the
+// four rows combined through readlane in SGPRs.  Four VALU ops and four
+// readlanes, no LDS round trip (the __shfl_xor butterfly was six
+// ds_bpermute_b32 round trips per reduction).  Returns a uniform value.
+#if !defined(TE_HOST)
+#define TE_DPP(v, ctrl) __builtin_amdgcn_update_dpp((int)(v), (int)(v), (ctrl), 0xF, 0xF, false)
+#endif
 TE_FN uint32_t te_sum(uint32_t v) {
 #if !defined(TE_HOST)
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-#endif
+  v += (uint32_t)TE_DPP(v, 0xB1);
+  v += (uint32_t)TE_DPP(v, 0x4E);
+  v += (uint32_t)TE_DPP(v, 0x141);
+  v += (uint32_t)TE_DPP(v, 0x140);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+#else
   return v;
+#endif
 }
 TE_FN int te_maxi(int v) {
 #if !defined(TE_HOST)
-  for (int o = 32; o > 0; o >>= 1) {
-    const int w = __shfl_xor(v, o);
-    v = v > w ? v : w;
-  }
-#endif
+  v = max(v, TE_DPP(v, 0xB1));
+  v = max(v, TE_DPP(v, 0x4E));
+  v = max(v, TE_DPP(v, 0x141));
+  v = max(v, TE_DPP(v, 0x140));
+  return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+#else
   return v;
+#endif
 }
 TE_FN int te_any(int v) {
 #if !defined(TE_HOST)
