@@ -750,8 +750,9 @@ TE_FN void te_load_scan(TeScanRegs &R, const int16_t *c, int q) {
 #endif
 }
 // The writer state travels by value (in registers) in and out: a reference
-// would pin the caller's register copy to the stack.
-TE_NOINL TeBits te_write_coeff(TeBits b_in, const int16_t *c, int size, int type) {
+// would pin the caller's register copy to the stack.  Inlined into
+// write_block (its only caller): no call frame per coded TU.
+TE_FN TeBits te_write_coeff(TeBits b_in, const int16_t *c, int size, int type) {
   TE_P(TP_WCOEF);
   TeBits b = te_bits_local(b_in);
   size = te_uni(size);

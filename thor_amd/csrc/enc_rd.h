@@ -337,7 +337,7 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, in
 
 // encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
 // component.  rf / fs: the frame being reconstructed at the CU origin.
-TE_NOINL int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs,
+TE_FN int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs,
                                int ypos, int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
                                int tb_split, int mode, int ur, int dl, int ts) {
   const TeFrame &F = *te_lds(&F_);
@@ -448,7 +448,7 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, Te
   const uint8_t *oY = F.oy + ypos * F.osy + xpos, *oU = F.ou + yC * F.osc + xC, *oV = F.ov + yC * F.osc + xC;
   int cy = 0, cu = 0, cv = 0;
   const int itype = (F.frame_type == TE_I) << 1;  // quantisation type follows the frame type (:1764)
-  if (mode == TE_INTRA) {
+  if (mode == TE_INTRA) {  // the chains inlined (te_enc_intra_comp is TE_FN): an I frame's candidates make no call per component
     const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
     cy = te_enc_intra_comp(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb,
                            p.coeff, recY, itype | 0, tb_split, p.intra_mode, ur, dl, p.ts);
