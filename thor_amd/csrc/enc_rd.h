@@ -423,7 +423,18 @@ TE_FN void te_put_kept(TeBits &b, const uint32_t *w, int nbits) {
 
 // encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
 // bi.rec, write the block's syntax.  Returns the bit count.
-TE_NOINL int te_encode_block(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
+// One out-of-line copy of the intra chain for the P / B frames' copy of
+// te_encode_block below.
+TE_NOINL int te_enc_intra_comp_nc(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos,
+                                  int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
+                                  int tb_split, int mode, int ur, int dl, int ts) {
+  return te_enc_intra_comp(F_, org, os, rf, fs, ypos, xpos, size, qp, pb_, coef, rec, type, tb_split, mode, ur, dl, ts);
+}
+// IFR: the I-frame copy, with the intra chains inlined (no call per
+// component); P / B frames use the other, whose body stays small for the
+// inter candidates that dominate them.
+template <bool IFR>
+TE_NOINL int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_here();
   TeBlockInfo &bi = *te_lds(&bi_);
@@ -448,14 +459,21 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, Te
   const uint8_t *oY = F.oy + ypos * F.osy + xpos, *oU = F.ou + yC * F.osc + xC, *oV = F.ov + yC * F.osc + xC;
   int cy = 0, cu = 0, cv = 0;
   const int itype = (F.frame_type == TE_I) << 1;  // quantisation type follows the frame type (:1764)
-  if (mode == TE_INTRA) {  // the chains inlined (te_enc_intra_comp is TE_FN): an I frame's candidates make no call per component
+  if (mode == TE_INTRA) {
     const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
-    cy = te_enc_intra_comp(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb,
-                           p.coeff, recY, itype | 0, tb_split, p.intra_mode, ur, dl, p.ts);
-    cu = te_enc_intra_comp(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
-                           p.coeff + p.cs, recU, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
-    cv = te_enc_intra_comp(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb,
-                           p.coeff + 2 * p.cs, recV, itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
+#define TE_INTRA_CHAINS(fn)                                                                                        \
+  cy = fn(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb, p.coeff, recY, itype | 0,    \
+          tb_split, p.intra_mode, ur, dl, p.ts);                                                                   \
+  cu = fn(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb, p.coeff + p.cs, recU, itype | 1,     \
+          tb_split && size > 8, p.intra_mode, ur, dl, p.ts);                                                       \
+  cv = fn(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb, p.coeff + 2 * p.cs, recV, itype | 1, \
+          tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
+    if constexpr (IFR) {
+      TE_INTRA_CHAINS(te_enc_intra_comp)
+    } else {
+      TE_INTRA_CHAINS(te_enc_intra_comp_nc)
+    }
+#undef TE_INTRA_CHAINS
   } else {
     const int bip = F.enable_bipred;
     if (mode == TE_SKIP) {
@@ -501,6 +519,9 @@ TE_NOINL int te_encode_block(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, Te
         p.ref_idx0 | p.ref_idx1 << 4 | p.pb_part << 8 | p.intra_mode << 12, nbits, cy | cu << 1 | cv << 2);
   if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
   return nbits;
+}
+TE_FN int te_encode_block(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_lds(&F)->frame_type == TE_I ? te_encode_block_t<true>(F, b, bi, p) : te_encode_block_t<false>(F, b, bi, p);
 }
 
 // cost_calc, enc/encode_block.c:1218-1228
