@@ -1414,7 +1414,23 @@ TE_NOINL int te_search_early_skip(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_
 // Template over the CU size: the quadtree recursion unrolls at compile time
 // (64 -> 32 -> 16 -> 8); level L = log2(64 / SIZE) owns TeScratch::lv[L].
 template <int SIZE>
+TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeSB &sb_, int ypos, int xpos, int qp);
+template <int SIZE>
+TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xpos, int qp);
+// A quadrant of the recursion: the 8x8 level (64 of an SB's 85 CUs) inlined
+// into the 16x16 one -- one call frame fewer per 8x8 CU (-3 % of a 4K I frame
+// at 240 streams) -- every other level a call.
+template <int NS>
+TE_FN uint32_t te_process_quad(const TeFrame &F, TeSB &sb, int ypos, int xpos, int qp) {
+  if constexpr (NS == 8) return te_process_block_b<8>(F, sb, ypos, xpos, qp);
+  return te_process_block<NS>(F, sb, ypos, xpos, qp);
+}
+template <int SIZE>
 TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeSB &sb_, int ypos, int xpos, int qp) {
+  return te_process_block_b<SIZE>(F_, sb_, ypos, xpos, qp);
+}
+template <int SIZE>
+TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xpos, int qp) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
@@ -1481,10 +1497,8 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeSB &sb_, int ypos, int x
       else if (ft != TE_I) te_put(b, 1, 0);
       if (SIZE == 64 && F.max_delta_qp) te_write_delta_qp(b, bi.delta_qp);
       cost_small = 0;
-      cost_small += te_process_block<NS>(F, sb, ypos, xpos, qp);
-      cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos, qp);
-      cost_small += te_process_block<NS>(F, sb, ypos, xpos + NS, qp);
-      cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos + NS, qp);
+      for (int q = 0; q < 4; q++)  // (0,0) (NS,0) (0,NS) (NS,NS): the reference's order
+        cost_small += te_process_quad<NS>(F, sb, ypos + (q & 1) * NS, xpos + (q >> 1) * NS, qp);
     }
   }
   if (encode_this) {
@@ -1497,10 +1511,8 @@ TE_NOINL uint32_t te_process_block(const TeFrame &F_, TeSB &sb_, int ypos, int x
         constexpr int NS = SIZE / 2;
         te_write_super_mode(b, F, bi, 0, 0, 1);
         cost_small = 0;
-        cost_small += te_process_block<NS>(F, sb, ypos, xpos, qp);
-        cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos, qp);
-        cost_small += te_process_block<NS>(F, sb, ypos, xpos + NS, qp);
-        cost_small += te_process_block<NS>(F, sb, ypos + NS, xpos + NS, qp);
+        for (int q = 0; q < 4; q++)
+          cost_small += te_process_quad<NS>(F, sb, ypos + (q & 1) * NS, xpos + (q >> 1) * NS, qp);
       }
     }
     if (cost <= cost_small) {
