@@ -473,9 +473,10 @@ def roofline_pass(lib, decs, groups, devs, frames_of, seq, isteps):
     frames = frames_of[0]
     pidx = [i for i, fr in enumerate(frames) if fr.frame_type != 0]  # the I frame has no inter pixels
     recon_ms = sum(per_frame[s * nf + i][1] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
+    prep_ms = sum(per_frame[s * nf + i][0] for s in range(isteps) for i in pidx) / (isteps * len(pidx))
     # per launch: the members' P frames of one frame index, averaged over the P frame indices
     alg = sum(recon_alg_bytes(fs[i], seq.width, seq.height) for fs in frames_of for i in pidx) / len(pidx)
-    return stage_ms, recon_ms, alg, B
+    return stage_ms, recon_ms, alg, B, prep_ms
 
 
 def launch_ranks(n: int) -> int:
@@ -798,7 +799,7 @@ def main():
     bit_exact = bits_ok(allk, bits) and decoded_ok(allk)
     rf_early = None
     if os.environ.get("THOR_BENCH_RF_EARLY"):  # diagnostic: the roofline pass before the timed steps too
-        _, rf_early, _, _ = roofline_pass(lib, decs, [groups[0]], devs, [parse_stream(bits[k])[1] for k in groups[0]],
+        _, rf_early, _, _, _ = roofline_pass(lib, decs, [groups[0]], devs, [parse_stream(bits[k])[1] for k in groups[0]],
                                           seq, 3)
 
     if dist is not None:
@@ -842,8 +843,10 @@ def main():
         decs[k].sync()
     t_do = (time.perf_counter() - t0) / dsteps
     frames_of = [parse_stream(bits[k])[1] for k in groups[0]]
-    stage_ms, recon_ms, alg, B = roofline_pass(lib, decs, [groups[0]], devs, frames_of, seq, 3)
+    stage_ms, recon_ms, alg, B, prep_ms = roofline_pass(lib, decs, [groups[0]], devs, frames_of, seq, 3)
     achieved = alg / (recon_ms / 1e3) / 1e9 if recon_ms > 0 else 0.0
+    path_ms = prep_ms + recon_ms
+    path_achieved = alg / (path_ms / 1e3) / 1e9 if path_ms > 0 else 0.0
     traffic = None
     tj = a.traffic_json or os.path.join(ROOT, "tools", "traffic_latest.json")
     if os.path.exists(tj):
@@ -916,6 +919,17 @@ def main():
                 "avg_launch_us": round(recon_ms * 1e3, 2),
                 **({"avg_launch_us_before_steps": round(rf_early * 1e3, 2)} if rf_early is not None else {}),
                 "frames_per_launch": B,
+                "path": {
+                    "kernels": ["k_frame_prep", "k_recon"],
+                    "achieved": round(path_achieved, 1),
+                    "frac": round(path_achieved / PEAK_HBM_GBS, 4),
+                    "avg_us": round(path_ms * 1e3, 2),
+                    "prep_avg_launch_us": round(prep_ms * 1e3, 2),
+                    "note": "the whole 4K inter-reconstruction path of a batched P launch: side info + MC words + "
+                            "dequant + inverse transform of every coded TU (k_frame_prep), then MC + residual add "
+                            "+ stores (k_recon); same algorithmic bytes over the sum of both kernels' launch "
+                            "durations (hipEvents on the decode stream)",
+                },
                 "launches": "batched P-frame decode launches of group 0 alone (streams of clips 0..7, the inter "
                             "stage: one k_recon launch -- 128x16 units, the frames' multi-key units first); "
                             "hipEvents on its stream",

@@ -148,6 +148,12 @@ typedef struct thor_frame_in {
   int32_t n_tu;
   const uint32_t *clpf_list; /* indices of the SBs whose CLPF flag is set (thor_build_clpf_list) */
   int32_t n_clpf;            /* -1: no list, scan every SB's flag */
+  /* k_recon units (128x16 luma) that hold several (MV, reference) keys in a
+   * half SB (thor_build_slow_list): dispatched first, so their long per-cell
+   * path overlaps the planned units instead of forming the launch's tail.
+   * NULL: no list (every unit in planned order, same output). */
+  const uint32_t *slow_list;
+  int32_t n_slow;
 } thor_frame_in_t;
 
 /* Decode one frame in each of `n` DIFFERENT contexts with one launch per stage
@@ -216,6 +222,13 @@ int thor_build_clpf_list(const uint8_t *host_flags, int nsb, uint32_t *out);
  * quarters in raster order, chroma of 8x8 CUs unsplit.  `out` may be NULL to
  * count; returns the count. */
 int thor_build_tu_list(const thor_block_t *host_blocks, int nblocks, thor_tu_t *out);
+/* Host helper: the frame's multi-key reconstruction units (thor_frame_in_t
+ * slow_list), ascending.  A half SB (64x32 luma) is multi-key when it holds an
+ * inter CU smaller than 64x64, or is a half inside the frame of a 64x64 INTER /
+ * BIPRED CU whose two quarters there differ in a motion vector; a unit (128x16
+ * luma: SB pair p, slice row 4 x SB row + quarter) is listed when the half of
+ * either of its SBs is.  `out` may be NULL to count; returns the count. */
+int thor_build_slow_list(const thor_block_t *host_blocks, int nblocks, int width, int height, uint32_t *out);
 
 /* Stage control for parity debugging: 0 recon only, 1 +deblock, 2 +CLPF (default 2). */
 int thor_dec_set_stop_stage(thor_dec_t *d, int stage);

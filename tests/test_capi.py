@@ -103,3 +103,60 @@ def test_build_tu_list_host_helper():
     assert out[4]["comp"] == 1 and out[4]["size"] == 4 and out[4]["qp"] == 36 and (out[4]["y"], out[4]["x"]) == (32, 16)
     # CU 2 (8x8 intra, tb split): four 4x4 luma TUs, q = 4
     assert out[12:]["coeff_off"].tolist() == [900, 916, 932, 948] and set(out[12:]["size"]) == {4}
+
+
+def _slow_units_py(b, W, H):
+    """numpy restatement of the multi-key half classification (recon.hip prep_body)
+    -> the set of k_recon units (128x16 luma) holding such a half."""
+    sbw, sbh = (W + 63) // 64, (H + 63) // 64
+    np_ = (sbw + 1) // 2
+    slow = set()
+    for B in b:
+        if B["mode"] == 1:
+            continue
+        sbx, sby = int(B["xpos"]) // 64, int(B["ypos"]) // 64
+        if int(B["size"]) < 64:
+            slow.add((sbx, sby, int(int(B["ypos"]) % 64 >= 32)))
+            continue
+        quarters = B["mode"] in (2, 3)
+        bi = B["mode"] == 3 or (B["mode"] in (0, 4) and B["dir"] == 2)
+        m0, m1 = B["mv0"].reshape(4, 2), B["mv1"].reshape(4, 2)
+        for h in range(2):
+            q0, q1 = (2 * h, 2 * h + 1) if quarters else (0, 0)
+            same = (m0[q0] == m0[q1]).all() and (not bi or (m1[q0] == m1[q1]).all())
+            if not same and int(B["ypos"]) + 32 * h < H:
+                slow.add((sbx, sby, h))
+    return sorted({(4 * sby + 2 * h + j) * np_ + sbx // 2 for (sbx, sby, h) in slow for j in range(2)})
+
+
+def test_build_slow_list_host_helper():
+    """thor_build_slow_list == the numpy restatement on hand-made CUs and on every
+    frame of golden streams (the reference encoder's .bit, host-parsed)."""
+    import numpy as np
+    from thor_amd.bitstream import parse_stream
+    from thor_amd.trace import BLOCK_DTYPE
+
+    lib = L.load()
+
+    def host(b, W, H):
+        b = np.ascontiguousarray(b, dtype=BLOCK_DTYPE)
+        n = lib.thor_build_slow_list(b.ctypes.data, len(b), W, H, None)
+        out = np.zeros(max(n, 1), np.uint32)
+        assert lib.thor_build_slow_list(b.ctypes.data, len(b), W, H, out.ctypes.data) == n
+        return out[:n].tolist()
+
+    b = np.zeros(4, BLOCK_DTYPE)
+    b["mode"] = [2, 0, 1, 3]
+    b["size"] = [64, 64, 32, 64]
+    b["xpos"], b["ypos"] = [0, 64, 128, 192], [0, 0, 0, 64]
+    b["mv0"][0] = [4, 0, 4, 0, 8, 0, 4, 0]  # INTER 64x64: quarters 2 and 3 differ -> half 1 multi-key
+    b["mv0"][3][0] = 2  # BIPRED 64x64 at SB (3, 1): quarter 0 differs from 1 -> half 0
+    got = host(b, 256, 128)
+    assert got == _slow_units_py(b, 256, 128)
+    assert got == [2 * 2 + 0, 3 * 2 + 0, (4 + 0) * 2 + 1, (4 + 1) * 2 + 1]
+    assert host(b[:0], 256, 128) == []
+    assert lib.thor_build_slow_list(None, 3, 256, 128, None) < 0
+    for name in ("cif_high.bit", "hd_low.bit", "k4_med.bit", "cif_hdb.bit"):
+        seq, frames = parse_stream(open(os.path.join(ROOT, "tests", "golden", name), "rb").read())
+        for fr in frames:
+            assert host(fr.blocks, seq.width, seq.height) == _slow_units_py(fr.blocks, seq.width, seq.height), name

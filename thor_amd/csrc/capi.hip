@@ -15,7 +15,7 @@
 
 // kernels (intra.hip, inter.hip, loopfilter.hip): the frame batch by value, first argument
 __global__ void k_frame_prep(const FrameBatch);
-__global__ void k_recon(const FrameBatch, int, unsigned long long *);
+__global__ void k_recon(const FrameBatch, int, int, unsigned long long *);
 __global__ void k_intra(const FrameBatch, unsigned long long *, int);
 __global__ void k_deblock_v(const FrameBatch, int, int);
 __global__ void k_deblock_h(const FrameBatch, int, int);
@@ -220,7 +220,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->ewy = (W + 2 * EDGE_MARGIN + 15) & ~15;
   d->ewc = (W / 2 + 2 * EDGE_MARGIN + 15) & ~15;
   ok = ok && dev_alloc(&d->edge, (size_t)((H + 63) / 64) * (d->ewy + 2 * d->ewc), "thor_dec_create: edge rows");
-  const size_t nplan = hplan_entries(W, H);  // plans, then the slow list (common.h)
+  const size_t nplan = hplan_entries(W, H);  // per half-SB plans (common.h)
   ok = ok && dev_alloc(&d->hplan, nplan * sizeof(uint4), "thor_dec_create: half-SB plans");
   ok = ok && hipMemset(d->hplan, 0, nplan * sizeof(uint4)) == hipSuccess;  // tag 0: no plan (gen starts at 1)
   ok = ok && hipMemset(d->ctl, 0, 64) == hipSuccess;
@@ -395,7 +395,7 @@ struct Batch {
   int n, cur[THOR_MAX_BATCH], frame_num[THOR_MAX_BATCH];
   // interpolated reference per frame: source slots (-1: none) and interpolate_frames' (ratio, pos)
   int ia[THOR_MAX_BATCH], ib[THOR_MAX_BATCH], iratio[THOR_MAX_BATCH], ipos[THOR_MAX_BATCH];
-  int max_prep, any_intra, any_clpf, any_deblock, clpf_grid, max_intra;
+  int max_prep, any_intra, any_clpf, any_deblock, clpf_grid, max_intra, max_slow;
   int intra_done;  // thor_dec_frame_intra ran the intra stage already
 };
 
@@ -412,6 +412,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     if (in.nblocks < 0 || (in.nblocks > 0 && !in.blocks)) return THOR_ERR_ARG;
     if (in.n_intra < 0 || (in.n_intra > 0 && !in.intra_list)) return THOR_ERR_ARG;
     if (in.n_tu < 0 || (in.n_tu > 0 && (!in.tu_list || !in.coeffs))) return THOR_ERR_ARG;
+    if (in.slow_list && (in.n_slow < 0 || in.n_slow > unit_count(W, H))) return THOR_ERR_ARG;
   }
   memset(&b.fb, 0, sizeof(b.fb));
   b.n = n;
@@ -420,6 +421,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
   b.any_intra = b.any_clpf = b.any_deblock = 0;
   b.clpf_grid = 0;
   b.max_intra = 0;
+  b.max_slow = 0;
   for (int i = 0; i < n; i++) {
     thor_dec *d = ds[i];
     const thor_frame_in_t &in = ins[i];
@@ -441,6 +443,9 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.hplan = d->hplan;
     if (++d->plan_gen == 0) d->plan_gen = 1;  // tag 0 marks "no plan"
     f.gen = (int)d->plan_gen;
+    f.slow = in.slow_list;
+    f.nslow = in.slow_list ? in.n_slow : 0;
+    b.max_slow = b.max_slow > f.nslow ? b.max_slow : f.nslow;
     f.blk = in.blocks;
     f.coeffs = in.coeffs;
     f.tus = in.tu_list;
@@ -540,10 +545,11 @@ static int batch_phase_a(thor_dec *lead, const Batch &b) {
   }
   {
     StageMark m(lead, ST_INTER);  // k_recon alone: the inter-reconstruction roofline kernel
-    // one flat grid: every frame's slow-list slots first (frame-interleaved), then
-    // each frame's halves in XCD-major order (inter.hip)
-    k_recon<<<dim3(n * (SLOW_CAP + 8 * ((unit_count(W, H) + 7) / 8)), 1), 64, recon_lds_pad(), st>>>(b.fb, n,
-                                                                                               lead->dbg_recon);
+    // one flat grid: every frame's slow-list units first (frame-interleaved, as
+    // many slots as the longest list), then each frame's units in XCD-major order
+    // (inter.hip)
+    k_recon<<<dim3(n * (b.max_slow + 8 * ((unit_count(W, H) + 7) / 8)), 1), 64, recon_lds_pad(), st>>>(
+        b.fb, n, b.max_slow, lead->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   return THOR_OK;
@@ -786,7 +792,7 @@ int thor_dec_frame(thor_dec_t *d, const thor_frame_hdr_t *hdr, const thor_block_
                    const int16_t *coeffs, const uint8_t *clpf_flags, const uint32_t *intra_list, int n_intra,
                    const thor_tu_t *tu_list, int n_tu) {
   if (!d || !hdr) return THOR_ERR_ARG;
-  thor_frame_in_t in = {blocks, nblocks, coeffs, clpf_flags, intra_list, n_intra, tu_list, n_tu, nullptr, -1};
+  thor_frame_in_t in = {blocks, nblocks, coeffs, clpf_flags, intra_list, n_intra, tu_list, n_tu, nullptr, -1, nullptr, 0};
   return thor_dec_frames(&d, 1, hdr, &in);
 }
 

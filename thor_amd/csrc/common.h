@@ -104,6 +104,8 @@ struct FrameCtx {
   // per-cell resolution.  Null: no plans (every half takes the per-cell path).
   uint4 *hplan;
   int gen;
+  const uint32_t *slow;  // the frame's multi-key units (null: none listed, every unit in planned order)
+  int nslow;
 };
 // A batch of frames travels in the kernel argument segment (8 x 384 B, under
 // the 4 KB kernarg limit): the host fills it per call, no upload copy.  Every
@@ -129,23 +131,15 @@ __host__ __device__ __forceinline__ int half_count(int W, int H) { return 2 * ((
 __host__ __device__ __forceinline__ int unit_pairs(int W) { return (((W + 63) >> 6) + 1) >> 1; }
 __host__ __device__ __forceinline__ int unit_count(int W, int H) { return unit_pairs(W) * 4 * ((H + 63) >> 6); }
 
-// The slow list of a frame: the units with several (MV, reference) keys in a
-// half (k_frame_prep appends them; k_recon dispatches them ahead of the planned
-// units so their long per-cell path overlaps the rest of the launch instead of
-// forming its tail).  It lives behind the plans in the hplan allocation (uint4s):
-//   [0, nh)                 per-half plans, .w == gen: planned (FrameCtx::hplan)
-//   [nh]                    u64 {count, gen} (count valid iff the high word == gen)
-//   [nh + 1, +SLOW_CAP/4)   SLOW_CAP list entries (unit indices)
-//   then                    u64 per unit {list position, gen} (claimed iff the high word == gen)
-// A slow unit at list position >= SLOW_CAP is reconstructed by its own
-// (planned-order) workgroup.
-#define SLOW_CAP 128
-__host__ __device__ __forceinline__ size_t hplan_utag_off(int W, int H) {
-  return (size_t)half_count(W, H) + 1 + SLOW_CAP / 4;
-}
-__host__ __device__ __forceinline__ size_t hplan_entries(int W, int H) {
-  return hplan_utag_off(W, H) + (size_t)(unit_count(W, H) + 1) / 2;
-}
+// The slow list of a frame (thor_frame_in_t::slow_list, built on the host by
+// thor_build_slow_list): the units with several (MV, reference) keys in a half.
+// k_recon dispatches them ahead of the planned units so their long per-cell
+// path overlaps the rest of the launch instead of forming its tail.  With a
+// list, k_frame_prep tags each multi-key half's plan record {.y = PLAN_SLOW,
+// .w = gen} (plain stores of one value, no atomics), and a planned-order
+// workgroup whose unit holds such a half leaves it to the list.
+#define PLAN_SLOW 0x80000000u
+__host__ __device__ __forceinline__ size_t hplan_entries(int W, int H) { return (size_t)half_count(W, H); }
 
 // Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits
 // (replaces the 44-byte deblock_data_t, common/types.h:127-135):

@@ -5,6 +5,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/thor_amd.h"
 
 // chroma_qp, common/common_block.c:78-83 (clamped index)
@@ -65,5 +67,46 @@ int thor_build_intra_list(const thor_block_t *host_blocks, int nblocks, uint32_t
       if (out) out[n] = (uint32_t)b;
       n++;
     }
+  return n;
+}
+
+// The multi-key k_recon units of a frame (include/thor_amd.h).  Restates the
+// classification k_frame_prep applies when it writes the half-SB plans
+// (prep_body, recon.hip): a half SB is planned when one 64x64 inter CU covers it
+// with one (MV, reference) key per prediction pass, and multi-key when it holds
+// a smaller inter CU or a 64x64 INTER / BIPRED CU whose two quarters there differ
+// (mv_arr per quarter, dec/decode_block.c:381-392).  Units in ascending order.
+int thor_build_slow_list(const thor_block_t *host_blocks, int nblocks, int width, int height, uint32_t *out) {
+  if (nblocks < 0 || (nblocks > 0 && !host_blocks) || width <= 0 || height <= 0) return THOR_ERR_ARG;
+  const int sbw = (width + 63) >> 6, sbh = (height + 63) >> 6, np = (sbw + 1) >> 1;
+  std::vector<uint8_t> slow((size_t)2 * sbw * sbh, 0);  // per half SB (FrameCtx::hplan order)
+  for (int b = 0; b < nblocks; b++) {
+    const thor_block_t &B = host_blocks[b];
+    if (B.mode == 1 /* M_INTRA */) continue;
+    const int sbx = B.xpos >> 6, sby = B.ypos >> 6;
+    if (sbx >= sbw || sby >= sbh) continue;  // outside the frame: k_frame_prep marks nothing either
+    const int hs = 2 * (sby * sbw + sbx);
+    if (B.size < 64) {
+      slow[hs + ((B.ypos & 63) >= 32)] = 1;
+      continue;
+    }
+    const bool quarters = B.mode == 2 || B.mode == 3;  // M_INTER, M_BIPRED
+    const bool bi = B.mode == 3 || ((B.mode == 0 || B.mode == 4) && B.dir == 2);
+    for (int h = 0; h < 2; h++) {
+      const int q0 = quarters ? 2 * h : 0, q1 = quarters ? 2 * h + 1 : 0;
+      const bool same = B.mv0[2 * q0] == B.mv0[2 * q1] && B.mv0[2 * q0 + 1] == B.mv0[2 * q1 + 1] &&
+                        (!bi || (B.mv1[2 * q0] == B.mv1[2 * q1] && B.mv1[2 * q0 + 1] == B.mv1[2 * q1 + 1]));
+      if (!same && B.ypos + 32 * h < height) slow[hs + h] = 1;
+    }
+  }
+  int n = 0;
+  for (int sby = 0; sby < sbh; sby++)
+    for (int q = 0; q < 4; q++)  // slice row 4 x sby + q: half q >> 1
+      for (int p = 0; p < np; p++) {
+        const int h = q >> 1, l = 2 * (sby * sbw + 2 * p) + h;
+        if (!slow[l] && !(2 * p + 1 < sbw && slow[l + 2])) continue;
+        if (out) out[n] = (uint32_t)((4 * sby + q) * np + p);
+        n++;
+      }
   return n;
 }

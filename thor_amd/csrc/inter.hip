@@ -892,11 +892,12 @@ __device__ __forceinline__ void plan_pass(ReconLds &L, const FrameCtx &f, __amdg
 #ifndef RECON_WPE
 #define RECON_WPE 1
 #endif
-__global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, int nfr, unsigned long long *__restrict__ dbg) {
+__global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, int nfr, int maxslow,
+                                                           unsigned long long *__restrict__ dbg) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ ReconLds L;
   const int lane = threadIdx.x;
-  // Flat grid (capi.hip): blocks [0, nfr x SLOW_CAP) take the frames' slow-list
+  // Flat grid (capi.hip): blocks [0, nfr x maxslow) take the frames' slow-list
   // entries (frame-interleaved, so every frame's multi-key units start first);
   // then each frame's NU blocks walk its units in XCD-major order --
   // workgroup b runs on XCD b % 8 (round-robin dispatch), so each XCD gets a
@@ -904,18 +905,16 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
   // rows in that XCD's L2.  Speed only, never correctness.
   const int W0 = F[0].W, H0 = F[0].H;
   const int sbw = (W0 + 63) >> 6, np = unit_pairs(W0), nu = unit_count(W0, H0), NU = 8 * ((nu + 7) >> 3);
-  const int nh = half_count(W0, H0);
-  const int nslow = nfr * SLOW_CAP;
+  const int nslow = nfr * maxslow;
   int fi, u;
   bool listed = false;
   if ((int)blockIdx.x < nslow) {
     fi = blockIdx.x % nfr;
     const int idx = blockIdx.x / nfr;
     const FrameCtx &f = F[fi];
-    if (!f.hplan || f.nblocks <= 0) return;
-    const unsigned long long c = *(const unsigned long long *)(f.hplan + nh);
-    if ((unsigned)(c >> 32) != (unsigned)f.gen || idx >= (int)(unsigned)c) return;
-    u = (int)((const unsigned *)(f.hplan + nh + 1))[idx];
+    if (!f.slow || f.nblocks <= 0 || idx >= f.nslow) return;
+    u = (int)f.slow[idx];
+    if (u >= nu) return;  // (the host builder never lists one)
     listed = true;
   } else {
     const int b = blockIdx.x - nslow;
@@ -964,21 +963,16 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
   // key per pass) -- no per-cell resolution (P0): scalar loads, then straight
   // to the window staging ----
   if (f.hplan && !listed) {
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     typedef unsigned u32x16 __attribute__((ext_vector_type(16)));
-    u32x2 tg;  // the unit's slow-list tag {position, gen}
     u32x16 pv;  // plans of halves hsb and hsb + 2 (scalar, uniform loads through the constant cache)
     const int hsb = 2 * (sby * sbw + 2 * pr) + h;
-    const unsigned long long *utag = (const unsigned long long *)(f.hplan + hplan_utag_off(W0, H0)) + u;
-    asm volatile("s_load_dwordx2 %0, %2, 0x0\n\ts_load_dwordx16 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(tg), "=&s"(pv)  // early clobber: the first load must not land in the second's address
-                 : "s"(utag), "s"(f.hplan + hsb)
-                 : "memory");
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(pv) : "s"(f.hplan + hsb) : "memory");
     STAMP(1);
-    if (tg.y == (unsigned)f.gen && tg.x < SLOW_CAP) return;  // a slow-list block has it
     const uint4 pa = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 pb = bex ? make_uint4(pv[8], pv[9], pv[10], pv[11]) : pa;
-    if ((int)pa.w == f.gen && (int)pb.w == f.gen) {
+    const bool cura = (int)pa.w == f.gen, curb = (int)pb.w == f.gen;
+    if ((cura && (pa.y & PLAN_SLOW)) || (curb && (pb.y & PLAN_SLOW))) return;  // a slow-list block has it
+    if (cura && curb) {
       const __amdgpu_buffer_rsrc_t ring =
           __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
       const unsigned ma = pa.y, mb = pb.y;

@@ -12,43 +12,14 @@
 // the packed side-info that copy_deblock_data (dec/decode_block.c:122-156)
 // stores for deblocking/CLPF.
 // ---------------------------------------------------------------------------
-// A half with several (MV, reference) keys: its two k_recon units join the
-// frame's slow list (common.h).  The first claimant of a unit this frame tags it
-// and appends it (count and tags are generation-stamped, so nothing is cleared
-// between frames).
-__device__ __forceinline__ void slow_claim(const FrameCtx &f, int sbx, int sby, int h) {
-  const int nh = half_count(f.W, f.H), np = unit_pairs(f.W);
-  unsigned long long *cnt = (unsigned long long *)(f.hplan + nh);
-  unsigned long long *utag = (unsigned long long *)(f.hplan + hplan_utag_off(f.W, f.H));
-  const unsigned long long g = (unsigned long long)(unsigned)f.gen << 32;
-  for (int j = 0; j < 2; j++) {
-    const int u = (4 * sby + 2 * h + j) * np + (sbx >> 1);
-    unsigned long long o = __hip_atomic_load(&utag[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool won = false;
-    while ((o >> 32) != (g >> 32)) {
-      const unsigned long long r = atomicCAS(&utag[u], o, g | 0xffffffffull);
-      if (r == o) {
-        won = true;
-        break;
-      }
-      o = r;
-    }
-    if (!won) continue;  // another CU of this unit got there first
-    unsigned long long c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned idx;
-    for (;;) {
-      const bool cur = (c >> 32) == (g >> 32);
-      const unsigned long long nw = cur ? c + 1 : (g | 1ull);
-      const unsigned long long r = atomicCAS(cnt, c, nw);
-      if (r == c) {
-        idx = cur ? (unsigned)c : 0u;
-        break;
-      }
-      c = r;
-    }
-    if (idx < SLOW_CAP) ((unsigned *)(f.hplan + nh + 1))[idx] = (unsigned)u;
-    __hip_atomic_store(&utag[u], g | idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+// A half with several (MV, reference) keys: tag its plan record as multi-key
+// (common.h), so the planned-order workgroup of each of its two k_recon units
+// leaves them to the slow-list workgroups (thor_build_slow_list lists the same
+// units).  Every CU of the half stores the same record: no atomics.
+__device__ __forceinline__ void slow_mark(const FrameCtx &f, int sbx, int sby, int h) {
+  const int sbw = (f.W + 63) >> 6;
+  if (sbx >= sbw || sby >= ((f.H + 63) >> 6)) return;
+  f.hplan[2 * (sby * sbw + sbx) + h] = make_uint4(0u, PLAN_SLOW, 0u, (unsigned)f.gen);
 }
 
 __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
@@ -111,16 +82,17 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   // (always so for SKIP / MERGE, which use mv_arr[0]; INTER / BIPRED halves of
   // a horizontal split too).
   // Every other half with inter work (smaller inter CUs, or a 64x64 INTER / BIPRED
-  // half whose two quarters differ) is multi-key: its first claimant appends it
-  // to the frame's slow list, which k_recon dispatches ahead of the planned halves.
-  if (f.hplan && S < 64 && lane == 0 && mode != M_INTRA) slow_claim(f, B.xpos >> 6, B.ypos >> 6, (B.ypos & 63) >= 32);
-  if (f.hplan && S == 64 && lane < 2 && mode != M_INTRA && s0 >= 0 && (!bi || s1 >= 0)) {
+  // half whose two quarters differ) is multi-key: with a slow list its record is
+  // tagged so (slow_mark), the list's workgroups reconstruct its units first.
+  if (f.hplan && f.slow && S < 64 && lane == 0 && mode != M_INTRA)
+    slow_mark(f, B.xpos >> 6, B.ypos >> 6, (B.ypos & 63) >= 32);
+  if (f.hplan && S == 64 && lane < 2 && mode != M_INTRA) {
     const int h = lane, q0 = quarters ? 2 * h : 0, q1 = quarters ? 2 * h + 1 : 0;
     const bool same = B.mv0[2 * q0] == B.mv0[2 * q1] && B.mv0[2 * q0 + 1] == B.mv0[2 * q1 + 1] &&
                       (!bi || (B.mv1[2 * q0] == B.mv1[2 * q1] && B.mv1[2 * q0 + 1] == B.mv1[2 * q1 + 1]));
     const bool inside = B.ypos + 32 * h < f.H;  // rows / columns past the frame edge are not stored (k_recon)
-    if (!same && inside) slow_claim(f, B.xpos >> 6, B.ypos >> 6, h);
-    if (same && inside) {
+    if (!same && inside && f.slow) slow_mark(f, B.xpos >> 6, B.ypos >> 6, h);
+    if (same && inside && s0 >= 0 && (!bi || s1 >= 0)) {
       int m0x = B.mv0[2 * q0], m0y = B.mv0[2 * q0 + 1], m1x = B.mv1[2 * q0], m1y = B.mv1[2 * q0 + 1];
       if (sg0) { m0x = -m0x; m0y = -m0y; }
       if (sg1) { m1x = -m1x; m1y = -m1y; }

@@ -38,6 +38,8 @@ class DeviceFrame:
     n_tu: int
     clpfl: int
     n_clpf: int
+    slow: int
+    n_slow: int
     nbytes: int  # bytes uploaded (descriptors + coefficients + flags + list)
 
 
@@ -107,6 +109,7 @@ class GpuDecoder:
         if not self.h:
             raise L.create_error("thor_dec_create")
         self._bufs = []
+        self.use_slow_list = True  # False: every k_recon unit in planned order (same output; tests compare both)
 
     def close(self):
         for b in self._bufs:
@@ -155,8 +158,12 @@ class GpuDecoder:
         clist = np.zeros(max(n_clpf, 1), np.uint32)
         if flags.size:
             self.lib.thor_build_clpf_list(flags.ctypes.data, len(flags), clist.ctypes.data)
+        W, H = self.seq.width, self.seq.height
+        n_slow = self.lib.thor_build_slow_list(blocks.ctypes.data, len(blocks), W, H, None)
+        slist = np.zeros(max(n_slow, 1), np.uint32)
+        self.lib.thor_build_slow_list(blocks.ctypes.data, len(blocks), W, H, slist.ctypes.data)
         # one host image, one device buffer, one copy (256-byte aligned parts)
-        parts = [blocks, coeffs, flags, ilist, tlist, clist]
+        parts = [blocks, coeffs, flags, ilist, tlist, clist, slist]
         offs, o = [], 0
         for a in parts:
             offs.append(o)
@@ -165,12 +172,12 @@ class GpuDecoder:
         for a, off in zip(parts, offs):
             img[off:off + a.nbytes] = a.view(np.uint8).reshape(-1)
         base = self._buf(img, pool, 0).ptr
-        bp, cp, fp, ip, tp, lp = (base + off for off in offs)
+        bp, cp, fp, ip, tp, lp, sp = (base + off for off in offs)
         hdr = L.ThorFrameHdr(fr.frame_num, fr.frame_type, fr.qp, fr.clpf_on,
                              (C.c_int32 * 2)(*fr.interp_refs), fr.interp_ratio, fr.interp_pos)
-        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + TU_DTYPE.itemsize * n_tu
+        nbytes = blocks.nbytes + coeffs.nbytes + flags.nbytes + 4 * n_intra + TU_DTYPE.itemsize * n_tu + 4 * n_slow
         return DeviceFrame(hdr, bp, len(blocks), cp, fp if flags.size else 0, ip, n_intra, tp, n_tu, lp, n_clpf,
-                           nbytes)
+                           sp, n_slow, nbytes)
 
     def decode(self, d: DeviceFrame):
         fi = self.frame_in(d)
@@ -179,7 +186,8 @@ class GpuDecoder:
 
     def frame_in(self, d: DeviceFrame) -> L.ThorFrameIn:
         return L.ThorFrameIn(d.blocks, d.nblocks, d.coeffs, d.clpf or None, d.intra, d.n_intra, d.tus, d.n_tu,
-                             d.clpfl if d.clpf else None, d.n_clpf if d.clpf else -1)
+                             d.clpfl if d.clpf else None, d.n_clpf if d.clpf else -1,
+                             d.slow if self.use_slow_list else None, d.n_slow)
 
     # ---- row-band sharding (thor_amd/shard.py) ----
     def set_band(self, sb_row0: int, sb_row1: int):

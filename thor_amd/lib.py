@@ -43,7 +43,7 @@ class ThorEncParams(C.Structure):
 class ThorFrameIn(C.Structure):
     _fields_ = [("blocks", C.c_void_p), ("nblocks", C.c_int32), ("coeffs", C.c_void_p), ("clpf_flags", C.c_void_p),
                 ("intra_list", C.c_void_p), ("n_intra", C.c_int32), ("tu_list", C.c_void_p), ("n_tu", C.c_int32),
-                ("clpf_list", C.c_void_p), ("n_clpf", C.c_int32)]
+                ("clpf_list", C.c_void_p), ("n_clpf", C.c_int32), ("slow_list", C.c_void_p), ("n_slow", C.c_int32)]
 
 
 class ThorParsedFrame(C.Structure):
@@ -56,7 +56,7 @@ class ThorParsedFrame(C.Structure):
 # Every symbol the public headers declare (checked by tests/test_capi.py).
 BATCHED_SYMBOLS = [
     "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_dec_frames", "thor_dec_frame_begin",
-    "thor_dec_frame_end", "thor_dec_set_band", "thor_dec_set_band_local", "thor_dec_frame_finish", "thor_dec_set_band_intra", "thor_dec_frame_intra", "thor_dec_get_rows", "thor_dec_put_rows", "thor_dec_put_ref_rows", "thor_dec_pad_frame", "thor_build_intra_list", "thor_build_tu_list", "thor_build_clpf_list", "thor_dec_set_stop_stage",
+    "thor_dec_frame_end", "thor_dec_set_band", "thor_dec_set_band_local", "thor_dec_frame_finish", "thor_dec_set_band_intra", "thor_dec_frame_intra", "thor_dec_get_rows", "thor_dec_put_rows", "thor_dec_put_ref_rows", "thor_dec_pad_frame", "thor_build_intra_list", "thor_build_tu_list", "thor_build_clpf_list", "thor_build_slow_list", "thor_dec_set_stop_stage",
     "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_stage_marks", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
@@ -128,6 +128,8 @@ def load(path: str = LIB_PATH):
     L.thor_build_tu_list.restype = i
     L.thor_build_clpf_list.argtypes = [P, i, P]
     L.thor_build_clpf_list.restype = i
+    L.thor_build_slow_list.argtypes = [P, i, i, i, P]
+    L.thor_build_slow_list.restype = i
     L.thor_dec_set_stop_stage.argtypes = [P, i]
     L.thor_dec_read_frame.argtypes = [P, i, P, P, P]
     L.thor_dec_read_frame.restype = i

@@ -141,7 +141,21 @@ static void fuzz_lists(int it) {
   std::vector<uint32_t> cl(nc > 0 ? nc : 0);
   CHECK(thor_build_clpf_list(nb ? fl.data() : nullptr, nb, cl.data()) == nc, "it %d: CLPF count changed", it);
   for (size_t j = 1; j < cl.size(); j++) CHECK(cl[j] > cl[j - 1], "it %d: CLPF list not increasing", it);
+  for (thor_block_t &B : blk)
+    for (int k = 0; k < 8; k++) {
+      B.mv0[k] = (int16_t)(rnd() % 3 ? 0 : rnd());
+      B.mv1[k] = (int16_t)(rnd() % 3 ? 0 : rnd());
+    }
+  const int nu = 4 * 34 * 30;  // units of a 4K frame (unit_count, common.h)
+  const int ns = thor_build_slow_list(bp, nb, 3840, 2160, nullptr);
+  CHECK(ns >= 0 && ns <= nu, "it %d: %d slow units", it, ns);
+  std::vector<uint32_t> sl(ns > 0 ? ns : 0);
+  CHECK(thor_build_slow_list(bp, nb, 3840, 2160, sl.data()) == ns, "it %d: slow count changed", it);
+  for (size_t j = 0; j < sl.size(); j++)
+    CHECK(sl[j] < (uint32_t)nu && (j == 0 || sl[j] > sl[j - 1]), "it %d: slow list entry %u", it, sl[j]);
   // the argument errors
+  CHECK(thor_build_slow_list(nullptr, 3, 64, 64, nullptr) == THOR_ERR_ARG, "slow list null");
+  CHECK(thor_build_slow_list(bp, nb, 0, 64, nullptr) == THOR_ERR_ARG, "slow list width");
   CHECK(thor_build_tu_list(nullptr, 3, nullptr) == THOR_ERR_ARG, "tu list null");
   CHECK(thor_build_intra_list(bp, -1, nullptr) == THOR_ERR_ARG, "intra list negative");
   CHECK(thor_build_clpf_list(nullptr, 5, nullptr) == THOR_ERR_ARG, "clpf list null");

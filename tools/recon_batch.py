@@ -58,6 +58,10 @@ if timing:
     us = 1e3 * sum(rec) / len(rec)
     print("k_recon P launch (%d frames): avg %.2f us min %.2f us  alg %.1f MB  %.1f GB/s  frac %.3f" % (
         B, us, 1e3 * min(rec), alg / 1e6, alg / us / 1e3, alg / us / 1e3 / 8000.0))
+    prep = [per[r * nf + i][0] for r in range(reps) for i in pidx]
+    pus = 1e3 * sum(prep) / len(prep)
+    print("k_frame_prep P launch: avg %.2f us min %.2f max %.2f us;  path (prep + recon) %.2f us  frac %.3f" % (
+        pus, 1e3 * min(prep), 1e3 * max(prep), pus + us, alg / (pus + us) / 1e3 / 8000.0))
 for d in decs:
     d.close()
 print("decoded %d x %d frames of %s" % (reps, nf, name))
