@@ -82,8 +82,9 @@ def test_row_sharded_halo_exchange_matches_reference(name, nframes, world):
 
 # Boundary exchange (no pre-deblock all-gather either): edge rows for the band's intra
 # chains from the band above, 8 deblocking halo rows either side (thor_amd/shard.py)
-@pytest.mark.parametrize("name,nframes,world", [("k4_med", 8, 2), ("k4_med", 8, 3), ("cif_high", 10, 3),
-                                                ("hd_low", 6, 2), ("cif_hdbi", 9, 2), ("k4_hdbi", 9, 3)])
+@pytest.mark.parametrize("name,nframes,world", [("k4_med", 8, 2), ("k4_med", 8, 3), ("k4_med", 8, 4),
+                                                ("cif_high", 10, 3), ("hd_low", 6, 2), ("cif_hdbi", 9, 2),
+                                                ("k4_hdbi", 9, 3)])
 def test_row_sharded_boundary_exchange_matches_reference(name, nframes, world):
     _run_sharded(name, nframes, world, True, True, True)
 

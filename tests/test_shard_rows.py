@@ -18,11 +18,19 @@ def test_band_partition():
         for world in (1, 2, 3, 4, 8):
             rows = band_rows(H, world)
             assert rows % 64 == 0 and rows * world >= nsb * 64
-            covered = []
+            covered, sizes = [], []
             for r in range(world):
                 b0, b1 = band_of(H, world, r)
                 covered += list(range(b0, b1))
+                sizes.append(b1 - b0)
+                assert 64 * (b1 - b0) <= rows
             assert covered == list(range(nsb)), (H, world)
+            assert max(sizes) - min(sizes) <= 1, (H, world, sizes)  # balanced
+            if nsb >= world:
+                assert min(sizes) >= 1, (H, world, sizes)  # no empty band
+    # the north star's 8-way split: 4K = 34 SB rows -> 5, 5, 4 x 6; 1080p = 17 -> 3, 2 x 7
+    assert [band_of(2160, 8, r)[1] - band_of(2160, 8, r)[0] for r in range(8)] == [5, 5, 4, 4, 4, 4, 4, 4]
+    assert [band_of(1080, 8, r)[1] - band_of(1080, 8, r)[0] for r in range(8)] == [3, 2, 2, 2, 2, 2, 2, 2]
 
 
 class NumpyContext:
@@ -181,7 +189,8 @@ def _worker(rank, world, port, W, H, q, local=False):
 
 
 @pytest.mark.parametrize("world,W,H,local", [(2, 352, 288, False), (3, 256, 200, False), (2, 128, 64, False),
-                                             (2, 352, 288, True), (3, 256, 200, True)])
+                                             (2, 352, 288, True), (3, 256, 200, True), (8, 128, 2160, False),
+                                             (8, 128, 2160, True)])
 def test_row_shard_exchange_gloo(world, W, H, local):
     import random
 
@@ -281,7 +290,7 @@ def _halo_worker(rank, world, port, W, H, q):
         q.put((rank, repr(e) + traceback.format_exc()[-600:]))
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 192, 320), (3, 128, 448)])
+@pytest.mark.parametrize("world,W,H", [(2, 192, 320), (3, 128, 448), (8, 128, 2160)])
 def test_row_shard_halo_exchange_gloo(world, W, H):
     """Halo mode: no second all-gather; before each frame every rank fetches the
     reference rows its band's vectors reach from their owners, and those rows
@@ -316,6 +325,11 @@ def test_missing_rows_tracking():
     assert sh.final[5] == [(90, 300)]
     assert sh.missing({5: (100, 300)}) == []
     assert sh.missing({5: (0, 320), 6: (10, 20)}) == [(5, 0, 90), (5, 300, 320), (6, 10, 20)]
+    # frames that leave the reference window are forgotten (bounded over a long stream)
+    sh.decoded, sh.window = [], 3
+    for f in (5, 6, 7, 8):
+        sh._retire(f)
+    assert 5 not in sh.final and sh.decoded == [6, 7, 8]
 
 
 def _halo_interp_worker(rank, world, port, W, H, q):
@@ -458,7 +472,7 @@ def _boundary_worker(rank, world, port, W, H, q):
         q.put((rank, repr(e) + traceback.format_exc()[-800:]))
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 192, 320), (3, 128, 448)])
+@pytest.mark.parametrize("world,W,H", [(2, 192, 320), (3, 128, 448), (8, 128, 2160), (8, 96, 1080)])
 def test_row_shard_boundary_exchange_gloo(world, W, H):
     """Boundary mode: no pre-deblock all-gather -- the band below gets the two
     edge rows of the band above (after that band's intra chains when its last
@@ -479,7 +493,7 @@ def test_boundary_plan():
             return 3
 
     sh = object.__new__(RowShard)
-    sh.H, sh.world, sh.rank = 448, 3, 1  # 7 SB rows, bands of 3: [0,3) [3,6) [6,7)
+    sh.H, sh.world, sh.rank = 448, 3, 1  # 7 SB rows, balanced bands: [0,3) [3,5) [5,7)
     fr = FakeFrame(1, 128, 448, np.random.default_rng(0), reach=2)
     fr.blocks["mode"][:] = 2
     assert sh.boundary_plan(fr) == {}
@@ -487,5 +501,5 @@ def test_boundary_plan():
     fr.blocks["mode"][np.flatnonzero(rows == 3)[:1]] = 1  # band 1's first row: band 0 hands over early
     assert sh.boundary_plan(fr) == {0: "early"}
     fr.blocks["mode"][np.flatnonzero(rows == 2)[:1]] = 1  # band 0's last row has intra: late
-    fr.blocks["mode"][np.flatnonzero(rows == 6)[:1]] = 1  # band 2 has intra; band 1's last row (5) none
+    fr.blocks["mode"][np.flatnonzero(rows == 6)[:1]] = 1  # band 2 has intra; band 1's last row (4) none
     assert sh.boundary_plan(fr) == {0: "late", 1: "early"}

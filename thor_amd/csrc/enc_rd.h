@@ -444,15 +444,6 @@ TE_NOINL int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, 
   const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, yC = ypos / 2, xC = xpos / 2, sC = size / 2;
   const int mode = p.mode;
   const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
-  const int re_use = (bi.final_encode & 1) && !F.enable_tb_split;
-  if (re_use) {
-    te_copy_bytes(bi.rec, bi.rec_best, size * size + 2 * sC * sC);
-    if (bi.best_nbits >= 0 && &p == &bi.bp) {  // the best candidate's own syntax bits
-      te_put_kept(b, bi.best_bits, bi.best_nbits);
-      return bi.best_nbits;
-    }
-    return te_write_block(b, F, bi, p, S.tx->scan);
-  }
   uint8_t *recY = bi.rec, *recU = te_pu(bi.rec, size), *recV = te_pv(bi.rec, size);
   const int tb_split = TE_MAX(0, p.tb_param), zero_block = p.tb_param == -1;
   p.tb_split = tb_split;
@@ -522,6 +513,27 @@ TE_NOINL int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, 
 }
 TE_FN int te_encode_block(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
   return te_lds(&F)->frame_type == TE_I ? te_encode_block_t<true>(F, b, bi, p) : te_encode_block_t<false>(F, b, bi, p);
+}
+// The final encode of a block with its best parameters bi.bp (process_block,
+// enc/encode_block.c:2953-2962 / 3012-3018).  Without tb-split the best
+// candidate's reconstruction is in rec_best and (usually) its syntax bits in
+// best_bits: copy them here, inline, so this common case makes no call -- a
+// call of te_encode_block_t saves and restores ~100 callee-saved VGPRs through
+// scratch.  Otherwise it is a full encode.
+TE_FN int te_encode_final(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_) {
+  const TeFrame &F = *te_lds(&F_);
+  TeBlockInfo &bi = *te_lds(&bi_);
+  TeBits &b = *te_lds(&b_);
+  if (!F.enable_tb_split) {  // re_use
+    const int size = bi.size, sC = size / 2;
+    te_copy_bytes(bi.rec, bi.rec_best, size * size + 2 * sC * sC);
+    if (bi.best_nbits >= 0) {  // the best candidate's own syntax bits
+      te_put_kept(b, bi.best_bits, bi.best_nbits);
+      return bi.best_nbits;
+    }
+    return te_write_block(b, F, bi, bi.bp, te_here().tx->scan);
+  }
+  return te_encode_block(F, b, bi, bi.bp);
 }
 
 // cost_calc, enc/encode_block.c:1218-1228
@@ -1266,6 +1278,64 @@ TE_NOINL uint32_t te_mode_decision(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi
   return min_cost;
 }
 
+// mode_decision_rdo of an I frame (enc/encode_block.c:2204-2479 with only the
+// intra branch live: an I-frame CU is never rectangular, encode_this).  Inlined
+// into process_block: te_mode_decision's body, sized for the P / B candidates,
+// saves ~110 callee-saved VGPRs through scratch per call.
+TE_FN uint32_t te_mode_decision_intra(const TeFrame &F_, TeBlockInfo &bi_, TeBits &b_, int16_t *tmp_coef) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_here();
+  TeBlockInfo &bi = *te_lds(&bi_);
+  TeBits &b = *te_lds(&b_);
+  TE_P(TP_MODE);
+  const int size = bi.size;
+  uint32_t min_cost = TE_MAX_UINT32, cost;
+  int intra_mode = TE_DC;
+  const int pos_ref = b.pos;
+  TeParam &tmp = *S.tmp;
+  te_zero_words(&tmp, sizeof(TeParam));
+  te_sync();
+  tmp.coeff = tmp_coef;
+  tmp.cs = bi.bp.cs;
+  tmp.ts = bi.bp.ts;
+  const int max_tb = bi.max_num_tb_part - 1;
+  if (F.intra_rdo) {
+    uint32_t min_icost = TE_MAX_UINT32;
+    int best_mode = TE_DC;
+    for (int im = TE_DC; im < F.num_intra_modes; im++) {
+      tmp.intra_mode = im;
+      for (int tbp = 0; tbp <= max_tb; tbp++) {
+        tmp.tb_param = tbp;
+        tmp.mode = TE_INTRA;
+        const int nbits = te_encode_block_t<true>(F, b, bi, tmp);
+        cost = te_cost(F, bi, bi.rec, size, size, nbits);
+        if (cost < min_icost) {
+          min_icost = cost;
+          best_mode = im;
+        }
+      }
+    }
+    intra_mode = best_mode;
+  } else {
+    te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
+  }
+  tmp.intra_mode = intra_mode;
+  for (int tbp = 0; tbp <= max_tb; tbp++) {
+    tmp.tb_param = tbp;
+    tmp.mode = TE_INTRA;
+    const int nbits = te_encode_block_t<true>(F, b, bi, tmp);
+    cost = te_cost(F, bi, bi.rec, size, size, nbits);
+    if (cost < min_cost) {
+      min_cost = cost;
+      te_copy_best(bi, tmp);
+      te_keep_best_bits(b, bi, nbits);
+    }
+  }
+  te_rewind(b, pos_ref);  // rewind (:2476)
+  TE_TR(F.frame_num, 5, bi.ypos, bi.xpos, size, min_cost, bi.bp.mode, TE_MAX_UINT32);
+  return min_cost;
+}
+
 // ---- early skip (enc/encode_block.c:2481-2783) -------------------------------
 // check_early_skip_sub_block (luma, :2505-2538): 2x2-average + (N/2)-point
 // transform against half the threshold (N = 4: plain 4-point transform).
@@ -1485,7 +1555,7 @@ TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xp
       if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
-      const int nbit = te_encode_block(F, b, bi, bi.bp);
+      const int nbit = te_encode_final(F, b, bi);
       cost = te_cost(F, bi, bi.rec, SIZE, SIZE, nbit);
       te_commit_block(F, bi);
       return cost;
@@ -1505,7 +1575,8 @@ TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xp
   if (encode_this) {
     bi.final_encode = 0;
     // the tmp coefficient set: whichever of cbuf[0..1] the best does not hold
-    cost = te_mode_decision(F, sb, bi, bi.bp.coeff == cb0 ? cb1 : cb0);
+    int16_t *const tc = bi.bp.coeff == cb0 ? cb1 : cb0;
+    cost = ft == TE_I ? te_mode_decision_intra(F, bi, b, tc) : te_mode_decision(F, sb, bi, tc);
     const int me_threshold = SIZE * SIZE * te_iq8[qp] / 8;
     if constexpr (SIZE > 8) {
       if (top_down && cost > (uint32_t)me_threshold) {
@@ -1519,7 +1590,7 @@ TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xp
     if (cost <= cost_small) {
       te_rewind(b, pos_ref);
       bi.final_encode = 1;
-      te_encode_block(F, b, bi, bi.bp);
+      te_encode_final(F, b, bi);
       te_commit_block(F, bi);
     }
   } else if (encode_rect) {
@@ -1531,7 +1602,7 @@ TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xp
       if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
-      te_encode_block(F, b, bi, bi.bp);
+      te_encode_final(F, b, bi);
       te_commit_block(F, bi);
     }
   }

@@ -37,8 +37,10 @@ read across bands) plus the halo rows it does not hold yet.  Frames with a
 temporal-interpolated reference need both sources whole (the interpolation's
 motion search spans the frame) -- fetched once per source, not per frame.
 
-Band b covers SB rows [b*R, (b+1)*R), R = ceil(SB rows / world); the last band
-may run past the frame (those rows are not copied).
+Bands are balanced: with S SB rows over N ranks, the first S mod N bands hold
+floor(S / N) + 1 SB rows and the others floor(S / N) (4K, 34 rows over 8: 5, 5,
+4, 4, 4, 4, 4, 4), so no band is empty while S >= N.  The all-gather slots are
+sized for the largest band; each rank copies only its own rows.
 """
 from __future__ import annotations
 
@@ -50,16 +52,21 @@ MAX_REQ = 16  # reference ranges one rank may request per frame (MAX_REF_FRAMES-
 
 
 def band_rows(height: int, world: int) -> int:
-    """Luma rows per band: whole SB rows, equal for every rank (all-gather)."""
+    """Luma rows of the largest band (whole SB rows): the all-gather slot size."""
     nsb = (height + 63) // 64
     return ((nsb + world - 1) // world) * 64
 
 
 def band_of(height: int, world: int, rank: int):
-    """(first SB row, end SB row) of `rank`'s band (end clamped to the frame)."""
+    """(first SB row, end SB row) of `rank`'s band: balanced, the first
+    nsb mod world bands one SB row taller (empty only when nsb < world)."""
     nsb = (height + 63) // 64
-    r = band_rows(height, world) // 64
-    return min(rank * r, nsb), min((rank + 1) * r, nsb)
+    q, r = divmod(nsb, world)
+
+    def start(b):
+        return b * q + min(b, r)
+
+    return start(rank), start(rank + 1)
 
 
 def band_bytes(width: int, height: int, world: int) -> int:
@@ -139,6 +146,8 @@ class RowShard:
         self.halo = halo
         self.halo_bytes = []  # per frame: bytes this rank received in halo exchanges
         self.final = {}  # halo mode: frame_num -> sorted disjoint luma row ranges this rank holds final
+        self.decoded = []  # halo mode: frame numbers in decode order (the last `window` keep their `final` entry)
+        self.window = 34  # MAX_SLOTS (thor_amd/decoder.py): a frame further back is no longer a reference
         self.dec, self.dist = dec, dist
         self.W, self.H = width, height
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
@@ -188,6 +197,7 @@ class RowShard:
         if self.halo:
             self._fetch_halo(frame)
             self.final[int(frame_num)] = []  # (re)decoded: only this rank's band is final
+            self._retire(int(frame_num))
             lo, hi = self.owned(self.rank)
             if hi > lo:
                 self._hold(frame_num, lo, hi)
@@ -412,12 +422,16 @@ class RowShard:
         return got
 
     def _exchange(self, frame_num: int):
+        """All-gather of the bands' rows: rank r's slot holds its owned rows
+        [lo, hi), packed as get_rows packs hi - lo rows (slots sized for the
+        largest band)."""
         d = self.dec
-        y0 = self.rank * self.rows
+        y0, y1 = self.owned(self.rank)
         if self.device_exchange:
             import torch
 
-            d.get_rows(frame_num, y0, self.rows, self.send.data_ptr())
+            if y1 > y0:
+                d.get_rows(frame_num, y0, y1 - y0, self.send.data_ptr())
             cur = torch.cuda.current_stream()
             if self.dstream is not None:  # the band rows are in `send` before the all-gather reads them
                 ev = torch.cuda.Event()
@@ -429,16 +443,19 @@ class RowShard:
                 ev.record(cur)
                 self.dstream.wait_event(ev)
             for r in range(self.world):
-                if r != self.rank:
-                    d.put_rows(frame_num, r * self.rows, self.rows, self.recv.data_ptr() + r * self.nbytes)
+                a, b = self.owned(r)
+                if r != self.rank and b > a:
+                    d.put_rows(frame_num, a, b - a, self.recv.data_ptr() + r * self.nbytes)
         else:
-            d.get_rows(frame_num, y0, self.rows, self.scratch[self.rank])
-            d.d2h(self.send.numpy(), self.scratch[self.rank])  # waits for the decoder's stream
+            if y1 > y0:
+                d.get_rows(frame_num, y0, y1 - y0, self.scratch[self.rank])
+                d.d2h(self.send.numpy(), self.scratch[self.rank])  # waits for the decoder's stream
             self.dist.all_gather(self.recv, self.send)
             for r in range(self.world):
-                if r != self.rank:
+                a, b = self.owned(r)
+                if r != self.rank and b > a:
                     d.h2d(self.scratch[r], self.recv[r].numpy())
-                    d.put_rows(frame_num, r * self.rows, self.rows, self.scratch[r])
+                    d.put_rows(frame_num, a, b - a, self.scratch[r])
 
     def _fetch_halo_device(self, parts, dev):
         """_fetch_halo's data movement with device buffers (nccl = RCCL point
@@ -497,6 +514,15 @@ class RowShard:
         return got
 
     # ---- which rows of which frames this rank holds final (halo mode) ----
+    def _retire(self, f: int):
+        """Frame f was just decoded: forget what this rank holds of frames that
+        left the reference window (so `final` stays bounded over a long stream)."""
+        if f in self.decoded:
+            self.decoded.remove(f)
+        self.decoded.append(f)
+        while len(self.decoded) > self.window:
+            self.final.pop(self.decoded.pop(0), None)
+
     def _hold(self, f: int, a: int, c: int):
         iv = self.final.setdefault(int(f), [])
         iv.append((int(a), int(c)))
@@ -538,7 +564,7 @@ class RowShard:
         lo, hi = self.owned(self.rank)
         if hi > lo:
             buf = d.scratch(self.nbytes)
-            d.get_rows(frame_num, lo, self.rows, buf)
+            d.get_rows(frame_num, lo, hi - lo, buf)
             d.d2h(mine, buf)
         dev = torch.device("cuda", torch.cuda.current_device()) if self.device_exchange else None
         src = torch.from_numpy(mine).to(dev) if dev is not None else torch.from_numpy(mine)
@@ -554,8 +580,8 @@ class RowShard:
                 continue
             p = parts[r].cpu().numpy()
             y[a:b] = p[:n * W].reshape(n, W)
-            o = self.rows * W
+            o = n * W
             for pl in (u, v):
                 pl[a // 2:b // 2] = p[o:o + (n // 2) * (W // 2)].reshape(n // 2, W // 2)
-                o += (self.rows // 2) * (W // 2)
+                o += (n // 2) * (W // 2)
         return y.tobytes() + u.tobytes() + v.tobytes()
