@@ -434,7 +434,7 @@ TE_NOINL int te_enc_intra_comp_nc(const TeFrame &F_, const uint8_t *org, int os,
 // component); P / B frames use the other, whose body stays small for the
 // inter candidates that dominate them.
 template <bool IFR>
-TE_NOINL int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
+TE_FN int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_here();
   TeBlockInfo &bi = *te_lds(&bi_);
@@ -511,9 +511,22 @@ TE_NOINL int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, 
   if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
   return nbits;
 }
-TE_FN int te_encode_block(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
-  return te_lds(&F)->frame_type == TE_I ? te_encode_block_t<true>(F, b, bi, p) : te_encode_block_t<false>(F, b, bi, p);
+// The two out-of-line copies (one call frame each; the I-frame copy may also be
+// inlined where it has a single call site, TE_EB1_INLINE)
+TE_NOINL int te_encode_block_i(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_encode_block_t<true>(F, b, bi, p);
 }
+TE_NOINL int te_encode_block_p(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_encode_block_t<false>(F, b, bi, p);
+}
+TE_FN int te_encode_block(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_lds(&F)->frame_type == TE_I ? te_encode_block_i(F, b, bi, p) : te_encode_block_p(F, b, bi, p);
+}
+#ifdef TE_EB1_INLINE
+#define TE_ENCODE_I te_encode_block_t<true>
+#else
+#define TE_ENCODE_I te_encode_block_i
+#endif
 // The final encode of a block with its best parameters bi.bp (process_block,
 // enc/encode_block.c:2953-2962 / 3012-3018).  Without tb-split the best
 // candidate's reconstruction is in rec_best and (usually) its syntax bits in
@@ -612,6 +625,200 @@ TE_NOINL int te_search_intra(const TeFrame &F_, const TeBlockInfo &bi_, int num_
 
 TE_FN uint32_t te_lambda_bits(double lam, int bits) { return (uint32_t)(lam * (double)bits + 0.5); }
 
+#if !defined(TE_HOST)
+// ---- candidate-parallel motion search (device) ------------------------------
+// motion_estimate tries its candidates one at a time: each SAD a full-wave pass
+// that ends in a reduction and a scalar compare after a memory round trip, most
+// lanes idle for the small blocks.  The candidates of one search step are
+// independent -- only the choice among them is ordered -- so here a step's
+// candidates are evaluated together: the block's 4x4 units spread over the
+// lanes (nu = w/4 x h/4 units, a power of two: nu <= 64 gives 64 / nu
+// candidates per pass, one unit per lane; nu > 64, nu / 64 units per lane and
+// two candidates per pass), the original held in registers in the same layout,
+// one segmented DPP reduction per pass, then the reference's ordered scan over
+// the step's costs (strictly below the running minimum): the same argmin, ties
+// to the earlier candidate, as the one-at-a-time loop.
+struct TeMeBlk {
+  int w4, lw4, nu, lnu;  // units per row and its log2; units in the block and its log2
+  uint32_t o[4][4];      // original unit rows: o[t][y] = row y of the lane's unit t
+};
+TE_FN int te_me_unit(const TeMeBlk &B, int t) { return B.nu <= 64 ? (TE_LANE & (B.nu - 1)) : TE_LANE + 64 * t; }
+TE_FN void te_me_blk(TeMeBlk &B, const uint8_t *org, int os, int w, int h) {
+  B.w4 = w >> 2;
+  B.lw4 = __builtin_ctz(B.w4);
+  B.nu = B.w4 * (h >> 2);
+  B.lnu = __builtin_ctz(B.nu);
+  const int nt = B.nu > 64 ? B.nu >> 6 : 1;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+#pragma unroll
+    for (int y = 0; y < 4; y++) B.o[t][y] = 0;
+    if (t < nt) {
+      const int u = te_me_unit(B, t), i0 = (u >> B.lw4) * 4, j = (u & (B.w4 - 1)) * 4;
+#pragma unroll
+      for (int y = 0; y < 4; y++) B.o[t][y] = te_ld4(org + (i0 + y) * os + j);
+    }
+  }
+}
+// the lane's part of the SAD of the block at p (full-pel)
+TE_FN uint32_t te_me_sad_lane(const TeMeBlk &B, const uint8_t *p, int rs) {
+  const int nt = B.nu > 64 ? B.nu >> 6 : 1;
+  uint32_t s = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+    if (t < nt) {
+      const int u = te_me_unit(B, t), i0 = (u >> B.lw4) * 4, j = (u & (B.w4 - 1)) * 4;
+      const uint8_t *q = p + i0 * rs + j;
+      uint32_t d[4];
+#pragma unroll
+      for (int y = 0; y < 4; y++) d[y] = te_ld4(q + y * rs);
+#pragma unroll
+      for (int y = 0; y < 4; y++) s = te_sad4(B.o[t][y], d[y], s);
+    }
+  return s;
+}
+// the lane's part of the SAD of the sub-pel prediction at mv (te_mc_luma's
+// 4x4-unit form, common/inter_prediction.c:120-180, fused: no prediction buffer)
+TE_FN uint32_t te_me_mcsad_lane(const TeMeBlk &B, const uint8_t *ref, int rs, TeMv mv, int sign, int bipred) {
+  const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
+  const int fy = my & 3, fx = mx & 3;
+  const uint8_t *r = ref + (my >> 2) * rs + (mx >> 2);
+  const int nt = B.nu > 64 ? B.nu >> 6 : 1;
+  uint32_t s = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    if (t >= nt) continue;
+    const int u = te_me_unit(B, t), i0 = (u >> B.lw4) * 4, j = (u & (B.w4 - 1)) * 4;
+    int o[4][4];
+    if (fx == 2 && fy == 2) {  // rows -1..5, columns -1..6, :145-157
+      uint32_t lo[7], hi[7];
+#pragma unroll
+      for (int q = 0; q < 7; q++) {
+        const uint8_t *p = r + (i0 - 1 + q) * rs + j - 1;
+        lo[q] = te_ld4(p);
+        hi[q] = te_ld4(p + 4);
+      }
+      int c[7][8];
+#pragma unroll
+      for (int q = 0; q < 7; q++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          c[q][k] = te_b(lo[q], k);
+          c[q][k + 4] = te_b(hi[q], k);
+        }
+#pragma unroll
+      for (int y = 0; y < 4; y++)
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          const int k = x + 1;
+          const int *a = c[y], *b = c[y + 1], *d = c[y + 2], *e = c[y + 3];
+          const int v = a[k] + a[k + 1] + b[k - 1] + 2 * b[k] + 2 * b[k + 1] + b[k + 2] + d[k - 1] + 2 * d[k] +
+                        2 * d[k + 1] + d[k + 2] + e[k] + e[k + 1];
+          o[y][x] = te_clip255((v + 8) >> 4);
+        }
+    } else {  // separable 6-tap (fraction 0: the identity taps {0, 0, 64, 0, 0, 0}, exact), :160-178
+      const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
+      const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
+      uint32_t d[9][3];
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        const uint8_t *p = r + (i0 - 2 + q) * rs + j - 2;
+        d[q][0] = te_ld4(p);
+        d[q][1] = te_ld4(p + 4);
+        d[q][2] = te_ld4(p + 8);
+      }
+      int hk[9][4];
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        int c[12];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          c[b] = te_b(d[q][0], b);
+          c[b + 4] = te_b(d[q][1], b);
+          c[b + 8] = te_b(d[q][2], b);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          int a = 0;
+#pragma unroll
+          for (int m = 0; m < 6; m++) a += fh[m] * c[x + m];
+          hk[q][x] = a;
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < 4; y++)
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          int a = 0;
+#pragma unroll
+          for (int k = 0; k < 6; k++) a += fv[k] * hk[y + k][x];
+          o[y][x] = te_clip255((a + 2048) >> 12);
+        }
+    }
+#pragma unroll
+    for (int y = 0; y < 4; y++) s = te_sad4(B.o[t][y], te_pack4(o[y][0], o[y][1], o[y][2], o[y][3]), s);
+  }
+  return s;
+}
+// v summed over every segment of 2^l lanes: l <= 4 in every lane of the segment
+// (DPP inside 16-lane rows), l = 5, 6 per row (te_seg_get adds the rows)
+TE_FN uint32_t te_seg_sum(uint32_t v, int l) {
+  if (l >= 1) v += (uint32_t)TE_DPP(v, 0xB1);   // lane ^ 1
+  if (l >= 2) v += (uint32_t)TE_DPP(v, 0x4E);   // lane ^ 2
+  if (l >= 3) v += (uint32_t)TE_DPP(v, 0x141);  // row half mirror: the two quads of 8 lanes
+  if (l >= 4) v += (uint32_t)TE_DPP(v, 0x140);  // row mirror: the two halves of a row
+  return v;
+}
+TE_FN uint32_t te_seg_get(uint32_t v, int l, int sl) {
+  if (l <= 4) return (uint32_t)__builtin_amdgcn_readlane((int)v, sl << l);
+  if (l == 5) return (uint32_t)__builtin_amdgcn_readlane((int)v, 32 * sl) + (uint32_t)__builtin_amdgcn_readlane((int)v, 32 * sl + 16);
+  return te_sum(v);
+}
+// The costs of candidates 0 .. n-1 (cand(k): the candidate vector, a pure
+// function of k evaluated per lane; SUBPEL: through the MC filters) plus
+// mvcost(c), scanned in order: a cost strictly below min_sad becomes the best.
+// Returns the index of the last improvement, -1 if none.
+template <bool SUBPEL, class Cand, class MvCost>
+TE_FN int te_me_scan(const TeMeBlk &B, const uint8_t *ref, int rs, int sign, int bipred, int n, Cand cand,
+                     MvCost mvcost, uint32_t &min_sad, TeMv &mv_opt) {
+  const int s = sign ? -1 : 1;
+  auto lane_sad = [&](TeMv c) -> uint32_t {
+    if constexpr (SUBPEL) return te_me_mcsad_lane(B, ref, rs, c, sign, bipred);
+    else return te_me_sad_lane(B, ref + s * (c.x >> 2) + s * (c.y >> 2) * rs, rs);
+  };
+  int best = -1;
+  auto take = [&](int k, uint32_t sad) {
+    const TeMv c = cand(k);
+    const uint32_t cost = sad + mvcost(c);
+    if (cost < min_sad) {
+      min_sad = cost;
+      mv_opt = c;
+      best = k;
+    }
+  };
+  if (B.nu <= 64) {  // 64 / nu candidates per pass, one unit per lane
+    const int G = 64 >> B.lnu, slot = TE_LANE >> B.lnu;
+    for (int base = 0; base < n; base += G) {
+      const int k = base + slot;
+      uint32_t v = 0;
+      if (k < n) v = lane_sad(cand(k));
+      v = te_seg_sum(v, B.lnu);
+      for (int sl = 0; sl < G && base + sl < n; sl++) take(base + sl, te_seg_get(v, B.lnu, sl));
+    }
+  } else {  // whole-wave blocks: two candidates per pass (both in flight before either reduction)
+    for (int base = 0; base < n; base += 2) {
+      const bool two = base + 1 < n;
+      const uint32_t v0 = lane_sad(cand(base));
+      const uint32_t v1 = two ? lane_sad(cand(base + 1)) : 0u;
+      const uint32_t s0 = te_sum(v0), s1 = te_sum(v1);
+      take(base, s0);
+      if (two) take(base + 1, s1);
+    }
+  }
+  return best;
+}
+#endif
+
 // motion_estimate, enc/encode_block.c:830-1016 (params->sync = 0).  `org` /
 // `os`: the block (or partition) of the original; `ref`: the reference at the
 // block (partition) origin; size: the CU size (clip_mv, the size-16 rules).
@@ -629,8 +836,30 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
   mv_opt.x = mv_opt.y = 0;
   mv_ref.y = (int16_t)((((int)mvc.y + 2) >> 2) << 2);
   mv_ref.x = (int16_t)((((int)mvc.x + 2) >> 2) << 2);
+#if !defined(TE_HOST)
+  TeMeBlk B;
+  te_me_blk(B, org, os, width, height);
+  auto mvcost = [&](TeMv c) -> uint32_t { return te_lambda_bits(lam, te_mv_bits(c.y - mvp.y, c.x - mvp.x)); };
+  const int wide32 = size == 16 && F.speed < 2 && F.speed > 0;  // speed 1: the step-32 pass takes widesad
+#endif
   if ((size == 16 && enable_bipred) || F.speed == 0) {  // telescope search
     int step = 32;
+#if !defined(TE_HOST)
+    // the 5 x 5 grid of a step, row-major, the centre skipped after the first step
+    for (; step >= 4 && !(step == 32 && wide32); step >>= 1) {
+      const TeMv ref0 = mv_ref;
+      const int st = step, skipc = step < 32;
+      auto cand = [&](int idx) -> TeMv {
+        const int q = idx + (skipc && idx >= 12 ? 1 : 0);
+        TeMv c;
+        c.y = (int16_t)(ref0.y + (q / 5 - 2) * st);
+        c.x = (int16_t)(ref0.x + (q % 5 - 2) * st);
+        return te_clip_mv(c, ypos, xpos, F.W, F.H, size, sign);
+      };
+      te_me_scan<false>(B, ref, rs, sign, enable_bipred, 25 - skipc, cand, mvcost, min_sad, mv_opt);
+      mv_ref = mv_opt;
+    }
+#endif
     while (step >= 4) {
       const int range = 2 * step;
       for (int k = -range; k <= range; k += step)
@@ -658,6 +887,19 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
       step >>= 1;
     }
   }
+#if !defined(TE_HOST)
+  if (size != 16) {  // candidate search (the size-16 candidates take widesad: one at a time below)
+    const TeMv *cl = sb.mc.mv[r];
+    auto cand = [&](int idx) -> TeMv {
+      const TeMv cm = cl[idx];
+      TeMv c;
+      c.y = (int16_t)(cm.y << 2);
+      c.x = (int16_t)(cm.x << 2);
+      return te_clip_mv(c, ypos, xpos, F.W, F.H, size, sign);
+    };
+    te_me_scan<false>(B, ref, rs, sign, enable_bipred, sb.mc.num[r], cand, mvcost, min_sad, mv_opt);
+  } else
+#endif
   for (int idx = 0; idx < sb.mc.num[r]; idx++) {  // candidate search
     int x = 0;
     const TeMv cm = sb.mc.mv[r][idx];
@@ -679,6 +921,22 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
   for (int step = 1; step < maxsteps; step++) {  // full-pel hexagon search
     const int8_t *diy = te_hex_dy, *dix = te_hex_dx;
     int dir = start - 1, best_dir = -1;
+#if !defined(TE_HOST)
+    {  // directions start .. end (cyclic), in order
+      const int nd = (end - start + 6) % 6 + 1, st0 = start;
+      const TeMv ref0 = mv_ref;
+      auto cand = [&](int idx) -> TeMv {
+        const int d = (st0 + idx) % 6;
+        TeMv c;
+        c.y = (int16_t)(ref0.y + dix[d] * 4);
+        c.x = (int16_t)(ref0.x + diy[d] * 4);
+        return te_clip_mv(c, ypos, xpos, F.W, F.H, size, sign);
+      };
+      const int bk = te_me_scan<false>(B, ref, rs, sign, enable_bipred, nd, cand, mvcost, min_sad, mv_opt);
+      best_dir = bk < 0 ? -1 : (st0 + bk) % 6;
+    }
+    if (0)
+#endif
     do {
       dir++;
       dir = dir == 6 ? 0 : dir;
@@ -705,6 +963,42 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
   uint32_t cmin = min_sad;
   if (F.speed == 0) {  // exact half- and quarter-pel search through the MC filters
     const int8_t *hm = te_hp_m, *hn = te_hp_n;
+#if !defined(TE_HOST)
+    {
+      const TeMv ref0 = mv_ref;
+      auto hcand = [&](int idx) -> TeMv {
+        TeMv c;
+        c.y = (int16_t)(ref0.y + hm[idx + 1]);
+        c.x = (int16_t)(ref0.x + hn[idx + 1]);
+        return c;
+      };
+      TeMv dummy;
+      const int hb = te_me_scan<true>(B, ref, rs, sign, enable_bipred, 8, hcand, mvcost, cmin, dummy);
+      if (hb >= 0) {
+        ydelta_hp = hm[hb + 1];
+        xdelta_hp = hn[hb + 1];
+      }
+      mv_opt.x = (int16_t)(mv_opt.x + xdelta_hp);
+      mv_opt.y = (int16_t)(mv_opt.y + ydelta_hp);
+      const int8_t *qm = te_qp_m, *qn = te_qp_n;
+      const TeMv opt0 = mv_opt;
+      auto qcand = [&](int idx) -> TeMv {
+        TeMv c;
+        c.y = (int16_t)(opt0.y + qm[idx + 1]);
+        c.x = (int16_t)(opt0.x + qn[idx + 1]);
+        return c;
+      };
+      auto qcost = [&](TeMv c) -> uint32_t {
+        return (uint32_t)(int)(lam * (double)te_mv_bits(c.y - mvp.y, c.x - mvp.x) + 0.5);
+      };
+      const int qb = te_me_scan<true>(B, ref, rs, sign, enable_bipred, 8, qcand, qcost, cmin, dummy);
+      if (qb >= 0) {
+        ydelta_qp = qm[qb + 1];
+        xdelta_qp = qn[qb + 1];
+      }
+    }
+    if (0) {
+#endif
     for (int i = 1; i <= 8; i++) {
       c.y = (int16_t)(mv_ref.y + hm[i]);
       c.x = (int16_t)(mv_ref.x + hn[i]);
@@ -732,6 +1026,9 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
         xdelta_qp = qn[i];
       }
     }
+#if !defined(TE_HOST)
+    }
+#endif
   } else {  // fast bilinear approximation
     mv_ref.x = (int16_t)(mv_ref.x * s);
     mv_ref.y = (int16_t)(mv_ref.y * s);
@@ -1298,34 +1595,28 @@ TE_FN uint32_t te_mode_decision_intra(const TeFrame &F_, TeBlockInfo &bi_, TeBit
   tmp.coeff = tmp_coef;
   tmp.cs = bi.bp.cs;
   tmp.ts = bi.bp.ts;
-  const int max_tb = bi.max_num_tb_part - 1;
-  if (F.intra_rdo) {
-    uint32_t min_icost = TE_MAX_UINT32;
-    int best_mode = TE_DC;
-    for (int im = TE_DC; im < F.num_intra_modes; im++) {
-      tmp.intra_mode = im;
-      for (int tbp = 0; tbp <= max_tb; tbp++) {
-        tmp.tb_param = tbp;
-        tmp.mode = TE_INTRA;
-        const int nbits = te_encode_block_t<true>(F, b, bi, tmp);
-        cost = te_cost(F, bi, bi.rec, size, size, nbits);
-        if (cost < min_icost) {
-          min_icost = cost;
-          best_mode = im;
-        }
-      }
-    }
-    intra_mode = best_mode;
-  } else {
-    te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
-  }
-  tmp.intra_mode = intra_mode;
-  for (int tbp = 0; tbp <= max_tb; tbp++) {
-    tmp.tb_param = tbp;
+  // intra_rdo: every (mode, tb split) candidate for the mode (:2446-2462), then the
+  // chosen mode's tb splits against the block's best (:2463-2474) -- one loop,
+  // so the encode has a single call site
+  const int ntb = bi.max_num_tb_part, nrdo = F.intra_rdo ? F.num_intra_modes * ntb : 0;
+  uint32_t min_icost = TE_MAX_UINT32;
+  int best_mode = TE_DC;
+  if (!F.intra_rdo) te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
+  for (int st = 0; st < nrdo + ntb; st++) {
+    const bool rdo = st < nrdo;
+    if (st == nrdo && F.intra_rdo) intra_mode = best_mode;
+    const int im = rdo ? TE_DC + st / ntb : intra_mode;
+    tmp.intra_mode = im;
+    tmp.tb_param = rdo ? st - (st / ntb) * ntb : st - nrdo;
     tmp.mode = TE_INTRA;
-    const int nbits = te_encode_block_t<true>(F, b, bi, tmp);
+    const int nbits = TE_ENCODE_I(F, b, bi, tmp);
     cost = te_cost(F, bi, bi.rec, size, size, nbits);
-    if (cost < min_cost) {
+    if (rdo) {
+      if (cost < min_icost) {
+        min_icost = cost;
+        best_mode = im;
+      }
+    } else if (cost < min_cost) {
       min_cost = cost;
       te_copy_best(bi, tmp);
       te_keep_best_bits(b, bi, nbits);
@@ -1392,7 +1683,12 @@ TE_FN int te_es_chroma(const uint8_t *org, int os, int size, const uint8_t *pb, 
 }
 
 // check_early_skip_block, :2613-2741.  Returns 1 when every sub-block is insignificant.
-TE_NOINL int te_check_early_skip(const TeFrame &F_, const TeBlockInfo &bi_, const TeParam &p_) {
+#ifdef TE_ES_INLINE
+TE_FN
+#else
+TE_NOINL
+#endif
+int te_check_early_skip(const TeFrame &F_, const TeBlockInfo &bi_, const TeParam &p_) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_here();
   const TeBlockInfo &bi = *te_lds(&bi_);

@@ -22,9 +22,10 @@ CATS = ["wcoef", "wblock", "inter_comp", "intra_comp", "enc_block", "cost", "sea
 
 def build():
     src = os.path.join(ROOT, "thor_amd", "csrc", "libthor_amd.hip")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-ffp-contract=off", "-DTHOR_ENC_PROFILE", "-o", LIB, src], check=True,
-                   cwd=os.path.dirname(src))
+    sys.path.insert(0, ROOT)
+    from thor_amd.build import FLAGS, HIPCC  # the product's flags, plus the cycle accounting
+
+    subprocess.run([HIPCC] + FLAGS + ["-w", "-DTHOR_ENC_PROFILE", "-o", LIB, src], check=True, cwd=os.path.dirname(src))
 
 
 def main():
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--name", default="k4_low")
     ap.add_argument("--frames", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--limit", type=int, default=0, help="code only the first LIMIT coded frames of the plan")
     a = ap.parse_args()
     if a.build:
         build()
@@ -51,7 +53,7 @@ def main():
         e.upload_sequence(frames)
     buf = lib.thor_dev_alloc(2 * 8 * 64)
     lib.thor_enc_profile_buffer(buf)
-    for i in range(n):
+    for i in range(a.limit or n):
         zero = np.zeros(128, np.uint64)
         lib.thor_h2d(buf, zero.ctypes.data, zero.nbytes)
         import time
