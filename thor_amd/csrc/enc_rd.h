@@ -772,7 +772,8 @@ TE_FN uint32_t te_seg_sum(uint32_t v, int l) {
 TE_FN uint32_t te_seg_get(uint32_t v, int l, int sl) {
   if (l <= 4) return (uint32_t)__builtin_amdgcn_readlane((int)v, sl << l);
   if (l == 5) return (uint32_t)__builtin_amdgcn_readlane((int)v, 32 * sl) + (uint32_t)__builtin_amdgcn_readlane((int)v, 32 * sl + 16);
-  return te_sum(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 // The costs of candidates 0 .. n-1 (cand(k): the candidate vector, a pure
 // function of k evaluated per lane; SUBPEL: through the MC filters) plus
