@@ -353,7 +353,11 @@ int thor_enc_next_input(const thor_enc_t *e);
 void *thor_enc_stream(thor_enc_t *e);
 /* Re-create the context's stream restricted to the CUs whose bits are set in
  * mask[0..nwords) (bit c % 32 of word c / 32 = CU c; hipExtStreamCreateWithCUMask).
- * A scheduling knob: CUs left out stay free for concurrent decode launches. */
+ * A scheduling knob: CUs left out stay free for concurrent decode launches.
+ * The masked stream is a BLOCKING stream (it orders against the null stream).
+ * The old stream is destroyed: a handle thor_enc_stream returned before is
+ * invalid afterwards.  Must not overlap a thor_enc_frames call on the context
+ * (nothing here guards against it).  On THOR_ERR_HIP the old stream is kept. */
 int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords);
 /* Code the next frame of each of `n` DIFFERENT contexts (same device and
  * size, n <= 512) with one launch per stage.  Thread-safe: calls on the same

@@ -15,7 +15,7 @@
 
 // kernels (intra.hip, inter.hip, loopfilter.hip): the frame batch by value, first argument
 __global__ void k_frame_prep(const FrameBatch);
-__global__ void k_recon(const FrameBatch, int, int, unsigned long long *);
+__global__ void k_recon(const FrameBatch, const ReconGeo, unsigned long long *);
 __global__ void k_intra(const FrameBatch, unsigned long long *, int);
 __global__ void k_deblock_v(const FrameBatch, int, int);
 __global__ void k_deblock_h(const FrameBatch, int, int);
@@ -548,8 +548,18 @@ static int batch_phase_a(thor_dec *lead, const Batch &b) {
     // one flat grid: every frame's slow-list units first (frame-interleaved, as
     // many slots as the longest list), then each frame's units in XCD-major order
     // (inter.hip)
-    k_recon<<<dim3(n * (b.max_slow + 8 * ((unit_count(W, H) + 7) / 8)), 1), 64, recon_lds_pad(), st>>>(
-        b.fb, n, b.max_slow, lead->dbg_recon);
+    ReconGeo g;
+    g.nfr = n;
+    g.maxslow = b.max_slow;
+    g.nu = unit_count(W, H);
+    g.NU = 8 * ((g.nu + 7) / 8);
+    g.np = unit_pairs(W);
+    g.mnfr = recon_recip((unsigned)g.nfr);
+    g.mNU = recon_recip((unsigned)g.NU);
+    g.mnp = recon_recip((unsigned)g.np);
+    memcpy(g.tl, k_taps.luma, sizeof(g.tl));
+    memcpy(g.tc, k_taps.chroma, sizeof(g.tc));
+    k_recon<<<dim3(n * (b.max_slow + g.NU), 1), 64, recon_lds_pad(), st>>>(b.fb, g, lead->dbg_recon);
     HIPCHK(hipGetLastError());
   }
   return THOR_OK;

@@ -139,6 +139,28 @@ __host__ __device__ __forceinline__ int unit_count(int W, int H) { return unit_p
 // .w = gen} (plain stores of one value, no atomics), and a planned-order
 // workgroup whose unit holds such a half leaves it to the list.
 #define PLAN_SLOW 0x80000000u
+
+// k_recon's launch geometry, from the host: every index division of the flat
+// grid as one multiply-high by a host-computed reciprocal (a runtime scalar
+// division is ~35 SALU + a VALU reciprocal round trip per wave).
+struct ReconGeo {
+  int nfr, maxslow;   // frames in the batch; slow-list slots per frame
+  int nu, NU, np;     // units per frame, NU = nu rounded up to 8, SB pairs per slice row
+  unsigned mnfr, mNU, mnp;  // reciprocals (recon_recip) of nfr, NU, np
+  // MC filter words (common/inter_prediction.c:47-70, packed int8 as inter.hip's
+  // TapTables): luma [bipred table][fraction][taps 0-3, taps 4-5], chroma [fraction].
+  // Read by uniform index with one scalar load each (a select chain over
+  // compile-time constants became table-address arithmetic, ~40 SALU a word).
+  int tl[2][4][2];
+  int tc[8];
+};
+static_assert(sizeof(FrameBatch) % 8 == 0, "ReconGeo follows the batch in k_recon's kernarg segment");
+// k_recon's ReconGeo argument, read in place in the kernarg segment (dynamic
+// indices: scalar loads, no private copy)
+#define RECON_GEO() ((const ReconGeo *)((const char *)__builtin_amdgcn_kernarg_segment_ptr() + sizeof(FrameBatch)))
+// q = x / d for x < 2^32 / d: m = floor((2^32 - 1) / d) + 1 (d > 1; d = 1: m = 0, q = x)
+__host__ __device__ __forceinline__ unsigned recon_recip(unsigned d) { return d > 1 ? 0xffffffffu / d + 1u : 0u; }
+__device__ __forceinline__ int recon_div(unsigned x, unsigned m) { return m ? (int)__umulhi(x, m) : (int)x; }
 __host__ __device__ __forceinline__ size_t hplan_entries(int W, int H) { return (size_t)half_count(W, H); }
 
 // Per-4x4-cell side information for deblocking / CLPF, packed into 16 bits

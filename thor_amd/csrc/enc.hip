@@ -451,8 +451,12 @@ int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords) {
     (void)hipGetLastError();
     return THOR_ERR_HIP;
   }
-  EHIP(hipStreamSynchronize(e->stream));
-  EHIP(hipStreamDestroy(e->stream));
+  // the old stream drains and goes; on a failure the new one is destroyed and the old one kept
+  if (hipStreamSynchronize(e->stream) != hipSuccess || hipStreamDestroy(e->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipStreamDestroy(s);
+    return THOR_ERR_HIP;
+  }
   e->stream = s;
   return THOR_OK;
 }

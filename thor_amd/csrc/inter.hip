@@ -97,19 +97,8 @@ struct TapTables {
   }
 };
 __constant__ TapTables g_taps = TapTables();
-// The same words as scalar selects of compile-time constants (no table load on
-// the fast path: a load there is one more dependent round trip before the
-// window staging can start).
+// The host copy of the same words: capi.hip puts it into k_recon's ReconGeo.
 constexpr TapTables k_taps = TapTables();
-__device__ __forceinline__ int luma_word(int bipred, int f, int w) {
-  const int u = f == 1 ? k_taps.luma[0][1][w] : f == 2 ? k_taps.luma[0][2][w] : f == 3 ? k_taps.luma[0][3][w] : k_taps.luma[0][0][w];
-  const int b = f == 1 ? k_taps.luma[1][1][w] : f == 2 ? k_taps.luma[1][2][w] : f == 3 ? k_taps.luma[1][3][w] : k_taps.luma[1][0][w];
-  return bipred ? b : u;
-}
-__device__ __forceinline__ int chroma_word(int f) {
-  return f == 1 ? k_taps.chroma[1] : f == 2 ? k_taps.chroma[2] : f == 3 ? k_taps.chroma[3] : f == 4 ? k_taps.chroma[4]
-       : f == 5 ? k_taps.chroma[5] : f == 6 ? k_taps.chroma[6] : f == 7 ? k_taps.chroma[7] : k_taps.chroma[0];
-}
 
 // Rounding constant of the 2-D filters with the (p - 128) bias folded in:
 // 2048 + 128 * 64 * 64 (every tap set sums to 64).
@@ -780,6 +769,9 @@ __device__ __forceinline__ void chroma4_fast(const uint8_t *bu, const uint8_t *b
 // into the prediction registers (no per-segment key match).
 __device__ __forceinline__ void filter_all(const RefWin &w, const Key &K, int bipred, int x0, uint32_t ty[8],
                                            uint32_t tc[4], bool acc, bool k0 = true, bool k1 = true) {
+  const ReconGeo *G = RECON_GEO();
+  auto luma_word = [&](int b, int f, int wd) { return G->tl[b][f][wd]; };
+  auto chroma_word = [&](int f) { return G->tc[f]; };
   const int lane = threadIdx.x, cc = LCC(lane), gr = LGR(lane);
   const int lwb = 4 * cc + ((x0 - 2 + K.dx) & 15);
   const int cwb = 2 * cc + (((x0 >> 1) - 1 + K.cdx) & 15);
@@ -892,7 +884,7 @@ __device__ __forceinline__ void plan_pass(ReconLds &L, const FrameCtx &f, __amdg
 #ifndef RECON_WPE
 #define RECON_WPE 1
 #endif
-__global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, int nfr, int maxslow,
+__global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, const ReconGeo g,
                                                            unsigned long long *__restrict__ dbg) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   __shared__ ReconLds L;
@@ -904,13 +896,13 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
   // contiguous band of slice rows and vertical neighbours share their reference
   // rows in that XCD's L2.  Speed only, never correctness.
   const int W0 = F[0].W, H0 = F[0].H;
-  const int sbw = (W0 + 63) >> 6, np = unit_pairs(W0), nu = unit_count(W0, H0), NU = 8 * ((nu + 7) >> 3);
-  const int nslow = nfr * maxslow;
+  const int sbw = (W0 + 63) >> 6, np = g.np, nu = g.nu, NU = g.NU;
+  const int nslow = g.nfr * g.maxslow;
   int fi, u;
   bool listed = false;
   if ((int)blockIdx.x < nslow) {
-    fi = blockIdx.x % nfr;
-    const int idx = blockIdx.x / nfr;
+    const int idx = recon_div(blockIdx.x, g.mnfr);
+    fi = blockIdx.x - idx * g.nfr;
     const FrameCtx &f = F[fi];
     if (!f.slow || f.nblocks <= 0 || idx >= f.nslow) return;
     u = (int)f.slow[idx];
@@ -918,7 +910,7 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
     listed = true;
   } else {
     const int b = blockIdx.x - nslow;
-    fi = b / NU;
+    fi = recon_div(b, g.mNU);
     const int loc = b - fi * NU, per = NU >> 3;
     u = (loc & 7) * per + (loc >> 3);
     if (u >= nu) return;
@@ -951,7 +943,7 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, i
     const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
     stamp[7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
   }
-  const int srow = u / np, pr = u - srow * np;  // slice row (4 per SB row), SB pair
+  const int srow = recon_div(u, g.mnp), pr = u - srow * np;  // slice row (4 per SB row), SB pair
   const int sby = srow >> 2, qtr = srow & 3, h = qtr >> 1;
   if (sby < f.band0 || sby >= f.band1) return;  // another shard's rows (row-band sharding)
   const int cs = f.W >> 2;
