@@ -19,6 +19,13 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 FLAGS += ["-Xclang", "-target-feature", "-Xclang", "-dot6-insts", "-Xclang", "-target-feature", "-Xclang", "-dot4-insts"]
 # k_recon: 5 waves per SIMD (96 VGPRs; a few spills on the per-cell path only)
 FLAGS += ["-DRECON_WPE=5"]
+# No interprocedural register allocation: with it (the AMDGPU default) a caller of
+# the encoder's non-inlined RD functions allocates against each callee's actual
+# clobber set, and a register-hungry callee (the candidate-parallel motion search)
+# turned the callers' values into spill / reload traffic around every call (the
+# 4K I frame, which never runs that callee, +8 %).  Without it every function
+# keeps the calling convention's contract: 240 x 4K I frame 1 270 -> 1 173 ms.
+FLAGS += ["-mllvm", "-enable-ipra=false"]
 
 
 def _stale() -> bool:

@@ -837,7 +837,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
   mv_opt.x = mv_opt.y = 0;
   mv_ref.y = (int16_t)((((int)mvc.y + 2) >> 2) << 2);
   mv_ref.x = (int16_t)((((int)mvc.x + 2) >> 2) << 2);
-#if !defined(TE_HOST)
+#if !defined(TE_HOST) && !defined(TE_ME_SEQ)
   TeMeBlk B;
   te_me_blk(B, org, os, width, height);
   auto mvcost = [&](TeMv c) -> uint32_t { return te_lambda_bits(lam, te_mv_bits(c.y - mvp.y, c.x - mvp.x)); };
@@ -845,7 +845,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
 #endif
   if ((size == 16 && enable_bipred) || F.speed == 0) {  // telescope search
     int step = 32;
-#if !defined(TE_HOST)
+#if !defined(TE_HOST) && !defined(TE_ME_SEQ)
     // the 5 x 5 grid of a step, row-major, the centre skipped after the first step
     for (; step >= 4 && !(step == 32 && wide32); step >>= 1) {
       const TeMv ref0 = mv_ref;
@@ -888,7 +888,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
       step >>= 1;
     }
   }
-#if !defined(TE_HOST)
+#if !defined(TE_HOST) && !defined(TE_ME_SEQ)
   if (size != 16) {  // candidate search (the size-16 candidates take widesad: one at a time below)
     const TeMv *cl = sb.mc.mv[r];
     auto cand = [&](int idx) -> TeMv {
@@ -922,7 +922,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
   for (int step = 1; step < maxsteps; step++) {  // full-pel hexagon search
     const int8_t *diy = te_hex_dy, *dix = te_hex_dx;
     int dir = start - 1, best_dir = -1;
-#if !defined(TE_HOST)
+#if !defined(TE_HOST) && !defined(TE_ME_SEQ)
     {  // directions start .. end (cyclic), in order
       const int nd = (end - start + 6) % 6 + 1, st0 = start;
       const TeMv ref0 = mv_ref;
@@ -964,7 +964,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
   uint32_t cmin = min_sad;
   if (F.speed == 0) {  // exact half- and quarter-pel search through the MC filters
     const int8_t *hm = te_hp_m, *hn = te_hp_n;
-#if !defined(TE_HOST)
+#if !defined(TE_HOST) && !defined(TE_ME_SEQ)
     {
       const TeMv ref0 = mv_ref;
       auto hcand = [&](int idx) -> TeMv {
@@ -1027,7 +1027,7 @@ TE_NOINL uint32_t te_motion_estimate(const TeFrame &F_, TeSB &sb_, int r, const 
         xdelta_qp = qn[i];
       }
     }
-#if !defined(TE_HOST)
+#if !defined(TE_HOST) && !defined(TE_ME_SEQ)
     }
 #endif
   } else {  // fast bilinear approximation
@@ -1602,6 +1602,39 @@ TE_FN uint32_t te_mode_decision_intra(const TeFrame &F_, TeBlockInfo &bi_, TeBit
   const int ntb = bi.max_num_tb_part, nrdo = F.intra_rdo ? F.num_intra_modes * ntb : 0;
   uint32_t min_icost = TE_MAX_UINT32;
   int best_mode = TE_DC;
+#ifdef TE_MDI_TWO
+  if (F.intra_rdo) {
+    for (int im = TE_DC; im < F.num_intra_modes; im++) {
+      tmp.intra_mode = im;
+      for (int tbp = 0; tbp < ntb; tbp++) {
+        tmp.tb_param = tbp;
+        tmp.mode = TE_INTRA;
+        const int nbits = TE_ENCODE_I(F, b, bi, tmp);
+        cost = te_cost(F, bi, bi.rec, size, size, nbits);
+        if (cost < min_icost) {
+          min_icost = cost;
+          best_mode = im;
+        }
+      }
+    }
+    intra_mode = best_mode;
+  } else {
+    te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
+  }
+  tmp.intra_mode = intra_mode;
+  for (int tbp = 0; tbp < ntb; tbp++) {
+    tmp.tb_param = tbp;
+    tmp.mode = TE_INTRA;
+    const int nbits = TE_ENCODE_I(F, b, bi, tmp);
+    cost = te_cost(F, bi, bi.rec, size, size, nbits);
+    if (cost < min_cost) {
+      min_cost = cost;
+      te_copy_best(bi, tmp);
+      te_keep_best_bits(b, bi, nbits);
+    }
+  }
+  (void)nrdo;
+#else
   if (!F.intra_rdo) te_search_intra(F, bi, F.num_intra_modes, &intra_mode);
   for (int st = 0; st < nrdo + ntb; st++) {
     const bool rdo = st < nrdo;
@@ -1623,6 +1656,7 @@ TE_FN uint32_t te_mode_decision_intra(const TeFrame &F_, TeBlockInfo &bi_, TeBit
       te_keep_best_bits(b, bi, nbits);
     }
   }
+#endif
   te_rewind(b, pos_ref);  // rewind (:2476)
   TE_TR(F.frame_num, 5, bi.ypos, bi.xpos, size, min_cost, bi.bp.mode, TE_MAX_UINT32);
   return min_cost;
