@@ -217,6 +217,73 @@ def config3_leg(torch, lib, streams: int = 128, nf: int = 2):
             "x_16_reference_cores": round(mpx / (16 * ref1), 2)}
 
 
+CFG5_CODED = (0, 16)  # the first two coded frames of the 17-frame HDB16 plan: the I frame and P frame 16
+
+
+def config5_frames():
+    """Display frames 0 and 16 of the seeded 4K clip tests/golden/k4_hdbi_high was encoded from (the only
+    input the I frame and P frame 16 read); synthesised in worker processes before the GPU is touched."""
+    from thor_amd import synth
+
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "streams.json")))["k4_hdbi_high"]
+    import multiprocessing as mp
+
+    pool = mp.get_context("fork").Pool(2)
+    try:
+        fr = pool.map(synth._i420, [(meta["width"], meta["height"], t, meta["seed"]) for t in CFG5_CODED])
+    finally:
+        pool.close()
+        pool.join()
+    return meta, fr
+
+
+def config5_leg(torch, lib, cfg5, streams: int = 64):
+    """BASELINE config 5 -- 4K config_HDB16_high_efficiency (hierarchical B, 16-frame sub-GOP, encoder_speed
+    0, temporal-interpolated references, 4 references, tb / pb split, delta-QP RD) -- as a throughput leg
+    beside `value`: `streams` independent contexts coding the first two coded frames of the 17-frame plan
+    (the I frame, then P frame 16: the telescope + exact sub-pel motion search at its longest distance),
+    one thor_enc_frames launch set per frame for all of them.  Every stream's bytes must equal the
+    reference Thorenc's tests/golden/k4_hdbi_high.bit (its first two frame chunks).  The P-16 batch is
+    latency bound (the superblock wavefront's critical path), so its time is also the single-stream time
+    of that frame."""
+    from thor_amd.encoder import GpuEncoder, encode_batch, params_for
+
+    meta, fr = cfg5
+    w, h, n = meta["width"], meta["height"], meta["frames"]
+    fsize = w * h * 3 // 2
+    want = open(os.path.join(ROOT, "tests", "golden", "k4_hdbi_high.bit"), "rb").read()
+    seq = torch.zeros((n, fsize), dtype=torch.uint8, device="cuda")  # display order; only frames 0, 16 are read
+    for t, x in zip(CFG5_CODED, fr):
+        seq[t].copy_(torch.from_numpy(x))
+    encs = [GpuEncoder(params_for(meta["config"], w, h, n, meta["extra"])) for _ in range(streams)]
+    try:
+        for e in encs:
+            e.use_device_sequence(seq.data_ptr(), n)
+        torch.cuda.synchronize()
+        out = [b""] * streams
+        frame_s = []
+        for _ in CFG5_CODED:
+            t0 = time.perf_counter()
+            ch = encode_batch(encs)
+            frame_s.append(time.perf_counter() - t0)
+            for k in range(streams):
+                out[k] += ch[k]
+        ok = all(want.startswith(o) and len(o) > 0 for o in out) and len(set(out)) == 1
+    finally:
+        for e in encs:
+            e.close()
+    t = sum(frame_s)
+    mpx = streams * w * h * len(CFG5_CODED) / t / 1e6
+    ref1 = 0.099  # BASELINE.md: config_HDB16_high_efficiency 1080p x 17, SIMD build, one core
+    return {"workload": "%d streams x the first 2 coded frames (I, P 16) of 4K config_HDB16_high_efficiency "
+                        "(encoder_speed 0, interpolated references), encode only, thor_enc_frames batches" % streams,
+            "mpx_s": round(mpx, 3), "seconds": round(t, 3), "frame_s": [round(x, 3) for x in frame_s],
+            "bit_exact": ok, "reference_single_core_mpx_s": ref1,
+            "reference_note": "the reference's figure is 1080p x 17 frames (all its frame types) on one core; "
+                              "per 4K frame that is 4 x 8.3 / 0.099 ~ 84 s",
+            "x_16_reference_cores": round(mpx / (16 * ref1), 2)}
+
+
 def pyramid_leg(torch, lib, reps: int = 50):
     """Temporal-interpolation luma pyramid (thor_scale_pyramid2, the chains of
     scale_frame_down2x2_simd calls of common/temporal_interp.c:1011-1019) on
@@ -531,6 +598,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config3-streams", type=int, default=128,
                     help="streams of the BASELINE config-3 encoder leg (1080p LDB high efficiency)")
+    ap.add_argument("--config5-streams", type=int, default=64,
+                    help="streams of the BASELINE config-5 encoder leg (4K HDB16 high efficiency, I + P 16); 0: off")
     ap.add_argument("--drop-in", nargs="?", const="hd_low", default=None, metavar="STREAM",
                     help="time the reference decoder's host C on this library's per-call surface "
                          "(oracle/_ref/thordec_amd) beside the reference Thordec on a golden .bit (default hd_low)")
@@ -578,6 +647,9 @@ def main():
     nclip = len(clips_meta)
 
     clips = None
+    cfg5 = None
+    if a.shard == "streams" and world == 1 and not a.no_legs and a.config5_streams > 0:
+        cfg5 = config5_frames()  # before anything touches the GPU (worker processes fork)
     if a.shard == "streams":  # synthesise the inputs before anything touches the GPU (worker processes fork)
         from thor_amd import synth
 
@@ -945,6 +1017,8 @@ def main():
             out["temporal_interp_comp"] = interp_leg(torch, lib)
             out["temporal_interp_frame"] = interp_frames_leg(torch, lib, clips[0])
             out["config3_encoder"] = config3_leg(torch, lib, a.config3_streams)
+            if cfg5 is not None:
+                out["config5_encoder"] = config5_leg(torch, lib, cfg5, a.config5_streams)
         if not a.no_cpu_baseline and world == 1:
             cb = cpu_baseline(bc, clips_meta, clips)
             if cb is not None:
