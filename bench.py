@@ -61,6 +61,13 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
 import numpy as np  # noqa: E402
 
 METRIC = "Mpixels/s encode+decode, 4K LDB_low_complexity; bit-exact vs ref"
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One progress line on stderr (stdout carries only the JSON line)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench %7.1f s] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 STAGES = ["prep", "inter", "intra", "deblock", "clpf", "pad"]
 HOST_THREADS = 16  # the GPU box's CPU share per GPU
@@ -266,6 +273,7 @@ def config5_leg(torch, lib, cfg5, streams: int = 64):
             t0 = time.perf_counter()
             ch = encode_batch(encs)
             frame_s.append(time.perf_counter() - t0)
+            progress("config-5 frame batch: %.1f s" % frame_s[-1])
             for k in range(streams):
                 out[k] += ch[k]
         ok = all(want.startswith(o) and len(o) > 0 for o in out) and len(set(out)) == 1
@@ -650,6 +658,7 @@ def main():
     cfg5 = None
     if a.shard == "streams" and world == 1 and not a.no_legs and a.config5_streams > 0:
         cfg5 = config5_frames()  # before anything touches the GPU (worker processes fork)
+        progress("config-5 input synthesised")
     if a.shard == "streams":  # synthesise the inputs before anything touches the GPU (worker processes fork)
         from thor_amd import synth
 
@@ -658,6 +667,7 @@ def main():
             c = synth.synth_frames(W, H, nf, cm["seed"], workers=8)
             assert hashlib.md5(c.tobytes()).hexdigest() == cm["synth_md5"], "synthetic clip %d drifted" % cm["seed"]
             clips.append(c)
+            progress("clip %d synthesised" % cm["seed"])
 
     import torch
 
@@ -866,8 +876,10 @@ def main():
         return ok
 
     allk = list(range(K))
+    progress("%d encoder + decoder contexts ready" % K)
     for _ in range(max(1, a.warmup)):
         _, bits, devs = step_pipe(allk)
+        progress("warmup step done")
     bit_exact = bits_ok(allk, bits) and decoded_ok(allk)
     rf_early = None
     if os.environ.get("THOR_BENCH_RF_EARLY"):  # diagnostic: the roofline pass before the timed steps too
@@ -881,6 +893,7 @@ def main():
     for _ in range(a.steps):
         te, bits, devs = step_pipe(allk)
         elapsed += te
+        progress("timed step: %.1f ms" % (te * 1e3))
         bit_exact &= bits_ok(allk, bits)
         bit_exact &= decoded_ok(allk)  # every timed step's decode checked too (outside the timed region)
     torch.cuda.synchronize(local)
@@ -889,6 +902,7 @@ def main():
     # the two legs one after the other (one untimed-for-value step): the split of the work
     dec_host_s[0] = 0.0
     t_enc, t_dec, bits, devs, fms = step(allk)
+    progress("serial step done")
     bit_exact &= bits_ok(allk, bits)
     enc_frame_ms = fms
     dec_host_ms = dec_host_s[0] * 1e3
@@ -915,6 +929,7 @@ def main():
         decs[k].sync()
     t_do = (time.perf_counter() - t0) / dsteps
     frames_of = [parse_stream(bits[k])[1] for k in groups[0]]
+    progress("roofline pass")
     stage_ms, recon_ms, alg, B, prep_ms = roofline_pass(lib, decs, [groups[0]], devs, frames_of, seq, 3)
     achieved = alg / (recon_ms / 1e3) / 1e9 if recon_ms > 0 else 0.0
     path_ms = prep_ms + recon_ms
@@ -1012,14 +1027,18 @@ def main():
             },
         }
         if world == 1 and not a.no_legs:
+            progress("legs")
             out["encoder_tu_chain"] = encoder_leg(torch, lib)
             out["temporal_pyramid"] = pyramid_leg(torch, lib)
             out["temporal_interp_comp"] = interp_leg(torch, lib)
             out["temporal_interp_frame"] = interp_frames_leg(torch, lib, clips[0])
+            progress("config-3 leg")
             out["config3_encoder"] = config3_leg(torch, lib, a.config3_streams)
+            progress("config-5 leg")
             if cfg5 is not None:
                 out["config5_encoder"] = config5_leg(torch, lib, cfg5, a.config5_streams)
         if not a.no_cpu_baseline and world == 1:
+            progress("CPU baseline")
             cb = cpu_baseline(bc, clips_meta, clips)
             if cb is not None:
                 out["cpu_baseline"] = cb
