@@ -39,16 +39,13 @@ def pmc(db, counter):
 
 
 def per_dispatch(db, counter, kernel):
-    """Values of `counter` for the widest-grid dispatches of `kernel` (the
-    batched launches), in dispatch order."""
+    """Values of `counter` for every dispatch of `kernel`, in dispatch order
+    (the PMC driver launches one per frame; k_recon's grid now varies with the
+    frame's slow list, so the grid size no longer identifies them)."""
     c = sqlite3.connect(db)
-    rows = [(float(v), int(g)) for n, v, g in c.execute(
-        "select kernel_name, value, grid_size from counters_collection where counter_name=? order by dispatch_id",
+    return [float(v) for n, v in c.execute(
+        "select kernel_name, value from counters_collection where counter_name=? order by dispatch_id",
         (counter,)) if short(n) == kernel]
-    if not rows:
-        return []
-    gmax = max(g for _, g in rows)
-    return [v for v, g in rows if g == gmax]
 
 
 def main():
