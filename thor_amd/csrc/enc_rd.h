@@ -1695,6 +1695,194 @@ TE_FN int te_es_luma(const uint8_t *org, int os, int size, const uint8_t *pb, in
   for (int e = TE_LANE; e < n * n; e += TE_NL) flag |= te_abs(X.C[e]) > thr;
   return te_any(flag);
 }
+#if !defined(TE_HOST)
+// The early-skip checks fused with their uni-pred prediction (device): the
+// prediction is never stored.  Each lane computes 4x4 MC outputs (te_mc_luma's
+// / te_mc_chroma's unit form, common/inter_prediction.c:72-180) with the
+// original's rows loaded in the same round trip, and reduces them straight to
+// what the check reads -- the 2x2-averaged residual (luma) or the column sums
+// (chroma) -- so one memory round trip and no prediction-buffer LDS round trip
+// per check.
+TE_FN void te_mc_luma_unit(const uint8_t *r, int rs, int i0, int j, int fx, int fy, int bipred, int o[4][4]) {
+  if (fx == 2 && fy == 2) {  // rows -1..5, columns -1..6, :145-157
+    uint32_t lo[7], hi[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
+      const uint8_t *p = r + (i0 - 1 + q) * rs + j - 1;
+      lo[q] = te_ld4(p);
+      hi[q] = te_ld4(p + 4);
+    }
+    int c[7][8];
+#pragma unroll
+    for (int q = 0; q < 7; q++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        c[q][k] = te_b(lo[q], k);
+        c[q][k + 4] = te_b(hi[q], k);
+      }
+#pragma unroll
+    for (int y = 0; y < 4; y++)
+#pragma unroll
+      for (int x = 0; x < 4; x++) {
+        const int k = x + 1;
+        const int *a = c[y], *b = c[y + 1], *d = c[y + 2], *e = c[y + 3];
+        const int v = a[k] + a[k + 1] + b[k - 1] + 2 * b[k] + 2 * b[k + 1] + b[k + 2] + d[k - 1] + 2 * d[k] +
+                      2 * d[k + 1] + d[k + 2] + e[k] + e[k + 1];
+        o[y][x] = te_clip255((v + 8) >> 4);
+      }
+    return;
+  }
+  if (!fx && !fy) {  // integer vector: a copy
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+      const uint32_t v = te_ld4(r + (i0 + y) * rs + j);
+#pragma unroll
+      for (int x = 0; x < 4; x++) o[y][x] = te_b(v, x);
+    }
+    return;
+  }
+  // separable 6-tap (fraction 0: the identity taps {0, 0, 64, 0, 0, 0}, exact), :160-178
+  const int8_t *fv = (bipred ? te_luma_bi : te_luma_uni)[fy];
+  const int8_t *fh = (bipred ? te_luma_bi : te_luma_uni)[fx];
+  uint32_t d[9][3];
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const uint8_t *p = r + (i0 - 2 + q) * rs + j - 2;
+    d[q][0] = te_ld4(p);
+    d[q][1] = te_ld4(p + 4);
+    d[q][2] = te_ld4(p + 8);
+  }
+  int hk[9][4];
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    int c[12];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      c[b] = te_b(d[q][0], b);
+      c[b + 4] = te_b(d[q][1], b);
+      c[b + 8] = te_b(d[q][2], b);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      int a = 0;
+#pragma unroll
+      for (int m = 0; m < 6; m++) a += fh[m] * c[x + m];
+      hk[q][x] = a;
+    }
+  }
+#pragma unroll
+  for (int y = 0; y < 4; y++)
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      int a = 0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) a += fv[k] * hk[y + k][x];
+      o[y][x] = te_clip255((a + 2048) >> 12);
+    }
+}
+// te_mc_chroma's 4x4 unit (fraction 0 included: the identity taps {0, 64, 0, 0} are exact)
+TE_FN void te_mc_chroma_unit(const uint8_t *r, int rs, int i0, int j, int fx, int fy, int o[4][4]) {
+  const int8_t *fh = te_chroma_f[fx], *fv = te_chroma_f[fy];
+  uint32_t lo[7], hi[7];
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const uint8_t *p = r + (i0 - 1 + q) * rs + j - 1;
+    lo[q] = te_ld4(p);
+    hi[q] = te_ld4(p + 4);
+  }
+  int hk[7][4];
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    int c[8];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      c[b] = te_b(lo[q], b);
+      c[b + 4] = te_b(hi[q], b);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      int a = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) a += fh[k] * c[x + k];
+      hk[q][x] = a;
+    }
+  }
+#pragma unroll
+  for (int y = 0; y < 4; y++)
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      int a = 0;
+#pragma unroll
+      for (int m = 0; m < 4; m++) a += fv[m] * hk[y + m][x];
+      o[y][x] = te_clip255((a + 2048) >> 12);
+    }
+}
+// te_mc_luma (sub-block origin `ref`, vector mv / sign) + te_es_luma, size 8..32
+TE_FN int te_es_luma_mc(const uint8_t *ref, int rs, TeMv mv, int sign, int bipred, const uint8_t *org, int os,
+                        int size, int thr) {
+  const TeScratch S = te_here();
+  TeTx &X = *S.tx;
+  const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
+  const int fy = my & 3, fx = mx & 3;
+  const uint8_t *r = ref + (my >> 2) * rs + (mx >> 2);
+  const int w4 = size >> 2, s2 = size >> 1;
+  if (TE_LANE < w4 * w4) {
+    const int u = TE_LANE, i0 = te_dv(u, w4) * 4, j = (u - te_dv(u, w4) * w4) * 4;
+    uint32_t ov[4];
+#pragma unroll
+    for (int y = 0; y < 4; y++) ov[y] = te_ld4(org + (i0 + y) * os + j);
+    int o[4][4];
+    te_mc_luma_unit(r, rs, i0, j, fx, fy, bipred, o);
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+        const int y = 2 * a, x = 2 * b;
+        const int s = te_b(ov[y], x) - o[y][x] + te_b(ov[y], x + 1) - o[y][x + 1] + te_b(ov[y + 1], x) - o[y + 1][x] +
+                      te_b(ov[y + 1], x + 1) - o[y + 1][x + 1];
+        X.R[(i0 / 2 + a) * s2 + j / 2 + b] = (int16_t)((s + 2) >> 2);
+      }
+  }
+  te_sync();
+  te_fwd_tx(X, s2, 0);
+  int flag = 0;
+  for (int e = TE_LANE; e < s2 * s2; e += TE_NL) flag |= te_abs(X.C[e]) > thr;
+  return te_any(flag);
+}
+// te_mc_chroma + te_es_chroma (size 4, 8 or 16; only the pixels the check reads)
+TE_FN int te_es_chroma_mc(const uint8_t *ref, int rs, TeMv mv, int sign, const uint8_t *org, int os, int size,
+                          int thr) {
+  const int mx = sign ? -mv.x : mv.x, my = sign ? -mv.y : mv.y;
+  const int fy = my & 7, fx = mx & 7;
+  const uint8_t *r = ref + (my >> 3) * rs + (mx >> 3);
+  int flag = 0;
+  const int nu = size == 8 ? 4 : 1;  // 8x8: every column over 8 rows; else the top-left 4x4, column pairs
+  int cs[4] = {0, 0, 0, 0};          // the lane's unit: column sums of org - pred over its 4 rows
+  if (TE_LANE < nu) {
+    const int i0 = (TE_LANE >> 1) * 4, j = (TE_LANE & 1) * 4;
+    uint32_t ov[4];
+#pragma unroll
+    for (int y = 0; y < 4; y++) ov[y] = te_ld4(org + (i0 + y) * os + j);
+    int o[4][4];
+    te_mc_chroma_unit(r, rs, i0, j, fx, fy, o);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+      for (int y = 0; y < 4; y++) cs[x] += te_b(ov[y], x) - o[y][x];
+  }
+  if (size == 8) {  // the bottom units' sums join the top ones' (lane ^ 2 within a quad)
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      const int tot = cs[x] + TE_DPP(cs[x], 0x4E);
+      if (TE_LANE < 2) flag |= te_wrap16(tot) > (int)(int16_t)thr;
+    }
+  } else if (TE_LANE == 0) {
+    flag = (cs[0] + cs[1] > thr) | (cs[2] + cs[3] > thr);
+  }
+  return te_any(flag);
+}
+#endif
+
 // check_early_skip_sub_blockC (:2540-2611): column sums of the residual
 // (8x8: all 8 columns over 8 rows; other sizes: the top-left 4x4 only, column
 // pairs) against the threshold
@@ -1762,6 +1950,12 @@ int te_check_early_skip(const TeFrame &F_, const TeBlockInfo &bi_, const TeParam
         const int sign = F.ref_fnum[p.ref_idx0] > F.frame_num;
         // the vector is clipped in place for every sub-block (:2722), and the clipped one serves chroma
         TeMv mv = te_clip_mv(p.mv0[0], ypos, xpos, F.W, F.H, size0, sign);
+#if !defined(TE_HOST)
+        if (te_es_luma_mc(F.refy[p.ref_idx0] + ry, F.rsy, mv, sign, bip, oY, F.osy, size0, thr_y)) return 0;
+        if (te_es_chroma_mc(F.refu[p.ref_idx0] + rc, F.rsc, mv, sign, oU, F.osc, s0c, thr_c)) return 0;
+        if (te_es_chroma_mc(F.refv[p.ref_idx0] + rc, F.rsc, mv, sign, oV, F.osc, s0c, thr_c)) return 0;
+        continue;
+#endif
         te_mc_luma(pb, size0, F.refy[p.ref_idx0] + ry, F.rsy, size0, size0, mv, sign, bip);
         if (te_es_luma(oY, F.osy, size0, pb, thr_y)) return 0;
         te_mc_chroma(pb, s0c, F.refu[p.ref_idx0] + rc, F.rsc, s0c, s0c, mv, sign);

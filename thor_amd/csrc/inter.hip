@@ -895,7 +895,7 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
   // workgroup b runs on XCD b % 8 (round-robin dispatch), so each XCD gets a
   // contiguous band of slice rows and vertical neighbours share their reference
   // rows in that XCD's L2.  Speed only, never correctness.
-  const int W0 = F[0].W, H0 = F[0].H;
+  const int W0 = F[0].W;
   const int sbw = (W0 + 63) >> 6, np = g.np, nu = g.nu, NU = g.NU;
   const int nslow = g.nfr * g.maxslow;
   int fi, u;
