@@ -683,7 +683,7 @@ def main():
     from thor_amd import lib as L
     from thor_amd.bitstream import Parser, parse_stream
     from thor_amd.decoder import GpuDecoder, decode_batch
-    from thor_amd.encoder import GpuEncoder, encode_batch, params_for
+    from thor_amd.encoder import GpuEncoder, encode_batch, encode_batch_begin, encode_batch_end, params_for
 
     lib = L.load()
     dev = torch.device("cuda", local)
@@ -816,15 +816,26 @@ def main():
         th = threading.Thread(target=consumer)
         th.start()
         sent = 0
+        E = [encs[k] for k in ks]
+
+        def collect(i):  # frame i's chunks: to the .bit files and the decode consumer
+            chunks = encode_batch_end(E)
+            for j, ch in enumerate(chunks):
+                bits[j].append(ch)
+            q.put([ch[4:] for ch in chunks])  # payload after the 4-byte chunk length (dec/getbits.c:48-69)
+            pipe_tl["enc_done_ms"][i] = round((time.perf_counter() - t0) * 1e3, 1)
+
         try:
+            # frame i + 1 is enqueued before frame i is collected: the GPU codes the next frame while the
+            # host reads the last one back (thor_enc_frames_begin / _end)
             for i in range(nf):
                 enc_wait(ks, evs[i])
-                chunks = encode_batch([encs[k] for k in ks])
-                for j, ch in enumerate(chunks):
-                    bits[j].append(ch)
-                q.put([ch[4:] for ch in chunks])  # payload after the 4-byte chunk length (dec/getbits.c:48-69)
-                sent += 1
-                pipe_tl["enc_done_ms"][i] = round((time.perf_counter() - t0) * 1e3, 1)
+                encode_batch_begin(E)
+                if i > 0:
+                    collect(i - 1)
+                    sent += 1
+            collect(nf - 1)
+            sent += 1
         finally:
             if sent < nf:
                 q.put(None)

@@ -368,6 +368,18 @@ int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords);
  * context's input frame thor_enc_next_input(es[i]), planar I420, luma stride
  * orig_stride[i] (NULL: width), chroma stride half of it.  Synchronous. */
 int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
+/* thor_enc_frames in two halves, so the device codes the next frame while the
+ * host collects the last one: _begin enqueues every stage of the batch and
+ * advances the contexts (the next frame may be begun at once: up to two
+ * batches in flight per device, a context's frames on one stream); _end waits
+ * for the OLDEST batch begun (the same es / n), reads its coded words back and
+ * makes them the contexts' chunks (thor_enc_frame_bytes).  On a device error
+ * _end drops every batch in flight and returns the failed batch's contexts to
+ * their state before it (that frame can be coded again; contexts only in a
+ * later dropped batch must be reset).  thor_enc_reset / _destroy refuse /
+ * drop a context with a batch in flight. */
+int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
+int thor_enc_frames_end(thor_enc_t *const *es, int n);
 int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride);
 /* The last coded frame's .bit chunk (4-byte big-endian length + payload,
  * enc/putbits.c:57-95; the first chunk carries the sequence header):

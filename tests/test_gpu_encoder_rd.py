@@ -161,6 +161,42 @@ def _encode_and_compare(name, nframes, streams, limit=None):
         enc.close()
 
 
+def test_pipelined_batches_match_reference(streams):
+    """thor_enc_frames_begin / _end: frame i + 1 of every context begun before
+    frame i is ended (two batches in flight) -- the same bytes as the reference
+    encoder; a third begin without an end is refused."""
+    import ctypes as C
+
+    from thor_amd import lib as L
+    from thor_amd.encoder import GpuEncoder, encode_batch_begin, encode_batch_end, params_for
+
+    meta = streams["cif_med"]
+    want = _frames(open("tests/golden/cif_med.bit", "rb").read())
+    encs = []
+    try:
+        for _ in range(3):
+            e = GpuEncoder(params_for(meta["config"], meta["width"], meta["height"], 10, meta["extra"]))
+            e.upload_sequence(_input(meta, 10))
+            encs.append(e)
+        got = [[] for _ in encs]
+        encode_batch_begin(encs)
+        for i in range(10):
+            if i + 1 < 10:
+                encode_batch_begin(encs)
+                if i == 0:  # two in flight: a third is refused
+                    n = len(encs)
+                    hs = (C.c_void_p * n)(*[e.h for e in encs])
+                    ptrs = (C.c_void_p * n)(*[e.next_input_ptr() for e in encs])
+                    assert encs[0].lib.thor_enc_frames_begin(hs, n, ptrs, None) == L.THOR_ERR_ARG
+            for k, ch in enumerate(encode_batch_end(encs)):
+                got[k].append(ch)
+        for k in range(len(encs)):
+            assert got[k] == want[:10], k
+    finally:
+        for e in encs:
+            e.close()
+
+
 def test_encoder_reset_recodes_the_sequence(streams):
     """thor_enc_reset: the context codes its sequence again, same .bit."""
     from thor_amd.encoder import GpuEncoder, params_for

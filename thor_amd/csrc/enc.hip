@@ -22,6 +22,7 @@
 #include "enc_gop.h"
 #include "enc_rd.h"
 
+#include <deque>
 #include <map>
 #include <mutex>
 
@@ -267,6 +268,8 @@ struct thor_enc {
   int *es_thr;
   uint32_t *hdr_words;   // device, 64 words
   uint32_t *out_words;   // device
+  uint32_t *out_words2;  // device: the other frame of a begin / end pipeline (thor_enc_frames_begin)
+  int opar;              // which of the two the next frame packs into
   int out_cap_words;
   int *out_bits;         // device
   // last coded frame
@@ -302,6 +305,7 @@ static int enc_alloc(thor_enc *e) {
   if (!dev_alloc(&e->hdr_words, 64 * 4, "thor_enc_create: header words")) return g_create_err.code;
   e->out_cap_words = (int)(((size_t)W * H * 2) / 4 + 1024);  // 16 bits per pixel: far above any real frame
   if (!dev_alloc(&e->out_words, (size_t)e->out_cap_words * 4 + 8, "thor_enc_create: output words")) return g_create_err.code;
+  if (!dev_alloc(&e->out_words2, (size_t)e->out_cap_words * 4 + 8, "thor_enc_create: output words (2)")) return g_create_err.code;
   if (!dev_alloc(&e->out_bits, sizeof(int), "thor_enc_create: output bit count")) return g_create_err.code;
   std::vector<int> es(2 * 52 * 4);
   te_es_thresholds(e->p.early_skip_thr, es.data());
@@ -325,12 +329,41 @@ struct EncPool {
   // counts (one readback), and pinned staging for the coded words (async
   // readbacks, one synchronisation)
   uint32_t *hdr_all = nullptr;
-  int *nb_all = nullptr;
+  int *nb_all = nullptr;  // [2][THOR_ENC_MAX_BATCH]: the bit counts of up to two batches in flight
+  int *nb_host = nullptr;  // pinned, same shape
+  hipEvent_t ev[2] = {nullptr, nullptr};
   uint8_t *rb_host = nullptr;
   size_t rb_cap = 0;
+  // batches begun and not yet ended (thor_enc_frames_begin / _end), oldest first
+  struct Pending {
+    std::vector<thor_enc *> es;
+    std::vector<int> cur;        // the slot each context coded into
+    std::vector<uint32_t *> words;  // the output buffer each context packed into
+    std::vector<int> frame_num;
+    int buf;                     // nb_all / nb_host / ev index
+    hipStream_t st;
+    // each context's state before the batch (restored when the batch fails)
+    struct Snap {
+      size_t pos;
+      bool first;
+      int last_slot, last_frame_num, opar;
+      std::vector<int> window;
+    };
+    std::vector<Snap> snap;
+  };
+  std::deque<Pending> pending;
+  int next_buf = 0;
 };
 static std::mutex g_pools_mu;
 static std::map<int, EncPool *> g_pools;
+static std::map<int, hipStream_t> g_copy_streams;  // per device: thor_enc_frames_end's readbacks
+
+static hipStream_t copy_stream_for(int device) {
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  hipStream_t &s = g_copy_streams[device];
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
 
 static EncPool &pool_for(int device) {
   std::lock_guard<std::mutex> lk(g_pools_mu);
@@ -347,7 +380,9 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n) {
     EHIP(hipMemset(P.err, 0, 64));
     EHIP(hipMalloc(&P.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
     EHIP(hipMalloc(&P.hdr_all, THOR_ENC_MAX_BATCH * 64 * sizeof(uint32_t)));
-    EHIP(hipMalloc(&P.nb_all, THOR_ENC_MAX_BATCH * sizeof(int)));
+    EHIP(hipMalloc(&P.nb_all, 2 * THOR_ENC_MAX_BATCH * sizeof(int)));
+    EHIP(hipHostMalloc((void **)&P.nb_host, 2 * THOR_ENC_MAX_BATCH * sizeof(int), hipHostMallocDefault));
+    for (int i = 0; i < 2; i++) EHIP(hipEventCreateWithFlags(&P.ev[i], hipEventDisableTiming));
   }
   if (nwork > P.nwork) {
     if (P.scratch) (void)hipFree(P.scratch);
@@ -421,7 +456,21 @@ void thor_enc_destroy(thor_enc_t *e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->progress,
-                  e->clpf_bits, e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_bits};
+                  e->clpf_bits, e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_words2, e->out_bits};
+  {  // a batch still pending with this context (begun, never ended) is dropped
+    EncPool &P = pool_for(e->device);
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (size_t b = 0; b < P.pending.size();) {
+      bool has = false;
+      for (thor_enc *x : P.pending[b].es) has |= x == e;
+      if (has) {
+        (void)hipStreamSynchronize(P.pending[b].st);
+        P.pending.erase(P.pending.begin() + b);
+      } else {
+        b++;
+      }
+    }
+  }
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -536,7 +585,7 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   J.clpf_bits = e->clpf_bits;
   J.clpf_flags = e->clpf_flags;
   J.cellinfo = e->cellinfo;
-  J.out_words = e->out_words;
+  J.out_words = e->opar ? e->out_words2 : e->out_words;
   J.out_bits = e->out_bits;
   J.nsbh = e->nsbh;
   J.nsbv = e->nsbv;
@@ -588,11 +637,18 @@ static int enc_interp(thor_enc *e, const TeFramePlan &pl) {
 }
 
 // Encode the next frame (coding order) of each of `n` contexts with one
-// launch per stage.  orig[i]: DEVICE pointer to context i's input frame
-// thor_enc_next_input(es[i]) as planar I420 (luma stride orig_stride[i],
-// chroma stride / 2).  All contexts must share device and frame size.  The
-// coded frames are read with thor_enc_frame_bytes.
-int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
+// launch per stage, in two halves: thor_enc_frames_begin enqueues every stage
+// of the batch (RD loop, loop filters, CLPF decision, bit packing, the bit
+// counts' readback) and advances the contexts' host state (GOP position,
+// reference window) without waiting; thor_enc_frames_end waits for the oldest
+// batch begun, reads its coded words back and makes them the contexts' chunks
+// (thor_enc_frame_bytes).  Up to two batches may be in flight, so a caller can
+// begin frame i + 1 before ending frame i: the device codes the next frame
+// while the host collects the last one.  orig[i]: DEVICE pointer to context i's
+// input frame thor_enc_next_input(es[i]) as planar I420 (luma stride
+// orig_stride[i], chroma stride / 2).  All contexts must share device and frame
+// size.  thor_enc_frames = begin + end.
+int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
   if (!es || !orig || n <= 0 || n > THOR_ENC_MAX_BATCH) return THOR_ERR_ARG;
   thor_enc *lead = es[0];
   for (int i = 0; i < n; i++) {
@@ -608,9 +664,17 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   const int nwork = n * nrows;
   EncPool &P = pool_for(lead->device);
   std::lock_guard<std::mutex> pool_lock(P.mu);
+  if (P.pending.size() >= 2) return THOR_ERR_ARG;  // end the oldest batch first
+  for (const EncPool::Pending &q : P.pending)
+    for (thor_enc *x : q.es)
+      for (int i = 0; i < n; i++)
+        if (x == es[i] && x->stream != lead->stream) return THOR_ERR_ARG;  // a context's frames stay on one stream
   int rc = pool_reserve(P, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS), (size_t)n * (lead->nsb + 1));
   if (rc != THOR_OK) return rc;
   hipStream_t st = lead->stream;
+  // the pool's workers and scratch are shared: a batch on another stream first waits for the pending ones
+  for (const EncPool::Pending &q : P.pending)
+    if (q.st != st) EHIP(hipStreamSynchronize(q.st));
   std::vector<TeJob> jobs(n);
   std::vector<TeFramePlan> plans(n);
   std::vector<int> cur(n);
@@ -693,25 +757,83 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
   }
   k_enc_pack<<<n, 256, 0, st>>>(P.jobs, P.scan, lead->out_cap_words);
   EHIP(hipGetLastError());
-  // read back every stream's frame: the bit counts in one copy, then every
-  // stream's words into pinned staging, asynchronously, one synchronisation
-  k_enc_nbits<<<1, 512, 0, st>>>(P.jobs, n, P.nb_all);
+  // the bit counts in one copy into pinned memory, an event behind it
+  const int buf = P.next_buf;
+  P.next_buf ^= 1;
+  int *nb_dev = P.nb_all + buf * THOR_ENC_MAX_BATCH, *nb_host = P.nb_host + buf * THOR_ENC_MAX_BATCH;
+  k_enc_nbits<<<1, 512, 0, st>>>(P.jobs, n, nb_dev);
   EHIP(hipGetLastError());
-  std::vector<int> nbits(n);
-  EHIP(hipMemcpyAsync(nbits.data(), P.nb_all, n * sizeof(int), hipMemcpyDeviceToHost, st));
-  EHIP(hipStreamSynchronize(st));
+  EHIP(hipMemcpyAsync(nb_host, nb_dev, n * sizeof(int), hipMemcpyDeviceToHost, st));
+  EHIP(hipEventRecord(P.ev[buf], st));
+  // the batch is in flight: advance every context (the next plan, the reference window)
+  EncPool::Pending q;
+  q.buf = buf;
+  q.st = st;
+  for (int i = 0; i < n; i++) {
+    thor_enc *e = es[i];
+    q.snap.push_back({e->pos, e->first, e->last_slot, e->last_frame_num, e->opar, e->slot_of_window});
+    q.es.push_back(e);
+    q.cur.push_back(cur[i]);
+    q.words.push_back(e->opar ? e->out_words2 : e->out_words);
+    q.frame_num.push_back(plans[i].frame_num);
+    // slide the window: the frame shifted out of ref[32] frees its slot
+    for (int r = 32; r > 0; r--) e->slot_of_window[r] = e->slot_of_window[r - 1];
+    e->slot_of_window[0] = cur[i];
+    e->last_slot = cur[i];
+    e->last_frame_num = plans[i].frame_num;
+    e->first = false;
+    e->pos++;
+    e->opar ^= 1;
+  }
+  P.pending.push_back(std::move(q));
+  return THOR_OK;
+}
+
+// End the oldest batch begun on these contexts (es / n as passed to the begin).
+// On a device error (e.g. a WPP wait that gave up) every pending batch is
+// dropped and the contexts return to their state before the failed one: that
+// frame can be coded again.
+int thor_enc_frames_end(thor_enc_t *const *es, int n) {
+  if (!es || n <= 0) return THOR_ERR_ARG;
+  EHIP(hipSetDevice(es[0]->device));
+  EncPool &P = pool_for(es[0]->device);
+  std::lock_guard<std::mutex> pool_lock(P.mu);
+  if (P.pending.empty() || (int)P.pending.front().es.size() != n) return THOR_ERR_ARG;
+  for (int i = 0; i < n; i++)
+    if (P.pending.front().es[i] != es[i]) return THOR_ERR_ARG;
+  EncPool::Pending q = std::move(P.pending.front());
+  P.pending.pop_front();
+  hipStream_t st = q.st;
+  EHIP(hipEventSynchronize(P.ev[q.buf]));
+  const int *nbits = P.nb_host + q.buf * THOR_ENC_MAX_BATCH;
   unsigned err = 0;
   EHIP(hipMemcpy(&err, P.err, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (err) {
-    fprintf(stderr, "thor_amd enc: device error flags 0x%x\n", err);
-    EHIP(hipMemset(P.err, 0, 4));
-    return THOR_ERR_HIP;
+  bool bad = err != 0;
+  for (int i = 0; i < n && !bad; i++) bad = nbits[i] < 0;
+  if (bad) {  // drop what is in flight, restore the contexts to before this batch
+    EHIP(hipStreamSynchronize(st));
+    for (const EncPool::Pending &r : P.pending) EHIP(hipStreamSynchronize(r.st));
+    std::deque<EncPool::Pending> later;
+    later.swap(P.pending);
+    for (int i = 0; i < n; i++) {
+      thor_enc *e = q.es[i];
+      const EncPool::Pending::Snap &sn = q.snap[i];
+      e->pos = sn.pos;
+      e->first = sn.first;
+      e->last_slot = sn.last_slot;
+      e->last_frame_num = sn.last_frame_num;
+      e->opar = sn.opar;
+      e->slot_of_window = sn.window;
+    }
+    if (err) {
+      fprintf(stderr, "thor_amd enc: device error flags 0x%x\n", err);
+      EHIP(hipMemset(P.err, 0, 4));
+      return THOR_ERR_HIP;
+    }
+    return THOR_ERR_NOMEM;  // a frame over the output buffer
   }
   std::vector<size_t> woff(n + 1, 0);
-  for (int i = 0; i < n; i++) {
-    if (nbits[i] < 0) return THOR_ERR_NOMEM;
-    woff[i + 1] = woff[i] + ((((size_t)nbits[i] + 7) / 8 + 3) / 4) * 4;
-  }
+  for (int i = 0; i < n; i++) woff[i + 1] = woff[i] + ((((size_t)nbits[i] + 7) / 8 + 3) / 4) * 4;
   if (woff[n] > P.rb_cap) {
     if (P.rb_host) (void)hipHostFree(P.rb_host);
     P.rb_host = nullptr;
@@ -719,12 +841,14 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
     EHIP(hipHostMalloc((void **)&P.rb_host, woff[n] * 2 + 4096, hipHostMallocDefault));
     P.rb_cap = woff[n] * 2 + 4096;
   }
+  // on a stream of their own: the batch's stream may already run the next batch
+  hipStream_t cs = copy_stream_for(es[0]->device);
   for (int i = 0; i < n; i++)
     if (woff[i + 1] > woff[i])
-      EHIP(hipMemcpyAsync(P.rb_host + woff[i], es[i]->out_words, woff[i + 1] - woff[i], hipMemcpyDeviceToHost, st));
-  EHIP(hipStreamSynchronize(st));
+      EHIP(hipMemcpyAsync(P.rb_host + woff[i], q.words[i], woff[i + 1] - woff[i], hipMemcpyDeviceToHost, cs));
+  EHIP(hipStreamSynchronize(cs));
   for (int i = 0; i < n; i++) {
-    thor_enc *e = es[i];
+    thor_enc *e = q.es[i];
     const size_t nb = ((size_t)nbits[i] + 7) / 8;
     const uint32_t *w = (const uint32_t *)(P.rb_host + woff[i]);
     e->chunk.resize(4 + nb);
@@ -733,19 +857,25 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
     e->chunk[2] = (uint8_t)(nb >> 8);
     e->chunk[3] = (uint8_t)nb;
     for (size_t b = 0; b < nb; b++) e->chunk[4 + b] = (uint8_t)(w[b >> 2] >> (24 - 8 * (b & 3)));
-    // slide the window: the frame shifted out of ref[32] frees its slot
-    for (int r = 32; r > 0; r--) e->slot_of_window[r] = e->slot_of_window[r - 1];
-    e->slot_of_window[0] = cur[i];
-    e->last_slot = cur[i];
-    e->last_frame_num = plans[i].frame_num;
-    e->first = false;
-    e->pos++;
   }
   return THOR_OK;
 }
 
+int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
+  const int rc = thor_enc_frames_begin(es, n, orig, orig_stride);
+  if (rc != THOR_OK) return rc;
+  return thor_enc_frames_end(es, n);
+}
+
 int thor_enc_reset(thor_enc_t *e) {
   if (!e) return THOR_ERR_ARG;
+  {  // not with a batch begun and not ended
+    EncPool &P = pool_for(e->device);
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (const EncPool::Pending &q : P.pending)
+      for (thor_enc *x : q.es)
+        if (x == e) return THOR_ERR_ARG;
+  }
   EHIP(hipSetDevice(e->device));
   EHIP(hipStreamSynchronize(e->stream));
   e->pos = 0;

@@ -537,9 +537,10 @@ TE_FN int te_encode_final(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_) {
   const TeFrame &F = *te_lds(&F_);
   TeBlockInfo &bi = *te_lds(&bi_);
   TeBits &b = *te_lds(&b_);
-  if (!F.enable_tb_split) {  // re_use
-    const int size = bi.size, sC = size / 2;
-    te_copy_bytes(bi.rec, bi.rec_best, size * size + 2 * sC * sC);
+  if (!F.enable_tb_split) {  // re_use: the best candidate's reconstruction becomes rec (a swap, as copy_best does)
+    uint8_t *t = bi.rec;
+    bi.rec = bi.rec_best;
+    bi.rec_best = t;
     if (bi.best_nbits >= 0) {  // the best candidate's own syntax bits
       te_put_kept(b, bi.best_bits, bi.best_nbits);
       return bi.best_nbits;
@@ -1968,7 +1969,8 @@ int te_check_early_skip(const TeFrame &F_, const TeBlockInfo &bi_, const TeParam
 }
 
 // search_early_skip_candidates, :2743-2783
-TE_NOINL int te_search_early_skip(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef) {
+TE_NOINL int te_search_early_skip(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_, int16_t *tmp_coef,
+                                  uint32_t *best_cost) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_here();
   TeSB &sb = *te_lds(&sb_);
@@ -2002,6 +2004,7 @@ TE_NOINL int te_search_early_skip(const TeFrame &F_, TeSB &sb_, TeBlockInfo &bi_
       }
     }
   }
+  *best_cost = min_cost;
   return early;
 }
 
@@ -2073,15 +2076,19 @@ TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xp
   }
   if (encode_this && ft != TE_I && F.early_skip_thr > 0.0f) {
     bi.final_encode = 2;
-    const int early = te_search_early_skip(F, sb, bi, tmp_coef);
+    uint32_t es_cost = 0;
+    const int early = te_search_early_skip(F, sb, bi, tmp_coef, &es_cost);
     te_rewind(b, pos_ref);
     if (early) {
       bi.final_encode = 3;
-      if (bi.bp.mode != TE_SKIP || bi.bp.tb_param != 0) bi.best_nbits = -1;
+      // the best candidate (a SKIP, tb_param 0) is re-used as it was costed: its reconstruction and bits,
+      // hence its cost_calc (:2966-2967) -- recomputed only if the parameters had to change
+      const int same = bi.bp.mode == TE_SKIP && bi.bp.tb_param == 0 && !F.enable_tb_split;
+      if (!same) bi.best_nbits = -1;
       bi.bp.mode = TE_SKIP;
       bi.bp.tb_param = 0;
       const int nbit = te_encode_final(F, b, bi);
-      cost = te_cost(F, bi, bi.rec, SIZE, SIZE, nbit);
+      cost = same ? es_cost : te_cost(F, bi, bi.rec, SIZE, SIZE, nbit);
       te_commit_block(F, bi);
       return cost;
     }

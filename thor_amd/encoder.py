@@ -131,3 +131,24 @@ def encode_batch(encs):
     strides = (C.c_int * n)(*[e.W for e in encs])
     L.check(lib.thor_enc_frames(hs, n, ptrs, strides), "thor_enc_frames")
     return [e.chunk() for e in encs]
+
+
+def encode_batch_begin(encs):
+    """Enqueue the next frame of every encoder in `encs` (thor_enc_frames_begin):
+    returns at once; encode_batch_end(encs) collects it.  The following frame
+    may be begun before this one is ended (two batches in flight)."""
+    n = len(encs)
+    lib = encs[0].lib
+    hs = (C.c_void_p * n)(*[e.h for e in encs])
+    ptrs = (C.c_void_p * n)(*[e.next_input_ptr() for e in encs])
+    strides = (C.c_int * n)(*[e.W for e in encs])
+    L.check(lib.thor_enc_frames_begin(hs, n, ptrs, strides), "thor_enc_frames_begin")
+
+
+def encode_batch_end(encs):
+    """The oldest batch begun on `encs`: every encoder's coded frame (bytes)."""
+    n = len(encs)
+    lib = encs[0].lib
+    hs = (C.c_void_p * n)(*[e.h for e in encs])
+    L.check(lib.thor_enc_frames_end(hs, n), "thor_enc_frames_end")
+    return [e.chunk() for e in encs]

@@ -60,7 +60,7 @@ BATCHED_SYMBOLS = [
     "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_stage_marks", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
-    "thor_enc_next_input", "thor_enc_stream", "thor_enc_set_cu_mask", "thor_enc_frames", "thor_enc_frame", "thor_enc_frame_bytes",
+    "thor_enc_next_input", "thor_enc_stream", "thor_enc_set_cu_mask", "thor_enc_frames", "thor_enc_frames_begin", "thor_enc_frames_end", "thor_enc_frame", "thor_enc_frame_bytes",
     "thor_enc_read_recon", "thor_enc_reset", "thor_enc_debug_stall",
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
@@ -170,6 +170,10 @@ def load(path: str = LIB_PATH):
     L.thor_enc_set_cu_mask.restype = i
     L.thor_enc_frames.argtypes = [P, i, P, P]
     L.thor_enc_frames.restype = i
+    L.thor_enc_frames_begin.argtypes = [P, i, P, P]
+    L.thor_enc_frames_begin.restype = i
+    L.thor_enc_frames_end.argtypes = [P, i]
+    L.thor_enc_frames_end.restype = i
     L.thor_enc_frame.argtypes = [P, P, i]
     L.thor_enc_frame.restype = i
     L.thor_enc_frame_bytes.argtypes = [P, P, C.c_size_t]
