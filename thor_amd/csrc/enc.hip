@@ -668,7 +668,7 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
   for (const EncPool::Pending &q : P.pending)
     for (thor_enc *x : q.es)
       for (int i = 0; i < n; i++)
-        if (x == es[i] && x->stream != lead->stream) return THOR_ERR_ARG;  // a context's frames stay on one stream
+        if (x == es[i] && q.st != lead->stream) return THOR_ERR_ARG;  // a context's frames stay on one batch stream
   int rc = pool_reserve(P, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS), (size_t)n * (lead->nsb + 1));
   if (rc != THOR_OK) return rc;
   hipStream_t st = lead->stream;
