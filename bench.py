@@ -800,8 +800,8 @@ def main():
                     if chunks is None:
                         return
 
-                    def host_leg(j):
-                        return decs[ks[j]].upload(parsers[j].parse(chunks[j]), pools[ks[j]][i])
+                    def host_leg(j):  # parse + one host image + one copy, native (GIL released)
+                        return decs[ks[j]].upload_payload(parsers[j], chunks[j], pools[ks[j]][i])
 
                     ds = list(pool.map(host_leg, range(len(ks))))
                     for g in gs:

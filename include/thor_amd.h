@@ -314,6 +314,18 @@ thor_parser_t *thor_parser_create(void);
 void thor_parser_destroy(thor_parser_t *p);
 int thor_parser_seq(const thor_parser_t *p, thor_seq_t *seq);
 int thor_parse_frame(thor_parser_t *p, const uint8_t *payload, size_t nbytes, thor_parsed_frame_t *out);
+/* One host image of a parsed frame's decoder input, for ONE host-to-device copy:
+ * descriptors | coefficient pool | CLPF flags | intra list | TU list | CLPF list
+ * | slow list, each part 256-byte aligned (the thor_build_* lists built here).
+ * Returns THOR_OK with the image written, or THOR_ERR_NOMEM when `cap` is below
+ * lay->bytes (`img` may be NULL to size it); lay gets the parts' offsets and
+ * counts either way (n_flags = 0 and n_clpf = -1 when the frame signals no CLPF). */
+typedef struct thor_frame_image {
+  uint64_t bytes;
+  uint64_t off_blocks, off_coeffs, off_flags, off_intra, off_tus, off_clpf, off_slow;
+  int32_t nblocks, ncoeffs, n_flags, n_intra, n_tu, n_clpf, n_slow;
+} thor_frame_image_t;
+int thor_frame_image(const thor_parsed_frame_t *pf, uint8_t *img, size_t cap, thor_frame_image_t *lay);
 
 /* ---- device-resident encoder (the full RD loop) ---- *
  * Encoder parameters: enc_params (enc/mainenc.h:34-88), the flags of the

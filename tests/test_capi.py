@@ -160,3 +160,50 @@ def test_build_slow_list_host_helper():
         seq, frames = parse_stream(open(os.path.join(ROOT, "tests", "golden", name), "rb").read())
         for fr in frames:
             assert host(fr.blocks, seq.width, seq.height) == _slow_units_py(fr.blocks, seq.width, seq.height), name
+
+
+def test_frame_image_matches_the_host_lists():
+    """thor_frame_image: one 256-aligned host image of a parsed frame whose parts
+    equal the parse output and the thor_build_* lists (the native form of
+    GpuDecoder.upload's image)."""
+    import ctypes as C
+
+    import numpy as np
+    from thor_amd.bitstream import split_chunks
+    from thor_amd.decoder import TU_DTYPE
+    from thor_amd.trace import BLOCK_DTYPE
+
+    lib = L.load()
+    for name in ("cif_high.bit", "k4_med.bit"):
+        p = lib.thor_parser_create()
+        try:
+            for payload in split_chunks(open(os.path.join(ROOT, "tests", "golden", name), "rb").read()):
+                out = L.ThorParsedFrame()
+                buf = C.create_string_buffer(payload, len(payload))
+                assert lib.thor_parse_frame(p, buf, len(payload), C.byref(out)) == 0
+                lay = L.ThorFrameImage()
+                assert lib.thor_frame_image(C.byref(out), None, 0, C.byref(lay)) == L.THOR_ERR_NOMEM
+                img = np.zeros(lay.bytes, np.uint8)
+                assert lib.thor_frame_image(C.byref(out), img.ctypes.data, img.nbytes, C.byref(lay)) == 0
+                nb = out.nblocks
+                blocks = np.frombuffer((C.c_uint8 * (nb * 72)).from_address(out.blocks), BLOCK_DTYPE).copy()
+                assert img[lay.off_blocks:lay.off_blocks + nb * 72].tobytes() == blocks.tobytes()
+                coeffs = np.frombuffer((C.c_int16 * out.ncoeffs).from_address(out.coeffs), np.int16)
+                assert np.array_equal(img[lay.off_coeffs:lay.off_coeffs + 2 * out.ncoeffs].view(np.int16), coeffs)
+                n = lib.thor_build_tu_list(blocks.ctypes.data, nb, None)
+                tus = np.zeros(max(n, 1), TU_DTYPE)
+                lib.thor_build_tu_list(blocks.ctypes.data, nb, tus.ctypes.data)
+                assert lay.n_tu == n and img[lay.off_tus:lay.off_tus + 12 * n].tobytes() == tus[:n].tobytes()
+                n = lib.thor_build_slow_list(blocks.ctypes.data, nb, out.seq.width, out.seq.height, None)
+                sl = np.zeros(max(n, 1), np.uint32)
+                lib.thor_build_slow_list(blocks.ctypes.data, nb, out.seq.width, out.seq.height, sl.ctypes.data)
+                assert lay.n_slow == n and np.array_equal(img[lay.off_slow:lay.off_slow + 4 * n].view(np.uint32), sl[:n])
+                if out.hdr.clpf_on:
+                    assert lay.n_flags == out.nclpf and lay.n_clpf >= 0
+                else:
+                    assert lay.n_flags == 0 and lay.n_clpf == -1
+                for off in (lay.off_blocks, lay.off_coeffs, lay.off_flags, lay.off_intra, lay.off_tus, lay.off_clpf,
+                            lay.off_slow):
+                    assert off % 256 == 0
+        finally:
+            lib.thor_parser_destroy(p)

@@ -706,4 +706,44 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
   return THOR_OK;
 }
 
+int thor_frame_image(const thor_parsed_frame_t *pf, uint8_t *img, size_t cap, thor_frame_image_t *lay) {
+  if (!pf || !lay || pf->nblocks < 0 || pf->ncoeffs < 0 || pf->nclpf < 0 || (pf->nblocks > 0 && !pf->blocks) ||
+      (pf->ncoeffs > 0 && !pf->coeffs) || (pf->nclpf > 0 && !pf->clpf_flags))
+    return THOR_ERR_ARG;
+  const thor_block_t *bl = pf->blocks;
+  const int nb = pf->nblocks, W = pf->seq.width, H = pf->seq.height;
+  const int nflags = pf->hdr.clpf_on ? pf->nclpf : 0;
+  memset(lay, 0, sizeof(*lay));
+  lay->nblocks = nb;
+  lay->ncoeffs = pf->ncoeffs;
+  lay->n_flags = nflags;
+  lay->n_intra = thor_build_intra_list(bl, nb, nullptr);
+  lay->n_tu = thor_build_tu_list(bl, nb, nullptr);
+  lay->n_clpf = nflags ? thor_build_clpf_list(pf->clpf_flags, nflags, nullptr) : -1;
+  lay->n_slow = thor_build_slow_list(bl, nb, W, H, nullptr);
+  if (lay->n_intra < 0 || lay->n_tu < 0 || lay->n_slow < 0) return THOR_ERR_ARG;
+  uint64_t o = 0;
+  auto part = [&](uint64_t &off, uint64_t n) {
+    off = o;
+    o += (n + 255) & ~(uint64_t)255;
+  };
+  part(lay->off_blocks, (uint64_t)nb * sizeof(thor_block_t));
+  part(lay->off_coeffs, (uint64_t)pf->ncoeffs * sizeof(int16_t));
+  part(lay->off_flags, (uint64_t)nflags);
+  part(lay->off_intra, (uint64_t)lay->n_intra * 4);
+  part(lay->off_tus, (uint64_t)lay->n_tu * sizeof(thor_tu_t));
+  part(lay->off_clpf, (uint64_t)(lay->n_clpf > 0 ? lay->n_clpf : 0) * 4);
+  part(lay->off_slow, (uint64_t)lay->n_slow * 4);
+  lay->bytes = o > 256 ? o : 256;
+  if (!img || cap < lay->bytes) return THOR_ERR_NOMEM;
+  if (nb) memcpy(img + lay->off_blocks, bl, (size_t)nb * sizeof(thor_block_t));
+  if (pf->ncoeffs) memcpy(img + lay->off_coeffs, pf->coeffs, (size_t)pf->ncoeffs * sizeof(int16_t));
+  if (nflags) memcpy(img + lay->off_flags, pf->clpf_flags, (size_t)nflags);
+  thor_build_intra_list(bl, nb, (uint32_t *)(img + lay->off_intra));
+  thor_build_tu_list(bl, nb, (thor_tu_t *)(img + lay->off_tus));
+  if (nflags) thor_build_clpf_list(pf->clpf_flags, nflags, (uint32_t *)(img + lay->off_clpf));
+  thor_build_slow_list(bl, nb, W, H, (uint32_t *)(img + lay->off_slow));
+  return THOR_OK;
+}
+
 }  // extern "C"

@@ -179,6 +179,35 @@ class GpuDecoder:
         return DeviceFrame(hdr, bp, len(blocks), cp, fp if flags.size else 0, ip, n_intra, tp, n_tu, lp, n_clpf,
                            sp, n_slow, nbytes)
 
+    def upload_payload(self, parser, payload: bytes, pool=None) -> DeviceFrame:
+        """Parse one frame payload (parser: a thor_amd.bitstream.Parser of this
+        stream) and upload its decoder input in one copy: the parse, the work
+        lists and the host image all in native code (thor_parse_frame +
+        thor_frame_image), no per-part numpy arrays."""
+        out = L.ThorParsedFrame()
+        buf = C.create_string_buffer(payload, len(payload))
+        rc = self.lib.thor_parse_frame(parser.h, buf, len(payload), C.byref(out))
+        if rc != 0:
+            raise ValueError("thor_parse_frame failed (%d)" % rc)
+        lay = L.ThorFrameImage()
+        img = pool.get("img") if pool is not None else None
+        rc = self.lib.thor_frame_image(C.byref(out), img.ctypes.data if img is not None else None,
+                                       img.nbytes if img is not None else 0, C.byref(lay))
+        if rc == L.THOR_ERR_NOMEM:
+            img = np.empty(lay.bytes + (lay.bytes >> 2), np.uint8)
+            if pool is not None:
+                pool["img"] = img
+            rc = self.lib.thor_frame_image(C.byref(out), img.ctypes.data, img.nbytes, C.byref(lay))
+        L.check(rc, "thor_frame_image")
+        base = self._buf(img[:lay.bytes], pool, 0).ptr
+        h = out.hdr
+        hdr = L.ThorFrameHdr(h.frame_num, h.frame_type, h.qp, h.clpf_on, (C.c_int32 * 2)(h.interp_ref[0], h.interp_ref[1]),
+                             h.interp_ratio, h.interp_pos)
+        return DeviceFrame(hdr, base + lay.off_blocks, lay.nblocks, base + lay.off_coeffs,
+                           base + lay.off_flags if lay.n_flags else 0, base + lay.off_intra, lay.n_intra,
+                           base + lay.off_tus, lay.n_tu, base + lay.off_clpf, lay.n_clpf, base + lay.off_slow,
+                           lay.n_slow, int(lay.bytes))
+
     def decode(self, d: DeviceFrame):
         fi = self.frame_in(d)
         hs = (C.c_void_p * 1)(self.h)

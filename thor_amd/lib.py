@@ -46,6 +46,13 @@ class ThorFrameIn(C.Structure):
                 ("clpf_list", C.c_void_p), ("n_clpf", C.c_int32), ("slow_list", C.c_void_p), ("n_slow", C.c_int32)]
 
 
+class ThorFrameImage(C.Structure):
+    """thor_frame_image_t (include/thor_amd.h)."""
+    _fields_ = [(n, C.c_uint64) for n in ("bytes", "off_blocks", "off_coeffs", "off_flags", "off_intra", "off_tus",
+                                          "off_clpf", "off_slow")] + \
+        [(n, C.c_int32) for n in ("nblocks", "ncoeffs", "n_flags", "n_intra", "n_tu", "n_clpf", "n_slow")]
+
+
 class ThorParsedFrame(C.Structure):
     """thor_parsed_frame_t (include/thor_amd.h)."""
     _fields_ = [("seq", ThorSeq), ("hdr", ThorFrameHdr), ("decode_order", C.c_int32), ("num_ref", C.c_int32),
@@ -62,7 +69,7 @@ BATCHED_SYMBOLS = [
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_set_cu_mask", "thor_enc_frames", "thor_enc_frames_begin", "thor_enc_frames_end", "thor_enc_frame", "thor_enc_frame_bytes",
     "thor_enc_read_recon", "thor_enc_reset", "thor_enc_debug_stall",
-    "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame",
+    "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame", "thor_frame_image",
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
     "thor_last_create_error",
@@ -186,6 +193,8 @@ def load(path: str = LIB_PATH):
     L.thor_parser_seq.restype = i
     L.thor_parse_frame.argtypes = [P, P, C.c_size_t, C.POINTER(ThorParsedFrame)]
     L.thor_parse_frame.restype = i
+    L.thor_frame_image.argtypes = [C.POINTER(ThorParsedFrame), P, C.c_size_t, C.POINTER(ThorFrameImage)]
+    L.thor_frame_image.restype = i
     L.thor_pyramid_levels.argtypes = [i, i]
     L.thor_pyramid_levels.restype = i
     L.thor_scale_pyramid.argtypes = [P, i, i, i, P, P, i, P]

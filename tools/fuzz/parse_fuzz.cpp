@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "../../thor_amd/csrc/host_lists.h"
 #include "../../thor_amd/csrc/parse.hip"
 
 typedef std::vector<uint8_t> Bytes;
@@ -51,6 +52,11 @@ static int parse_all(const std::vector<Bytes> &fr, int *bad) {
       for (int i = 0; i < out.nblocks; i++) s += out.blocks[i].coeff_off[0] + out.blocks[i].size + out.blocks[i].qp;
       for (int i = 0; i < out.ncoeffs; i++) s += out.coeffs[i];
       for (int i = 0; i < out.nclpf; i++) s += out.clpf_flags[i];
+      // the decoder's upload image (thor_frame_image): sized, then written
+      thor_frame_image_t lay;
+      if (thor_frame_image(&out, nullptr, 0, &lay) != THOR_ERR_NOMEM) (*bad)++;
+      std::vector<uint8_t> img(lay.bytes);
+      if (thor_frame_image(&out, img.data(), img.size(), &lay) != THOR_OK) (*bad)++;
     } else if (rc > 0 || rc < -16) {
       (*bad)++;
     }
