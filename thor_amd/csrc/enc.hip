@@ -135,6 +135,19 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   }
 }
 
+// Every context's cell state (deblock_data, cleared per frame: enc/encode_frame.c:74)
+// and WPP progress words to zero, one launch for the batch (grid y = context),
+// 16-byte stores.
+__global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ jobs, long long cell_bytes) {
+  const TeJob &J = jobs[blockIdx.y];
+  uint4 *c = (uint4 *)J.F.cells;
+  const long long n16 = cell_bytes >> 4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256)
+    c[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < J.nsbv; i += 256) J.progress[i] = 0u;
+}
+
 // TeCell (deblock_data_t) -> the 16-bit cell words the decoder's loop filter
 // kernels read (same packing as prep_body, recon.hip).
 __global__ __launch_bounds__(256) void k_enc_cellinfo(const TeJob *__restrict__ jobs) {
@@ -294,7 +307,7 @@ static int enc_alloc(thor_enc *e) {
   if (!dev_alloc(&e->slots, e->slot_bytes * e->nslots, "thor_enc_create: reconstruction ring")) return g_create_err.code;
   EHIP(hipMemset(e->slots, 0, e->slot_bytes * e->nslots));
   const size_t ncell = (size_t)(W / 4) * (H / 4);
-  if (!dev_alloc(&e->cells, ncell * sizeof(TeCell), "thor_enc_create: cell state")) return g_create_err.code;
+  if (!dev_alloc(&e->cells, ncell * sizeof(TeCell) + 16, "thor_enc_create: cell state")) return g_create_err.code;  // + k_enc_clear's 16-byte rounding
   if (!dev_alloc(&e->cellinfo, ncell * sizeof(uint16_t), "thor_enc_create: cell side info")) return g_create_err.code;
   if (!dev_alloc(&e->sb_words, (size_t)e->nsb * THOR_ENC_SB_WORDS * 4, "thor_enc_create: SB bit strings")) return g_create_err.code;
   if (!dev_alloc(&e->sb_nbits, (size_t)e->nsb * sizeof(int), "thor_enc_create: SB bit counts")) return g_create_err.code;
@@ -600,9 +613,7 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
     if (hb.bytes[i >> 3] & (0x80 >> (i & 7))) hw[i >> 5] |= 0x80000000u >> (i & 31);
   J.hdr_bits = (int)hb.nbits;
   J.hdr_words = hdr_dev;
-  EHIP(hipMemsetAsync(e->cells, 0, (size_t)(W / 4) * (H / 4) * sizeof(TeCell), st));
-  EHIP(hipMemsetAsync(e->progress, 0, (size_t)e->nsbv * sizeof(unsigned), st));
-  return THOR_OK;
+  return THOR_OK;  // the cells and progress words are cleared by k_enc_clear (one launch for the batch)
 }
 
 static thor_yuv_planes_t enc_slot_planes(const thor_enc *e, int slot) {
@@ -705,6 +716,14 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
       }
   EHIP(hipMemcpyAsync(P.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
   EHIP(hipMemsetAsync(P.ticket, 0, 4, st));
+  {
+    const long long cb = (long long)(W / 4) * (H / 4) * (long long)sizeof(TeCell);
+    static_assert(sizeof(TeCell) % 4 == 0, "cells clear as words");
+    const long long n16 = (cb + 15) / 16;
+    const int gx = (int)((n16 + 255) / 256 < 1024 ? (n16 + 255) / 256 : 1024);
+    k_enc_clear<<<dim3(gx > 0 ? gx : 1, n), 256, 0, st>>>(P.jobs, ((cb + 15) / 16) * 16);
+    EHIP(hipGetLastError());
+  }
   // persistent workers take row tickets until none are left: more workgroups
   // than the chip holds at once (two per SIMD at this kernel's register and LDS
   // use) would only start as the first ones run out of work
