@@ -14,29 +14,34 @@ from conftest import GOLD
 pytestmark = pytest.mark.gpu
 
 
+def _load(name, nframes):
+    from conftest import trace_path
+    from thor_amd.trace import load_trace
+
+    meta = json.load(open(os.path.join(GOLD, "streams.json")))[name]
+    bit = os.path.join(GOLD, name + ".bit")
+    if os.path.exists(bit):  # the host parser's output (carries the interpolated-reference headers)
+        from thor_amd.bitstream import parse_stream
+
+        seq, frames = parse_stream(open(bit, "rb").read())
+    else:
+        seq, frames = load_trace(trace_path(name))
+    return meta, seq, frames[:nframes]
+
+
 def _worker(rank, world, port, name, nframes, q, local=False, halo=False, boundary=False):
     import hashlib
 
     import torch.distributed as dist
 
-    from conftest import trace_path
     from thor_amd.decoder import GpuDecoder
     from thor_amd.shard import RowShard
-    from thor_amd.trace import load_trace
 
     dec = None
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        meta = json.load(open(os.path.join(GOLD, "streams.json")))[name]
-        bit = os.path.join(GOLD, name + ".bit")
-        if os.path.exists(bit):  # the host parser's output (carries the interpolated-reference headers)
-            from thor_amd.bitstream import parse_stream
-
-            seq, frames = parse_stream(open(bit, "rb").read())
-        else:
-            seq, frames = load_trace(trace_path(name))
-        frames = frames[:nframes]
+        meta, seq, frames = _load(name, nframes)
         dec = GpuDecoder(seq)
         sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=False, band_local=local, halo=halo,
                       boundary=boundary)
@@ -129,3 +134,51 @@ def test_row_shard_device_exchange_rccl(local):
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["bit_exact"] is True, line
+
+
+# The device-exchange (RCCL) branches with several ranks and partial bands: one
+# thread per rank, every rank's decoder context and staging tensors on cuda:0,
+# tests/fake_dist.py standing in for torch.distributed with nccl's stream
+# semantics (the box has one card, so RCCL itself cannot run two ranks there).
+# This is the decoder-stream / collective-stream event ordering of shard.py's
+# device path under real concurrency; RCCL's own transport stays unverified.
+@pytest.mark.parametrize("name,nframes,world,mode", [
+    ("k4_med", 8, 2, "gather"), ("cif_med", 10, 3, "gather"),
+    ("k4_med", 8, 3, "local"), ("cif_hdbi", 9, 2, "local"),
+    ("k4_med", 8, 3, "halo"), ("cif_high", 10, 3, "halo"), ("cif_hdbi", 9, 2, "halo"),
+    ("k4_med", 8, 4, "boundary"), ("k4_hdbi", 9, 3, "boundary"), ("hd_low", 6, 2, "boundary")])
+def test_row_shard_device_exchange_threads(name, nframes, world, mode):
+    import hashlib
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fake_dist import run_ranks
+
+    from thor_amd.decoder import GpuDecoder
+    from thor_amd.lib import load
+    from thor_amd.shard import RowShard
+
+    load()  # before the rank threads
+    meta, seq, frames = _load(name, nframes)
+    local, halo, boundary = mode != "gather", mode in ("halo", "boundary"), mode == "boundary"
+
+    def body(rank, dist):
+        dec = GpuDecoder(seq)
+        try:
+            sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=local, halo=halo,
+                          boundary=boundary)
+            assert sh.dstream is not None
+            bad = []
+            for fr in frames:
+                sh.decode(dec.upload(fr), fr.frame_num, fr)
+                got = hashlib.md5(sh.assemble(fr.frame_num) if halo else dec.read_i420(fr.frame_num)).hexdigest()
+                if got != meta["stage_md5"][fr.decode_order]["final"]:
+                    bad.append(fr.decode_order)
+            moved = (sum(sh.boundary_bytes) if boundary else 0) + (sum(sh.halo_bytes) if halo and not boundary else 0)
+            return bad, dist.bytes_moved, moved
+        finally:
+            dec.close()
+
+    res = run_ranks(world, body)
+    assert [r[0] for r in res] == [[] for _ in range(world)], res
+    assert all(r[1] > 0 for r in res), res  # every rank received rows through the device path

@@ -503,3 +503,45 @@ def test_boundary_plan():
     fr.blocks["mode"][np.flatnonzero(rows == 2)[:1]] = 1  # band 0's last row has intra: late
     fr.blocks["mode"][np.flatnonzero(rows == 6)[:1]] = 1  # band 2 has intra; band 1's last row (4) none
     assert sh.boundary_plan(fr) == {0: "late", 1: "early"}
+
+
+@pytest.mark.parametrize("mode,world,W,H", [("gather", 3, 256, 200), ("local", 8, 128, 2160), ("halo", 3, 128, 448),
+                                            ("boundary", 3, 128, 448), ("boundary", 8, 96, 1080)])
+def test_fake_dist_carries_row_shard_protocols(mode, world, W, H):
+    """tests/fake_dist.py (the thread-per-rank stand-in the device-exchange GPU
+    test drives RowShard through) matches and orders every op of the gather,
+    band-local, halo and boundary protocols as gloo does: the same NumpyContext
+    checks pass with CPU tensors and no rank blocks."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fake_dist import run_ranks
+
+    from thor_amd.shard import RowShard
+
+    local, halo, boundary = mode != "gather", mode in ("halo", "boundary"), mode == "boundary"
+
+    def body(rank, dist):
+        rng = np.random.default_rng(13)  # same frames on every rank
+        nf = 5
+        truth = {f: (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8),
+                     rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)) for f in range(nf)}
+        frames = {f: FakeFrame(f, W, H, rng, reach=6) for f in range(nf)}
+        for f in range(nf):
+            b = frames[f].blocks
+            if len(b):
+                rows = b["ypos"].astype(np.int64) >> 6
+                pick = np.isin(rows, [(f + k) % ((H + 63) // 64) for k in (0, 2)])
+                b["mode"][pick & (np.arange(len(b)) % 2 == 0)] = 1
+        ctx = NumpyContext(W, H, truth)
+        if halo:
+            ctx.halo = True
+            ctx.frames = frames
+        sh = RowShard(ctx, dist, W, H, device_exchange=False, band_local=local, halo=halo, boundary=boundary)
+        for f in range(nf):
+            sh.decode(f, f, frames[f])
+        dist.barrier()
+        return dist.bytes_moved
+
+    moved = run_ranks(world, body)
+    assert all(m > 0 for m in moved), moved
