@@ -142,43 +142,26 @@ def test_row_shard_device_exchange_rccl(local):
 # semantics (the box has one card, so RCCL itself cannot run two ranks there).
 # This is the decoder-stream / collective-stream event ordering of shard.py's
 # device path under real concurrency; RCCL's own transport stays unverified.
-@pytest.mark.parametrize("name,nframes,world,mode", [
-    ("k4_med", 8, 2, "gather"), ("cif_med", 10, 3, "gather"),
-    ("k4_med", 8, 3, "local"), ("cif_hdbi", 9, 2, "local"),
-    ("k4_med", 8, 3, "halo"), ("cif_high", 10, 3, "halo"), ("cif_hdbi", 9, 2, "halo"),
-    ("k4_med", 8, 4, "boundary"), ("k4_hdbi", 9, 3, "boundary"), ("hd_low", 6, 2, "boundary")])
-def test_row_shard_device_exchange_threads(name, nframes, world, mode):
-    import hashlib
+# In a child process (tests/shard_threads_case.py): torch's HIP runtime comes
+# up there before the decoder library's (in this process the library already
+# initialised HIP and torch then finds no GPU).
+THREAD_CASES = [("k4_med", 8, 2, "gather"), ("cif_med", 10, 3, "gather"),
+                ("k4_med", 8, 3, "local"), ("cif_hdbi", 9, 2, "local"),
+                ("k4_med", 8, 3, "halo"), ("cif_high", 10, 3, "halo"), ("cif_hdbi", 9, 2, "halo"),
+                ("k4_med", 8, 4, "boundary"), ("k4_hdbi", 9, 3, "boundary"), ("hd_low", 6, 2, "boundary")]
+
+
+def test_row_shard_device_exchange_threads():
+    import subprocess
     import sys
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from fake_dist import run_ranks
-
-    from thor_amd.decoder import GpuDecoder
-    from thor_amd.lib import load
-    from thor_amd.shard import RowShard
-
-    load()  # before the rank threads
-    meta, seq, frames = _load(name, nframes)
-    local, halo, boundary = mode != "gather", mode in ("halo", "boundary"), mode == "boundary"
-
-    def body(rank, dist):
-        dec = GpuDecoder(seq)
-        try:
-            sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=local, halo=halo,
-                          boundary=boundary)
-            assert sh.dstream is not None
-            bad = []
-            for fr in frames:
-                sh.decode(dec.upload(fr), fr.frame_num, fr)
-                got = hashlib.md5(sh.assemble(fr.frame_num) if halo else dec.read_i420(fr.frame_num)).hexdigest()
-                if got != meta["stage_md5"][fr.decode_order]["final"]:
-                    bad.append(fr.decode_order)
-            moved = (sum(sh.boundary_bytes) if boundary else 0) + (sum(sh.halo_bytes) if halo and not boundary else 0)
-            return bad, dist.bytes_moved, moved
-        finally:
-            dec.close()
-
-    res = run_ranks(world, body)
-    assert [r[0] for r in res] == [[] for _ in range(world)], res
-    assert all(r[1] > 0 for r in res), res  # every rank received rows through the device path
+    here = os.path.dirname(os.path.abspath(__file__))
+    args = [",".join(map(str, c)) for c in THREAD_CASES]
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "shard_threads_case.py")] + args, capture_output=True,
+                       text=True, timeout=240, cwd=os.path.dirname(here))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(res) == len(THREAD_CASES), res
+    for case, (bad, moved) in zip(THREAD_CASES, res):
+        assert bad == [[] for _ in range(case[2])], (case, bad)
+        assert all(m > 0 for m in moved), (case, moved)  # every rank received rows through the device path

@@ -749,6 +749,151 @@ TE_FN void te_load_scan(TeScanRegs &R, const int16_t *c, int q) {
   R.nz[3] = __ballot(R.v3 != 0);
 #endif
 }
+#if !defined(TE_HOST)
+// write_coeff's events from pos 0 with every lane coding its own positions
+// (device).  The coder's mode before position p is a two-state recurrence --
+// level mode continues over non-zero levels and ends after a coded zero; run
+// mode returns to level mode after a level > 1 -- i.e. L[p+1] = big[p] |
+// (nz[p] & L[p]), L[0] = 1, which is the carry chain of nz + big + 1 over the
+// 256 scan positions (scalar adds).  Each lane then codes its position's event
+// -- level mode: the level VLC (table 1 after a previous level-mode level > 3,
+// or at the start of an intra luma block; table 0 otherwise) and the sign;
+// run mode, at a non-zero: the run/level code from the position after the
+// previous event, then the level / sign -- as one code word of <= 58 bits
+// (|level| <= 32768), and the words go into the writer in scan order.  Then
+// the tail: the extra level-mode zero and EOB, as the serial coder.
+TE_FN int te_prev_bit(uint64_t w, int base) { return w ? base + 63 - __builtin_clzll(w) : -1; }
+TE_FN void te_coeff_events(TeBits &b, const TeScanRegs &R, int N, int size, int chroma, int intra, int last_pos) {
+  const int l = TE_LANE;
+  uint64_t big[4], g3[4], Lm[4];
+  big[0] = __ballot(te_abs(R.v0) > 1);
+  big[1] = __ballot(te_abs(R.v1) > 1);
+  big[2] = __ballot(te_abs(R.v2) > 1);
+  big[3] = __ballot(te_abs(R.v3) > 1);
+  g3[0] = __ballot(te_abs(R.v0) > 3);
+  g3[1] = __ballot(te_abs(R.v1) > 3);
+  g3[2] = __ballot(te_abs(R.v2) > 3);
+  g3[3] = __ballot(te_abs(R.v3) > 3);
+  uint64_t cin = 1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t a = R.nz[k], t = a + big[k], s = t + cin;
+    Lm[k] = s ^ a ^ big[k];
+    cin = (t < a) | (s < t);
+  }
+  const uint64_t below = (1ull << l) - 1;  // lanes' lower positions within a word (l < 64)
+  int pl_lo = -1, pe_lo = -1;             // highest level-mode / event position in the words already done
+  const int kmax = last_pos >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (k > kmax) break;
+    const int v = k == 0 ? R.v0 : (k == 1 ? R.v1 : (k == 2 ? R.v2 : R.v3));
+    const int p = 64 * k + l;
+    const uint64_t upto = kmax > k ? ~0ull : (last_pos == 64 * k + 63 ? ~0ull : ((2ull << (last_pos & 63)) - 1));
+    const uint64_t lw = Lm[k] & upto, ew = (Lm[k] | R.nz[k]) & upto;
+    int len = 0;
+    uint64_t code = 0;
+    const int level = te_abs(v), sign = v < 0 ? 1 : 0;
+    if ((lw >> l) & 1) {  // level mode
+      int pl = te_prev_bit(lw & below, 64 * k);
+      if (pl < 0) pl = pl_lo;
+      int adapt = 0;
+      if (!chroma) {
+        if (pl < 0) {
+          adapt = intra;
+        } else {
+          const int kw = pl >> 6;
+          const uint64_t gw = kw == k ? g3[k] : (kw == 0 ? g3[0] : (kw == 1 ? g3[1] : g3[2]));
+          adapt = (int)((gw >> (pl & 63)) & 1);
+        }
+      }
+      unsigned c;
+      len = te_vlc((unsigned)adapt, (unsigned)level, &c);
+      code = c;
+      if (level) {
+        code = (code << 1) | (uint64_t)sign;
+        len++;
+      }
+    } else if ((ew >> l) & 1) {  // run mode, a non-zero level
+      int pe = te_prev_bit(ew & below, 64 * k);
+      if (pe < 0) pe = pe_lo;
+      const int ps = pe + 1, run = p - ps;
+      const int cn = te_find_code(run, level, N - ps - 1, chroma, 0);
+      unsigned c1, c2;
+      int n1, n2;
+      if (chroma && size <= 8) {
+        n1 = te_vlc(10, (unsigned)cn, &c1);
+      } else if (cn == 0) {
+        n1 = 2;
+        c1 = 2;
+      } else {
+        n1 = te_vlc(2, (unsigned)(cn + 1), &c1);
+      }
+      if (level > 1) {
+        n2 = te_vlc(0, (unsigned)(2 * (level - 2) + sign), &c2);
+      } else {
+        n2 = 1;
+        c2 = (unsigned)sign;
+      }
+      code = ((uint64_t)c1 << n2) | c2;
+      len = n1 + n2;
+    }
+    // the words in scan order (the writer is uniform: scalar puts)
+    uint64_t em = __ballot(len > 0);
+    const uint32_t chi = (uint32_t)(code >> 32), clo = (uint32_t)code;
+    while (em) {
+      const int s = __builtin_ctzll(em);
+      em &= em - 1;
+      const int n = __builtin_amdgcn_readlane(len, s);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)clo, s);
+      if (n > 32) {
+        te_put(b, n - 32, (uint32_t)__builtin_amdgcn_readlane((int)chi, s));
+        te_put(b, 32, lo);
+      } else {
+        te_put(b, n, lo);
+      }
+    }
+    const int plw = te_prev_bit(lw, 64 * k), pew = te_prev_bit(ew, 64 * k);
+    if (plw >= 0) pl_lo = plw;
+    if (pew >= 0) pe_lo = pew;
+  }
+  // tail (write_bits.c:223-252): after the last non-zero, still in level mode
+  // -> one more zero level; then EOB unless the block is full
+  int pos = last_pos + 1;
+  if (pos < N) {
+    const int kl = last_pos >> 6;
+    const uint64_t nzw = R.nz[0] * (kl == 0) | R.nz[1] * (kl == 1) | R.nz[2] * (kl == 2) | R.nz[3] * (kl == 3);
+    const uint64_t bw = big[0] * (kl == 0) | big[1] * (kl == 1) | big[2] * (kl == 2) | big[3] * (kl == 3);
+    const uint64_t lmw = Lm[0] * (kl == 0) | Lm[1] * (kl == 1) | Lm[2] * (kl == 2) | Lm[3] * (kl == 3);
+    const int bl = last_pos & 63;
+    const bool fin = ((nzw >> bl) & 1) ? (((bw | lmw) >> bl) & 1) != 0 : true;  // (no non-zero: cbp says never)
+    if (fin) {
+      int adapt = 0;
+      if (!chroma) {
+        if (pl_lo < 0) {
+          adapt = intra;
+        } else {
+          const int kw = pl_lo >> 6;
+          const uint64_t gw = g3[0] * (kw == 0) | g3[1] * (kw == 1) | g3[2] * (kw == 2) | g3[3] * (kw == 3);
+          adapt = (int)((gw >> (pl_lo & 63)) & 1);
+        }
+      }
+      te_put_vlc(b, (unsigned)adapt, 0);
+      pos++;
+    }
+  }
+  if (pos < N) {
+    const int cn = te_find_code(0, 0, 0, chroma, 1);
+    if (chroma && size <= 8) {
+      te_put_vlc(b, 0, cn);
+    } else {
+      if (cn == 0) te_put(b, 2, 2);
+      else te_put_vlc(b, 2, cn + 1);
+    }
+  }
+}
+#endif
+
 // The writer state travels by value (in registers) in and out: a reference
 // would pin the caller's register copy to the stack.  Inlined into
 // write_block (its only caller): no call frame per coded TU.
@@ -775,6 +920,12 @@ TE_FN TeBits te_write_coeff(TeBits b_in, const int16_t *c, int size, int type) {
       te_put(b, 1, 0);
     }
   }
+#if !defined(TE_HOST) && !defined(TE_WCOEF_SERIAL)
+  if (pos == 0) {  // (not the chroma single +-1 DC)
+    te_coeff_events(b, R, N, size, chroma, intra, last_pos);
+    return b;
+  }
+#endif
   int level_mode = 1, level = 1;
   while (pos <= last_pos) {
     if (level_mode) {
@@ -1022,35 +1173,55 @@ TE_NOINL int te_write_block(TeBits &bo_, const TeFrame &F_, const TeBlockInfo &b
       }
     }
     te_put_vlc(b, 0, code);
-    if (tb_split == 0) {
-      if (p.cbp_y) b = te_write_coeff(b, te_tile(p, 0, 0), size, coeff_type | 0);
-      if (p.cbp_u) b = te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1);
-      if (p.cbp_v) b = te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1);
-    } else if (size > 8) {
-      for (int index = 0; index < 4; index++) {
-        const int cy = (p.cbp_y >> (3 - index)) & 1, cu = (p.cbp_u >> (3 - index)) & 1,
-                  cv = (p.cbp_v >> (3 - index)) & 1;
-        code = cbp_table[cy + (cu << 1) + (cv << 2)];
-        if (bi.ctx.cbp == 0 && code < 2) code = 1 - code;
-        te_put_vlc(b, 0, code);
-        if (cy) b = te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0);
-        if (cu) b = te_write_coeff(b, te_tile(p, 1, index), size / 4, coeff_type | 1);
-        if (cv) b = te_write_coeff(b, te_tile(p, 2, index), size / 4, coeff_type | 1);
-      }
-    } else {
-      for (int index = 0; index < 4; index++) {
+    // The coded tiles in syntax order, with the split CBP codes between them,
+    // as one loop: a single coefficient-coder call site (its device body is
+    // large; eight inlined copies doubled write_block's code).
+    //   no split:   Y, U, V
+    //   split > 8:  per quarter: CBP code, Y, U, V
+    //   split 8x8:  per quarter: cbp_y bit, Y; then the chroma CBP, U, V
+    const int nstep = tb_split == 0 ? 3 : (size > 8 ? 16 : 11);
+#pragma clang loop unroll(disable)
+    for (int s = 0; s < nstep; s++) {
+      int comp = 0, index = 0, tsz = 0, on = 0;
+      if (tb_split == 0) {
+        comp = s;
+        tsz = s ? size / 2 : size;
+        on = s == 0 ? p.cbp_y : (s == 1 ? p.cbp_u : p.cbp_v);
+      } else if (size > 8) {
+        index = s >> 2;
+        const int cy = (p.cbp_y >> (3 - index)) & 1, cu = (p.cbp_u >> (3 - index)) & 1, cv = (p.cbp_v >> (3 - index)) & 1;
+        if ((s & 3) == 0) {
+          code = cbp_table[cy + (cu << 1) + (cv << 2)];
+          if (bi.ctx.cbp == 0 && code < 2) code = 1 - code;
+          te_put_vlc(b, 0, code);
+          continue;
+        }
+        comp = (s & 3) - 1;
+        tsz = comp ? size / 4 : size / 2;
+        on = comp == 0 ? cy : (comp == 1 ? cu : cv);
+      } else if (s < 8) {
+        index = s >> 1;
         const int cy = (p.cbp_y >> (3 - index)) & 1;
-        te_put(b, 1, cy);
-        if (cy) b = te_write_coeff(b, te_tile(p, 0, index), size / 2, coeff_type | 0);
+        if ((s & 1) == 0) {
+          te_put(b, 1, cy);
+          continue;
+        }
+        tsz = size / 2;
+        on = cy;
+      } else if (s == 8) {
+        // chroma of an 8x8 CU is not split: cbp_u / cbp_v are the block values here
+        const int cbp = p.cbp_u + 2 * p.cbp_v;
+        if (cbp == 0) te_put(b, 1, 1);
+        else if (cbp == 1) te_put(b, 2, 1);
+        else if (cbp == 2) te_put(b, 3, 1);
+        else te_put(b, 3, 0);
+        continue;
+      } else {
+        comp = s - 8;
+        tsz = size / 2;
+        on = comp == 1 ? p.cbp_u : p.cbp_v;
       }
-      // chroma of an 8x8 CU is not split: cbp_u / cbp_v are the block values here
-      const int cbp = p.cbp_u + 2 * p.cbp_v;
-      if (cbp == 0) te_put(b, 1, 1);
-      else if (cbp == 1) te_put(b, 2, 1);
-      else if (cbp == 2) te_put(b, 3, 1);
-      else te_put(b, 3, 0);
-      if (p.cbp_u) b = te_write_coeff(b, te_tile(p, 1, 0), size / 2, coeff_type | 1);
-      if (p.cbp_v) b = te_write_coeff(b, te_tile(p, 2, 0), size / 2, coeff_type | 1);
+      if (on) b = te_write_coeff(b, te_tile(p, comp, index), tsz, coeff_type | (comp ? 1 : 0));
     }
   }
   bo = b;

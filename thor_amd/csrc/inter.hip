@@ -881,6 +881,9 @@ __device__ __forceinline__ void plan_pass(ReconLds &L, const FrameCtx &f, __amdg
   filter_all(L.win, K, f.bipred, x0, ty, tc, acc, mine, mine);
 }
 
+#ifndef RECON_RES_PREFETCH
+#define RECON_RES_PREFETCH 1
+#endif
 #ifndef RECON_WPE
 #define RECON_WPE 1
 #endif
@@ -968,6 +971,26 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
       const __amdgpu_buffer_rsrc_t ring =
           __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
       const unsigned ma = pa.y, mb = pb.y;
+#if RECON_RES_PREFETCH
+      if ((ma | mb) & (CELL_RES(0) | CELL_RES(1) | CELL_RES(2))) {
+        // The unit's residual lines into L2 now, so the reads after the filter
+        // hit there instead of waiting on HBM: one dword per 128-B line (luma
+        // rows are 2 lines, chroma rows 1), written to LDS the fast path does
+        // not use (buffer_load ... lds holds no register); out-of-range
+        // offsets read nothing (buffer bounds).  Lanes 0-31 luma, 32-47 U/V.
+        typedef __attribute__((address_space(3))) void lds_void;
+        const int npx = f.W * f.H;
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)resid, 0, 3 * npx, 0x00020000);
+        unsigned off = 0xffffffffu;
+        if (lane < 32) {
+          off = 2u * (unsigned)((y0 + (lane >> 1)) * f.W + x0 + 64 * (lane & 1));
+        } else if (lane < 48) {
+          const int wc = f.W >> 1;
+          off = 2u * (unsigned)(npx + ((lane >> 3) & 1) * (npx >> 2) + ((y0 >> 1) + (lane & 7)) * wc + (x0 >> 1));
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_void *)(void *)L.mv0, 4, off, 0, 0, 0);
+      }
+#endif
       const bool mine_a = cc < 16;  // filter lanes: columns of the left SB
       uint32_t ly[8], lc[4];
       {  // pass 0: mv0 (one window when both SBs share the key, else one per SB)
