@@ -564,7 +564,14 @@ TE_FN void te_f121(const uint8_t *in, uint8_t *out, int len) {
 // (enc/encode_block.c:1250, always (left, top)) instead of the position-aware one.
 TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int mode, int search_dc) {
   TE_P(TP_IPRED);
-  const int nn = n * n;
+  // four horizontally adjacent pixels per lane and step (n >= 4), one dword store
+  const int n4 = (n * n) >> 2;
+  auto quad = [&](auto px) {
+    for (int g = TE_LANE; g < n4; g += TE_NL) {
+      const int e = 4 * g, i = te_dv(e, n), j = e - i * n;
+      te_st4(pb + e, te_pack4(px(i, j), px(i, j + 1), px(i, j + 2), px(i, j + 3)));
+    }
+  };
   switch (mode) {
     case TE_PLANAR: {  // :182-214, C division truncating toward zero
       for (int k = TE_LANE; k < 2 * n; k += TE_NL) {
@@ -580,17 +587,14 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       }
       te_sync();
       const int TL = nb.left[1] + 2 * nb.left[0] + 2 * nb.tl + 2 * nb.top[0] + nb.top[1];
-      for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
-        pb[e] = (uint8_t)te_clip255((nb.L[i] + nb.T[j] - TL + 4) / 8);
-      }
+      quad([&](int i, int j) { return te_clip255((nb.L[i] + nb.T[j] - TL + 4) / 8); });
       break;
     }
     case TE_HOR:
-      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.left[te_dv(e, n)];
+      quad([&](int i, int j) { return (int)nb.left[i]; });
       break;
     case TE_VER:
-      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = nb.top[e - te_dv(e, n) * n];
+      quad([&](int i, int j) { return (int)nb.top[j]; });
       break;
     case TE_UPLEFT:
     case TE_UPUPLEFT:
@@ -599,28 +603,29 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       te_f121(nb.top, nb.tF, n);
       const int tlF = (2 * nb.tl + nb.left[0] + nb.top[0] + 2) >> 2;
       te_sync();
-      for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
-        int v;
-        if (mode == TE_UPLEFT) {  // :216-240
+      if (mode == TE_UPLEFT) {  // :216-240
+        quad([&](int i, int j) {
           const int d = i - j;
-          v = d > 0 ? nb.lF[d - 1] : (d == 0 ? tlF : nb.tF[-d - 1]);
-        } else if (mode == TE_UPUPLEFT) {  // :279-307
+          return (int)(d > 0 ? nb.lF[d - 1] : (d == 0 ? tlF : nb.tF[-d - 1]));
+        });
+      } else if (mode == TE_UPUPLEFT) {  // :279-307
+        quad([&](int i, int j) {
           const int d = i - 2 * j;
-          if (d > 1) v = nb.lF[d - 2];
-          else if (d == 1) v = tlF;
-          else if (d == 0) v = (tlF + nb.tF[0]) >> 1;
-          else if (d & 1) v = nb.tF[(-d) / 2];
-          else v = (nb.tF[(-d) / 2] + nb.tF[(-d) / 2 - 1]) >> 1;
-        } else {  // :309-337
+          if (d > 1) return (int)nb.lF[d - 2];
+          if (d == 1) return tlF;
+          if (d == 0) return (tlF + nb.tF[0]) >> 1;
+          if (d & 1) return (int)nb.tF[(-d) / 2];
+          return (nb.tF[(-d) / 2] + nb.tF[(-d) / 2 - 1]) >> 1;
+        });
+      } else {  // :309-337
+        quad([&](int i, int j) {
           const int d = 2 * i - j;
-          if (d < -1) v = nb.tF[-d - 2];
-          else if (d == -1) v = tlF;
-          else if (d == 0) v = (tlF + nb.lF[0]) >> 1;
-          else if (d & 1) v = nb.lF[d / 2];
-          else v = (nb.lF[d / 2] + nb.lF[d / 2 - 1]) >> 1;
-        }
-        pb[e] = (uint8_t)v;
+          if (d < -1) return (int)nb.tF[-d - 2];
+          if (d == -1) return tlF;
+          if (d == 0) return (tlF + nb.lF[0]) >> 1;
+          if (d & 1) return (int)nb.lF[d / 2];
+          return (nb.lF[d / 2] + nb.lF[d / 2 - 1]) >> 1;
+        });
       }
       break;
     }
@@ -628,25 +633,23 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
     case TE_UPUPRIGHT: {
       te_f121(nb.top, nb.tF, 2 * n);
       te_sync();
-      for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
-        if (mode == TE_UPRIGHT) {  // :242-256
-          pb[e] = nb.tF[i + j + 1];
-        } else {  // :258-277
+      if (mode == TE_UPRIGHT) {  // :242-256
+        quad([&](int i, int j) { return (int)nb.tF[i + j + 1]; });
+      } else {  // :258-277
+        quad([&](int i, int j) {
           const int d = i + 2 * j;
-          pb[e] = (d & 1) ? nb.tF[(d + 1) / 2] : (uint8_t)((nb.tF[d / 2] + nb.tF[d / 2 + 1]) >> 1);
-        }
+          return (d & 1) ? (int)nb.tF[(d + 1) / 2] : (nb.tF[d / 2] + nb.tF[d / 2 + 1]) >> 1;
+        });
       }
       break;
     }
     case TE_DOWNLEFTLEFT: {  // :339-361
       te_f121(nb.left, nb.lF, 2 * n);
       te_sync();
-      for (int e = TE_LANE; e < nn; e += TE_NL) {
-        const int i = te_dv(e, n), j = e - te_dv(e, n) * n;
+      quad([&](int i, int j) {
         const int d = 2 * i + j;
-        pb[e] = (d & 1) ? nb.lF[(d + 1) / 2] : (uint8_t)((nb.lF[d / 2] + nb.lF[d / 2 + 1]) >> 1);
-      }
+        return (d & 1) ? (int)nb.lF[(d + 1) / 2] : (nb.lF[d / 2] + nb.lF[d / 2 + 1]) >> 1;
+      });
       break;
     }
     default: {  // DC, :145-160 (and out-of-range modes, :386-387)
@@ -656,7 +659,7 @@ TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int 
       for (int k = TE_LANE; k < n; k += TE_NL) s += a[k] + b[k];
       s = te_sum(s);
       const int dc = ((int)s + n) / (2 * n);
-      for (int e = TE_LANE; e < nn; e += TE_NL) pb[e] = (uint8_t)dc;
+      quad([&](int, int) { return dc; });
       break;
     }
   }
@@ -777,8 +780,10 @@ TE_FN void te_fwd_tx(TeTx &X, int size, int fast) {
 }
 
 // quantize, enc/encode_block.c:75-172 (rdoq = 0): X.C -> levels (q x q
-// raster) in X.C.  Returns cbp.
-TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
+// raster) in X.C.  Returns cbp.  With `coef`: the levels go there (raster)
+// and X.C holds them dequantized instead -- the chains' quantize, level copy
+// and dequantize in one pass (X.C is only read when cbp != 0).
+TE_FN int te_quant_t(TeTx &X, int qp, int size, int type, int16_t *coef) {
   TE_P(TP_QUANT);
   const int intra = (type >> 1) & 1, chroma = type & 1;
   const int lg = te_log2(size), q = TE_MIN(size, 16), nq = q * q;
@@ -820,30 +825,42 @@ TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
   if (cbp) {  // "RDOQ light" (:134-168), serial over the scan.  Only positions whose
     // initial level exceeds 1 can trigger: earlier iterations modify indices
     // below the one they visit, so S[pos] is still its initial value when pos
-    // is visited.  Visit just those, in order, with the current levels.
+    // is visited.  Visit just those, in order.  Every test the loop makes on
+    // the current levels is |S| > 1 or S != 0, so it runs on two scan-order
+    // bit masks (uniform registers) that each change updates -- no LDS round
+    // trip or barrier per candidate; the changed levels go to X.S for the
+    // raster pass below.
     const int n = chroma ? last_pos + 1 : nq;
     const int thr = (73 * te_gdequant[qp % 6] << (qp / 6)) >> (4 + lg);
-    uint64_t cand[4];
+    uint64_t big[4], nzm[4];
 #if defined(TE_HOST)
-    for (int k = 0; k < 4; k++) cand[k] = 0;
-    for (int pos = 2; pos < n; pos++)
-      if (te_abs(X.S[pos]) > 1) cand[pos >> 6] |= 1ULL << (pos & 63);
+    for (int k = 0; k < 4; k++) big[k] = nzm[k] = 0;
+    for (int pos = 0; pos < nq; pos++) {
+      if (te_abs(X.S[pos]) > 1) big[pos >> 6] |= 1ULL << (pos & 63);
+      if (X.S[pos] != 0) nzm[pos >> 6] |= 1ULL << (pos & 63);
+    }
 #else
     for (int k = 0; k < 4; k++) {
       const int pos = TE_LANE + 64 * k;
-      cand[k] = __ballot(pos >= 2 && pos < n && te_abs(X.S[pos]) > 1);
+      const int sv = pos < nq ? X.S[pos] : 0;
+      big[k] = __ballot(te_abs(sv) > 1);
+      nzm[k] = __ballot(sv != 0);
     }
 #endif
+#define TE_BIG(p) ((big[(p) >> 6] >> ((p) & 63)) & 1)
+#define TE_NZ(p) ((nzm[(p) >> 6] >> ((p) & 63)) & 1)
     for (int k = 0; k < 4; k++) {
-      uint64_t m = cand[k];
+      const int lo = TE_MAX(2, 64 * k), hi = TE_MIN(n, 64 * k + 64);
+      if (lo >= hi) continue;
+      uint64_t m = big[k] & (hi - 64 * k >= 64 ? ~0ULL : ((1ULL << (hi - 64 * k)) - 1)) & (~0ULL << (lo - 64 * k));
       while (m) {
         const int pos = k * 64 + __builtin_ctzll(m);
         m &= m - 1;
         int flag = 1;
-        if (pos > 2 && te_abs(X.S[pos - 3]) > 1) flag = 0;
-        if (pos > 3 && te_abs(X.S[pos - 4]) > 1 && te_abs(X.S[pos - 3]) > 0) flag = 0;
+        if (pos > 2 && TE_BIG(pos - 3)) flag = 0;
+        if (pos > 3 && TE_BIG(pos - 4) && TE_NZ(pos - 3)) flag = 0;
         if (pos == 2 && (chroma == 0 || last_pos >= 6)) flag = 0;
-        if (flag && X.S[pos - 2] == 0 && X.S[pos - 1] == 0 && te_abs(X.S[pos]) > 1) {
+        if (flag && !TE_NZ(pos - 2) && !TE_NZ(pos - 1) && TE_BIG(pos)) {
           const int c1 = X.O[pos], c2 = X.O[pos - 1], c3 = X.O[pos - 2];
           const int K1 = te_abs(c1), K2 = te_abs(c2), K3 = te_abs(c3), K4 = TE_MAX(K2, K3);
           int at, v;
@@ -857,22 +874,38 @@ TE_FN int te_quant(TeTx &X, int qp, int size, int type) {
             at = pos - 2;
             v = c3 < 0 ? -1 : 1;
           }
-          te_sync();
           if (TE_LANE == 0) X.S[at] = (int16_t)v;
-          te_sync();
+          big[at >> 6] &= ~(1ULL << (at & 63));  // |v| == 1
+          nzm[at >> 6] |= 1ULL << (at & 63);
         }
       }
     }
+#undef TE_BIG
+#undef TE_NZ
   }
   te_sync();
+  if (coef) {  // the levels to the candidate's coefficient tile, X.C dequantized (common_block.c:132-146)
+    const int rshift = lg - 1, add = 1 << (rshift - 1), lshift = qp / 6, dscale = te_gdequant[qp % 6];
 #pragma unroll
-  for (int t = 0; t < NS; t++) {  // back to raster (:170-174)
-    const int r = TE_LANE + TE_NL * t;
-    if (r < nq) X.C[r] = X.S[posv[t]];
+    for (int t = 0; t < NS; t++) {
+      const int r = TE_LANE + TE_NL * t;
+      if (r < nq) {
+        const int lev = X.S[posv[t]];
+        coef[r] = (int16_t)lev;
+        X.C[r] = (int16_t)te_wrap16(((lev * dscale) * (1 << lshift) + add) >> rshift);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NS; t++) {  // back to raster (:170-174)
+      const int r = TE_LANE + TE_NL * t;
+      if (r < nq) X.C[r] = X.S[posv[t]];
+    }
   }
   te_sync();
   return cbp;
 }
+TE_FN int te_quant(TeTx &X, int qp, int size, int type) { return te_quant_t(X, qp, size, type, nullptr); }
 
 // dequantize (common/common_block.c:132-146), int16 truncating store, in place
 TE_FN void te_dequant(TeTx &X, int qp, int size) {
@@ -881,6 +914,21 @@ TE_FN void te_dequant(TeTx &X, int qp, int size) {
   const int lshift = qp / 6, scale = te_gdequant[qp % 6];
   for (int e = TE_LANE; e < q * q; e += TE_NL) X.C[e] = (int16_t)te_wrap16(((X.C[e] * scale) * (1 << lshift) + add) >> rshift);
   te_sync();
+}
+#ifndef TE_QUANT_FUSE
+#define TE_QUANT_FUSE 1
+#endif
+// quantize -> the levels into the candidate's tile -> X.C dequantized (when cbp)
+TE_FN int te_quant_chain(TeTx &X, int qp, int size, int type, int16_t *coef) {
+#if TE_QUANT_FUSE
+  return te_quant_t(X, qp, size, type, coef);
+#else
+  const int cbp = te_quant(X, qp, size, type);
+  const int q = TE_MIN(size, 16);
+  for (int e = TE_LANE; e < q * q; e += TE_NL) coef[e] = (int16_t)X.C[e];
+  if (cbp) te_dequant(X, qp, size);
+  return cbp;
+#endif
 }
 
 // inverse_transform (common/transform.c:432-518): X.C (q x q) -> X.R

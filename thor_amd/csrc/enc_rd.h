@@ -309,13 +309,8 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, in
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
       te_residual_tx(X, org + i * os + j, os, pb + i * size + j, size, s2, fast);
       te_fwd_tx(X, s2, fast);
-      const int bit = te_quant(X, qp, s2, type);
-      const int q = TE_MIN(s2, 16);
-      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * ts + e] = (int16_t)X.C[e];
-      if (bit) {
-        te_dequant(X, qp, s2);
-        te_inv_tx(X, s2);
-      }
+      const int bit = te_quant_chain(X, qp, s2, type, coef + t * ts);
+      if (bit) te_inv_tx(X, s2);
       te_recon(rec + i * size + j, size, pb + i * size + j, size, X, s2, bit);
       cbp = (cbp << 1) + bit;
     }
@@ -324,13 +319,8 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, in
   const int fast = (size == 64 && F.speed > 0) || F.speed > 1;
   te_residual_tx(X, org, os, pb, size, size, fast);
   te_fwd_tx(X, size, fast);
-  cbp = te_quant(X, qp, size, type);
-  const int q = TE_MIN(size, 16);
-  for (int e = TE_LANE; e < q * q; e += TE_NL) coef[e] = (int16_t)X.C[e];
-  if (cbp) {
-    te_dequant(X, qp, size);
-    te_inv_tx(X, size);
-  }
+  cbp = te_quant_chain(X, qp, size, type, coef);
+  if (cbp) te_inv_tx(X, size);
   te_recon(rec, size, pb, size, X, size, cbp);
   return cbp;
 }
@@ -347,7 +337,7 @@ TE_FN int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const
   TeTx &X = *S.tx;
   const int fast = F.speed > 1;
   if (tb_split) {
-    const int s2 = size / 2, q = TE_MIN(s2, 16);
+    const int s2 = size / 2;
     int cbp = 0;
     for (int t = 0; t < 4; t++) {
       const int i = (t >> 1) * s2, j = (t & 1) * s2;
@@ -355,12 +345,8 @@ TE_FN int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const
       te_intra_pred(*S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
       te_residual_tx(X, org + i * os + j, os, pb, s2, s2, fast);
       te_fwd_tx(X, s2, fast);
-      const int bit = te_quant(X, qp, s2, type);
-      for (int e = TE_LANE; e < q * q; e += TE_NL) coef[t * ts + e] = (int16_t)X.C[e];
-      if (bit) {
-        te_dequant(X, qp, s2);
-        te_inv_tx(X, s2);
-      }
+      const int bit = te_quant_chain(X, qp, s2, type, coef + t * ts);
+      if (bit) te_inv_tx(X, s2);
       te_recon(rec + i * size + j, size, pb, s2, X, s2, bit);
       cbp = (cbp << 1) + bit;
     }
@@ -370,13 +356,8 @@ TE_FN int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const
   te_intra_pred(*S.nb, ypos, xpos, size, pb, mode, 0);
   te_residual_tx(X, org, os, pb, size, size, fast);
   te_fwd_tx(X, size, fast);
-  const int cbp = te_quant(X, qp, size, type);
-  const int q = TE_MIN(size, 16);
-  for (int e = TE_LANE; e < q * q; e += TE_NL) coef[e] = (int16_t)X.C[e];
-  if (cbp) {
-    te_dequant(X, qp, size);
-    te_inv_tx(X, size);
-  }
+  const int cbp = te_quant_chain(X, qp, size, type, coef);
+  if (cbp) te_inv_tx(X, size);
   te_recon(rec, size, pb, size, X, size, cbp);
   return cbp;
 }
