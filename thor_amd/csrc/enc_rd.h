@@ -554,8 +554,140 @@ TE_CONST int8_t te_hex_dy[6] = {1, 2, 1, -1, -2, -1}, te_hex_dx[6] = {-1, 0, 1, 
 TE_CONST int8_t te_hp_m[9] = {0, 0, -2, 2, 0, -2, -2, 2, 2}, te_hp_n[9] = {0, -2, 0, 0, 2, -2, 2, -2, 2};  // :942-943
 TE_CONST int8_t te_qp_m[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, te_qp_n[9] = {0, -1, 0, 0, 1, -1, 1, -1, 1};
 
+#if !defined(TE_HOST)
+// The search's predictions without a prediction buffer: pixel (i, j) of
+// `mode` straight from the neighbour arrays (the same formulas as
+// te_intra_pred, enc_pix.h).  lF / tF hold the 2n-long 1-2-1 filtered edges
+// (what the up-right and down-left-left modes read); the n-long filter of the
+// up-left modes differs from them only at index n - 1 (lFe / tFe).  T / L:
+// the planar edge sums.
+struct TeIpc {
+  int dc, TL, tlF, tFe, lFe;
+};
+TE_FN int te_ipx(const TeNbr &nb, const TeIpc &c, int n, int mode, int i, int j) {
+  switch (mode) {
+    case TE_PLANAR:
+      return te_clip255((nb.L[i] + nb.T[j] - c.TL + 4) / 8);
+    case TE_HOR:
+      return nb.left[i];
+    case TE_VER:
+      return nb.top[j];
+    case TE_UPLEFT: {
+      const int d = i - j;
+      if (d > 0) return d - 1 == n - 1 ? c.lFe : nb.lF[d - 1];
+      return d == 0 ? c.tlF : (-d - 1 == n - 1 ? c.tFe : nb.tF[-d - 1]);
+    }
+    case TE_UPUPLEFT: {
+      const int d = i - 2 * j;
+      if (d > 1) return d - 2 == n - 1 ? c.lFe : nb.lF[d - 2];
+      if (d == 1) return c.tlF;
+      const int t0 = nb.tF[0];
+      if (d == 0) return (c.tlF + t0) >> 1;
+      const int h = (-d) / 2, th = h == n - 1 ? c.tFe : nb.tF[h];
+      if (d & 1) return th;
+      return (th + (h - 1 == n - 1 ? c.tFe : nb.tF[h - 1])) >> 1;
+    }
+    case TE_UPLEFTLEFT: {
+      const int d = 2 * i - j;
+      if (d < -1) return -d - 2 == n - 1 ? c.tFe : nb.tF[-d - 2];
+      if (d == -1) return c.tlF;
+      const int l0 = nb.lF[0];
+      if (d == 0) return (c.tlF + l0) >> 1;
+      const int h = d / 2, lh = h == n - 1 ? c.lFe : nb.lF[h];
+      if (d & 1) return lh;
+      return (lh + (h - 1 == n - 1 ? c.lFe : nb.lF[h - 1])) >> 1;
+    }
+    case TE_UPRIGHT:
+      return nb.tF[i + j + 1];
+    case TE_UPUPRIGHT: {
+      const int d = i + 2 * j;
+      return (d & 1) ? (int)nb.tF[(d + 1) / 2] : (nb.tF[d / 2] + nb.tF[d / 2 + 1]) >> 1;
+    }
+    case TE_DOWNLEFTLEFT: {
+      const int d = 2 * i + j;
+      return (d & 1) ? (int)nb.lF[(d + 1) / 2] : (nb.lF[d / 2] + nb.lF[d / 2 + 1]) >> 1;
+    }
+    default:  // DC (the search's: (left, top) always)
+      return c.dc;
+  }
+}
+TE_FN uint32_t te_ipx4(const TeNbr &nb, const TeIpc &c, int n, int mode, int i, int j) {
+  return te_pack4(te_ipx(nb, c, n, mode, i, j), te_ipx(nb, c, n, mode, i, j + 1), te_ipx(nb, c, n, mode, i, j + 2),
+                  te_ipx(nb, c, n, mode, i, j + 3));
+}
+// the arrays and constants te_ipx reads, for the n x n block whose edges are in nb
+TE_FN TeIpc te_ipx_setup(TeNbr &nb, int n) {
+  for (int k = TE_LANE; k < 2 * n; k += TE_NL) {
+    // 1-2-1 filters of both edges over 2n (filter_121, common/intra_prediction.c:39-48)
+    const int e = k == 2 * n - 1;
+    nb.tF[k] = (uint8_t)(k == 0 ? (3 * nb.top[0] + nb.top[1] + 2) >> 2
+                                : (e ? (nb.top[k - 1] + 3 * nb.top[k] + 2) >> 2
+                                     : (nb.top[k - 1] + 2 * nb.top[k] + nb.top[k + 1] + 2) >> 2));
+    nb.lF[k] = (uint8_t)(k == 0 ? (3 * nb.left[0] + nb.left[1] + 2) >> 2
+                                : (e ? (nb.left[k - 1] + 3 * nb.left[k] + 2) >> 2
+                                     : (nb.left[k - 1] + 2 * nb.left[k] + nb.left[k + 1] + 2) >> 2));
+    // planar edge sums (:182-214)
+    const int s = k >= n, jj = k - s * n;
+    const uint8_t *a = s ? nb.left : nb.top;
+    int v;
+    if (jj == 0) v = 3 * a[0] + 2 * a[0] + 2 * a[1] + a[2];
+    else if (jj == 1) v = a[0] + 2 * a[0] + 2 * a[1] + 2 * a[2] + a[3];
+    else if (jj == n - 2) v = a[n - 4] + 2 * a[n - 3] + 2 * a[n - 2] + 2 * a[n - 1] + a[n - 1];
+    else if (jj == n - 1) v = a[n - 3] + 2 * a[n - 2] + 2 * a[n - 1] + 3 * a[n - 1];
+    else v = a[jj - 2] + 2 * a[jj - 1] + 2 * a[jj] + 2 * a[jj + 1] + a[jj + 2];
+    (s ? nb.L : nb.T)[jj] = v;
+  }
+  uint32_t sum = 0;
+  for (int k = TE_LANE; k < n; k += TE_NL) sum += nb.left[k] + nb.top[k];
+  sum = te_sum(sum);
+  TeIpc c;
+  c.dc = ((int)sum + n) / (2 * n);
+  c.TL = nb.left[1] + 2 * nb.left[0] + 2 * nb.tl + 2 * nb.top[0] + nb.top[1];
+  c.tlF = (2 * nb.tl + nb.left[0] + nb.top[0] + 2) >> 2;
+  c.tFe = (nb.top[n - 2] + 3 * nb.top[n - 1] + 2) >> 2;
+  c.lFe = (nb.left[n - 2] + 3 * nb.left[n - 1] + 2) >> 2;
+  te_sync();
+  return c;
+}
+#endif
+
+#if !defined(TE_HOST)
+// blocks of 16 x 16 and up: T 4-pixel chunks per lane, the original in registers, one mode after the other
+template <int T>
+TE_FN void te_isearch(const TeNbr &nb, const TeIpc &c, const uint8_t *o, int os, int size, const int8_t *order, int n,
+                      int &min_sad, int &best) {
+  const int w4 = size >> 2;
+  uint32_t org[T];
+  int ci[T], cj[T];
+#pragma unroll
+  for (int t = 0; t < T; t++) {
+    const int g = TE_LANE + 64 * t;
+    ci[t] = te_dv(g, w4);
+    cj[t] = (g - ci[t] * w4) * 4;
+    org[t] = te_ld4(o + ci[t] * os + cj[t]);
+  }
+#pragma unroll 1
+  for (int k = 0; k < n; k++) {
+    const int mode = order[k];
+    uint32_t a = 0;
+#pragma unroll
+    for (int t = 0; t < T; t++) a = te_sad4(org[t], te_ipx4(nb, c, size, mode, ci[t], cj[t]), a);
+    const int sad = (int)te_sum(a);
+    if (sad < min_sad) {
+      best = mode;
+      min_sad = sad;
+    }
+  }
+}
+#endif
+
 // search_intra_prediction_params, enc/encode_block.c:1230-1329: SAD over the
 // first `num_modes` modes in the order DC, HOR, VER, PLANAR, [UPLEFT ...].
+// Device: every mode's prediction computed in registers against the original
+// (no prediction buffer, no barrier per mode) -- 8x8: four modes at a time,
+// one per 16-lane row (a row's sum is one DPP reduction); larger blocks: the
+// modes one after the other over the whole wave, their sums reduced together.
+// The first strictly smaller SAD wins, in the search order, as the reference.
 TE_NOINL int te_search_intra(const TeFrame &F_, const TeBlockInfo &bi_, int num_modes, int *mode_out) {
   const TeFrame &F = *te_lds(&F_);
   const TeScratch S = te_here();
@@ -569,38 +701,70 @@ TE_NOINL int te_search_intra(const TeFrame &F_, const TeBlockInfo &bi_, int num_
   const int n = num_modes == 4 ? 4 : 10;
   const uint8_t *o = F.oy + ypos * F.osy + xpos;
 #if !defined(TE_HOST)
-  // the original block in registers once (4-pixel chunks, up to 16 per lane), each
-  // mode's SAD against the compact prediction in LDS
-  const int w4 = size >> 2, n4 = w4 * size;
-  uint32_t org[16];
+  const TeNbr &nb = *S.nb;
+  const TeIpc c = te_ipx_setup(*S.nb, size);
+  if (size == 8) {
+    const int ch = TE_LANE & 15, row = TE_LANE >> 4, i = ch >> 1, j = (ch & 1) * 4;
+    const uint32_t org = te_ld4(o + i * F.osy + j);
 #pragma unroll
-  for (int t = 0; t < 16; t++) {
-    const int g = TE_LANE + 64 * t;
-    org[t] = 0;
-    if (g < n4) {
-      const int i = te_dv(g, w4), j = (g - i * w4) * 4;
-      org[t] = te_ld4(o + i * F.osy + j);
+    for (int pass = 0; pass < 3; pass++) {
+      if (4 * pass >= n) break;
+      const int k = 4 * pass + row;
+      uint32_t a = 0;
+      if (k < n) a = te_sad4(org, te_ipx4(nb, c, 8, order[k], i, j), 0);
+      a += (uint32_t)TE_DPP(a, 0xB1);
+      a += (uint32_t)TE_DPP(a, 0x4E);
+      a += (uint32_t)TE_DPP(a, 0x141);
+      a += (uint32_t)TE_DPP(a, 0x140);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int kk = 4 * pass + r;
+        const int sad = __builtin_amdgcn_readlane((int)a, 16 * r);
+        if (kk < n && sad < min_sad) {
+          best = order[kk];
+          min_sad = sad;
+        }
+      }
     }
-  }
-#endif
-  for (int k = 0; k < n; k++) {
-    te_intra_pred(*S.nb, ypos, xpos, size, S.pb, order[k], 1);
-#if !defined(TE_HOST)
-    uint32_t a = 0;
+  } else if (size == 16) {
+    te_isearch<1>(nb, c, o, F.osy, size, order, n, min_sad, best);
+  } else {  // 32, 64: few calls, many chunks per lane -- the prediction buffer keeps the code small
+    const int w4 = size >> 2, n4 = w4 * size;
+    uint32_t org[16];
 #pragma unroll
     for (int t = 0; t < 16; t++) {
       const int g = TE_LANE + 64 * t;
-      if (g < n4) a = te_sad4(org[t], te_ld4(S.pb + 4 * g), a);
+      org[t] = 0;
+      if (g < n4) {
+        const int i = te_dv(g, w4), j = (g - i * w4) * 4;
+        org[t] = te_ld4(o + i * F.osy + j);
+      }
     }
-    const int sad = (int)te_sum(a);
+    for (int k = 0; k < n; k++) {
+      te_intra_pred(*S.nb, ypos, xpos, size, S.pb, order[k], 1);
+      uint32_t a = 0;
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const int g = TE_LANE + 64 * t;
+        if (g < n4) a = te_sad4(org[t], te_ld4(S.pb + 4 * g), a);
+      }
+      const int sad = (int)te_sum(a);
+      if (sad < min_sad) {
+        best = order[k];
+        min_sad = sad;
+      }
+    }
+  }
 #else
+  for (int k = 0; k < n; k++) {
+    te_intra_pred(*S.nb, ypos, xpos, size, S.pb, order[k], 1);
     const int sad = (int)te_sad(o, F.osy, S.pb, size, size, size);
-#endif
     if (sad < min_sad) {
       best = order[k];
       min_sad = sad;
     }
   }
+#endif
   *mode_out = best;
   return min_sad;
 }

@@ -1,0 +1,15 @@
+# Round 5w: the intra mode search without a prediction buffer (8x8: four modes at once, one per 16-lane row; 16x16: per mode over the wave) -- encoder parity, A/B vs the previous commit (PRES), cycle profile
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+OUT=gpurun_out/r05w
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_encoder_rd.py tests/test_gpu_encoder.py -k "not hdb16 and not hierarchical" > $OUT/pytest_enc.log 2>&1 || { echo PYTEST_ENC_FAIL; tail -30 $OUT/pytest_enc.log; exit 1; }
+tail -1 $OUT/pytest_enc.log
+for V in PRES A PRES A; do
+  if [ $V = A ]; then LIBP=thor_amd/libthor_amd.so; else LIBP=var/lib_$V.so; fi
+  THOR_AMD_LIB=$LIBP timeout -k 10 170 python3 tools/enc_speed.py --name k4_low --batch 240 --frames 4 > $OUT/enc_$V.txt 2>&1 || { tail -20 $OUT/enc_$V.txt; exit 1; }
+  echo "$V $(tail -1 $OUT/enc_$V.txt)"
+done
+timeout -k 10 300 python3 tools/enc_profile.py --name k4_low --frames 8 --limit 3 --batch 1 > $OUT/prof1.txt 2>&1 || { tail -20 $OUT/prof1.txt; exit 1; }
+head -16 $OUT/prof1.txt
