@@ -3,11 +3,11 @@
 //
 // Per frame (and per batch of up to THOR_ENC_MAX_BATCH streams, one launch
 // per stage for all of them):
-//   k_enc_rows      WPP superblock rows: one wave64 per SB row (tickets handed
-//                   out in order, so a row only ever waits on rows held by
-//                   running waves); SB (k, l) starts when SB (k-1, l+1) is
-//                   done (the up-right neighbour is the furthest one the RD
-//                   loop reads, enc/encode_block.c:2819-2879).  The RD loop of
+//   k_enc_rows      the RD loop: persistent wave64 workers take the batch's
+//                   superblocks from one queue in readiness order; SB (k, l) is
+//                   queued when SB (k, l-1) and SB (k-1, l+1) are done (the
+//                   up-right neighbour is the furthest one the RD loop reads,
+//                   enc/encode_block.c:2819-2879).  The RD loop of
 //                   the SB (enc_rd.h) writes the reconstruction into the ring
 //                   slot, the 4x4 side info and the SB's bit string.
 //   k_enc_cellinfo  side info -> the decoder's 16-bit cell words
@@ -40,7 +40,8 @@ struct TeJob {
   TeFrame F;
   uint32_t *sb_words;   // [nsb][THOR_ENC_SB_WORDS]
   int *sb_nbits;        // [nsb]
-  unsigned *progress;   // [nsbv] SBs finished per row
+  unsigned *deps;       // [nsb] finished dependencies per SB (left, up-right), k_enc_rows' scheduler
+  int qbase;            // this job's range of the scheduler queue k_enc_clear marks empty
   int8_t *clpf_bits;    // [nsb_full]: -1 no bit, else the flag
   uint8_t *clpf_flags;  // [nsb_full]: CLPF applied (k_clpf input)
   uint16_t *cellinfo;
@@ -58,8 +59,20 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// WPP worker: grid of persistent single-wave workgroups; ticket t -> stream
-// t % n, SB row t / n.
+// Superblock scheduler.  An SB (k, l) may be coded once its left neighbour
+// (k, l - 1) and its up-right one (k - 1, min(l + 1, nsbh - 1)) are done -- the
+// WPP order of the reference's neighbour reads (enc/encode_block.c:2819-2879).
+// Workers are persistent single-wave workgroups that take the batch's SBs from
+// one queue in readiness order: the worker that completes an SB counts it
+// into its dependants' counters (`deps`) and queues each one it completes.
+// A worker that took slot h waits until slot h is filled; every SB is queued
+// exactly once, so every slot below the batch's SB count fills (the slots a
+// waiting worker holds are past every queued SB, and a queued SB is always
+// held by a running worker).  Unlike one worker per SB row, a worker never
+// idles while its row waits for the row above: it codes whatever SB of any
+// stream is ready.  No state travels between a worker's SBs (the SB's syntax
+// state is reset per SB, te_encode_sb; neighbours come from the cells and the
+// reconstruction in global memory).
 // Two workers per SIMD: the RD loop is a latency-bound chain of small
 // dependent steps (LDS round trips, VALU -> SALU hand-offs), so a second wave
 // hides part of it -- 15 % off the 4K I frame at 240 streams.
@@ -69,9 +82,24 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 #define THOR_ENC_WPE 2
 #endif
 #define TE_WPE __attribute__((amdgpu_waves_per_eu(THOR_ENC_WPE)))
-__global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, int n, unsigned *ticket, int nrows,
-                                                 TeScratchMem *scratch, unsigned *err, unsigned long long spin_limit,
-                                                 int stall_row) {
+#define TE_Q_EMPTY 0xffffffffu
+__device__ __forceinline__ unsigned te_q_item(int s, int k, int l) { return (unsigned)s << 16 | (unsigned)k << 8 | (unsigned)l; }
+// (lane 0) one more finished dependency of SB (k, l) of job s; queue it when that was its last.
+// Relaxed atomics: the worker's release fence after its SB already wrote its
+// results back to device scope (every dependency's did, before its count), and
+// the worker that takes the SB acquires once -- an acquire / release per
+// atomic here would write back and invalidate the XCD's L2 several times per SB.
+__device__ __forceinline__ void te_dep_done(const TeJob &J, int s, int k, int l, unsigned *q, unsigned *items) {
+  const unsigned need = (unsigned)((l > 0) + (k > 0));
+  const unsigned old = __hip_atomic_fetch_add(&J.deps[k * J.nsbh + l], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 == need) {
+    const unsigned slot = __hip_atomic_fetch_add(&q[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&items[slot], te_q_item(s, k, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, unsigned total, unsigned *q,
+                                                 unsigned *items, TeScratchMem *scratch, unsigned *err,
+                                                 unsigned long long spin_limit, int stall_row) {
   __shared__ TeFrame s_F;  // the job's frame parameters, read all through the RD loop
   __shared__ TeSB s_sb;    // the superblock's bit writer and ME candidate lists
   // the worker's buffers (te_here): LDS at fixed addresses (g_te_*), global at
@@ -81,71 +109,90 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   te_load_zig();
   TeSB &sb = s_sb;
   const int lane = threadIdx.x;
-  bool dead = false;  // a wait of this wave gave up (reported): it waits no more, so the grid drains
+  int cur = -1;  // the job whose frame parameters s_F holds
   for (;;) {
-    unsigned t = 0;
-    if (lane == 0) t = atomicAdd(ticket, 1u);
-    t = __builtin_amdgcn_readfirstlane(t);
-    if ((int)t >= n * nrows) break;
-    const int s = (int)t % n, k = (int)t / n;
-    const TeJob &J = jobs[s];
-    if (k >= J.nsbv) continue;
-    {  // the job's frame parameters into LDS
-      const uint32_t *src = (const uint32_t *)&J.F;
-      uint32_t *dst = (uint32_t *)&s_F;
-      for (int e = lane; e < (int)(sizeof(TeFrame) / 4); e += 64) dst[e] = src[e];
-      te_sync();
-    }
-    unsigned seen = 0;  // progress of the row above observed (and acquired) so far
-    for (int l = 0; l < J.nsbh; l++) {
-      const unsigned need = (unsigned)(l + 2 < J.nsbh ? l + 2 : J.nsbh);
-      if (k > 0 && need > seen && !dead) {  // SB (k-1, l+1) (or the whole row above) must be done
-        TE_P(TP_WAIT);
-        unsigned v = 0, gave_up = 0;
-        if (lane == 0) {
-          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-          while ((v = te_ld_relaxed(&J.progress[k - 1])) < need) {
-            __builtin_amdgcn_s_sleep(8);
-            // a wedged dependency (spin_limit, 5 minutes by default): give up, reported; never hang the GPU
-            if (__builtin_amdgcn_s_memrealtime() - t0 > spin_limit) {
-              atomicOr(err, 1u);
-              gave_up = 1;
-              break;
-            }
+    unsigned h = 0;
+    if (lane == 0) h = __hip_atomic_fetch_add(&q[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h = __builtin_amdgcn_readfirstlane(h);
+    if (h >= total) break;
+    unsigned item = 0, gave_up = 0;
+    {
+      TE_P(TP_WAIT);
+      if (lane == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        while ((item = te_ld_relaxed(&items[h])) == TE_Q_EMPTY) {
+          __builtin_amdgcn_s_sleep(4);
+          // a wedged dependency (spin_limit, 5 minutes by default): give up, reported; never hang the GPU
+          if (__builtin_amdgcn_s_memrealtime() - t0 > spin_limit) {
+            atomicOr(err, 1u);
+            gave_up = 1;
+            break;
           }
         }
-        if (__builtin_amdgcn_readfirstlane(gave_up)) dead = true;
-        seen = __builtin_amdgcn_readfirstlane(v);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
-      const int sbi = k * J.nsbh + l;
-      sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
-      sb.bits.cap = THOR_ENC_SB_WORDS * 32;
-      te_encode_sb(s_F, sb, k, l);
-      if (lane == 0) {
-        J.sb_nbits[sbi] = sb.bits.pos;
-        if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
+    }
+    if (__builtin_amdgcn_readfirstlane(gave_up)) break;  // this wave waits no more, so the grid drains
+    item = __builtin_amdgcn_readfirstlane(item);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int s = (int)(item >> 16), k = (int)((item >> 8) & 255), l = (int)(item & 255);
+    const TeJob &J = jobs[s];
+    if (s != cur) {  // the job's frame parameters into LDS
+      const uint32_t *src = (const uint32_t *)&J.F;
+      uint32_t *dst = (uint32_t *)&s_F;
+      te_sync();
+      for (int e = lane; e < (int)(sizeof(TeFrame) / 4); e += 64) dst[e] = src[e];
+      te_sync();
+      cur = s;
+    }
+    const int sbi = k * J.nsbh + l;
+    sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
+    sb.bits.cap = THOR_ENC_SB_WORDS * 32;
+    te_encode_sb(s_F, sb, k, l);
+    if (lane == 0) {
+      J.sb_nbits[sbi] = sb.bits.pos;
+      if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      // dependants: (k, l + 1) by its left neighbour; (k + 1, l - 1) by its up-right one, and
+      // (k + 1, l) too at the row end (its up-right is clipped to this SB).  stall_row: a
+      // diagnostics hook (thor_enc_debug_stall) -- that row never releases the row below
+      if (l + 1 < J.nsbh) te_dep_done(J, s, k, l + 1, q, items);
+      if (k + 1 < J.nsbv && k != stall_row) {
+        if (l >= 1) te_dep_done(J, s, k + 1, l - 1, q, items);
+        if (l == J.nsbh - 1) te_dep_done(J, s, k + 1, l, q, items);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0 && k != stall_row)  // stall_row: a diagnostics hook (thor_enc_debug_stall), -1 normally
-        __hip_atomic_store(&J.progress[k], (unsigned)(l + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
 // Every context's cell state (deblock_data, cleared per frame: enc/encode_frame.c:74)
-// and WPP progress words to zero, one launch for the batch (grid y = context),
-// 16-byte stores.
-__global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ jobs, long long cell_bytes) {
-  const TeJob &J = jobs[blockIdx.y];
+// and SB dependency counters to zero, one launch for the batch (grid y =
+// context), 16-byte stores; the scheduler queue: each job's SB (0, 0) in slot
+// s, the job's other SBs' slots empty, head 0, tail n.
+__global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ jobs, long long cell_bytes, unsigned *q,
+                                                   unsigned *items) {
+  const int s = blockIdx.y;
+  const TeJob &J = jobs[s];
   uint4 *c = (uint4 *)J.F.cells;
   const long long n16 = cell_bytes >> 4;
+  const int nsb = J.nsbv * J.nsbh;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256)
     c[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (blockIdx.x == 0)
-    for (int i = threadIdx.x; i < J.nsbv; i += 256) J.progress[i] = 0u;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nsb; i += gridDim.x * 256) {
+    J.deps[i] = 0u;
+    J.sb_nbits[i] = 0;  // an SB a failed launch never codes packs as nothing
+  }
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nsb - 1; i += gridDim.x * 256) items[J.qbase + i] = TE_Q_EMPTY;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    items[s] = te_q_item(s, 0, 0);
+    if (s == 0) {
+      q[0] = 0u;
+      q[1] = gridDim.y;
+    }
+  }
 }
 
 // TeCell (deblock_data_t) -> the 16-bit cell words the decoder's loop filter
@@ -192,6 +239,12 @@ __device__ __forceinline__ void te_or_bits(uint32_t *dst, long long pos, const u
     if (sh && (w << (32 - sh))) atomicOr(&dst[(p >> 5) + 1], w << (32 - sh));
   }
 }
+// An SB's bit count as packed: within its word buffer (a count past it is an
+// error the launch already flagged; packing stays inside the buffers).
+__device__ __forceinline__ int te_sb_bits(const TeJob &J, int i) {
+  const int b = J.sb_nbits[i];
+  return b < 0 ? 0 : (b > THOR_ENC_SB_WORDS * 32 ? THOR_ENC_SB_WORDS * 32 : b);
+}
 __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs, long long *scan_tmp, int out_cap_words) {
   const TeJob &J = jobs[blockIdx.x];
   const int nsb = J.nsbh * J.nsbv;
@@ -201,7 +254,7 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
     long long o = J.hdr_bits;
     for (int i = 0; i < nsb; i++) {
       off[i] = o;
-      o += J.sb_nbits[i];
+      o += te_sb_bits(J, i);
     }
     off[nsb] = o;
     if (J.clpf) {
@@ -221,7 +274,7 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
   __syncthreads();
   if (threadIdx.x == 0) te_or_bits(J.out_words, 0, J.hdr_words, J.hdr_bits);
   for (int i = threadIdx.x; i < nsb; i += 256)
-    te_or_bits(J.out_words, off[i], J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, J.sb_nbits[i]);
+    te_or_bits(J.out_words, off[i], J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, te_sb_bits(J, i));
   if (threadIdx.x == 0 && J.clpf) {
     long long p = off[nsb];
     const uint32_t two = 0x80000000u;  // bits 1, 0
@@ -275,7 +328,7 @@ struct thor_enc {
   uint16_t *cellinfo;
   uint32_t *sb_words;
   int *sb_nbits;
-  unsigned *progress;
+  unsigned *deps;
   int8_t *clpf_bits;
   uint8_t *clpf_flags;
   int *es_thr;
@@ -311,7 +364,7 @@ static int enc_alloc(thor_enc *e) {
   if (!dev_alloc(&e->cellinfo, ncell * sizeof(uint16_t), "thor_enc_create: cell side info")) return g_create_err.code;
   if (!dev_alloc(&e->sb_words, (size_t)e->nsb * THOR_ENC_SB_WORDS * 4, "thor_enc_create: SB bit strings")) return g_create_err.code;
   if (!dev_alloc(&e->sb_nbits, (size_t)e->nsb * sizeof(int), "thor_enc_create: SB bit counts")) return g_create_err.code;
-  if (!dev_alloc(&e->progress, (size_t)e->nsbv * sizeof(unsigned), "thor_enc_create: WPP progress")) return g_create_err.code;
+  if (!dev_alloc(&e->deps, (size_t)e->nsb * sizeof(unsigned), "thor_enc_create: SB dependency counters")) return g_create_err.code;
   if (!dev_alloc(&e->clpf_bits, (size_t)e->nsb_full + 1, "thor_enc_create: CLPF bits")) return g_create_err.code;
   if (!dev_alloc(&e->clpf_flags, (size_t)e->nsb_full + 1, "thor_enc_create: CLPF flags")) return g_create_err.code;
   if (!dev_alloc(&e->es_thr, 2 * 52 * 4 * sizeof(int), "thor_enc_create: early-skip thresholds")) return g_create_err.code;
@@ -334,7 +387,9 @@ struct EncPool {
   std::mutex mu;
   size_t nwork = 0;
   TeScratchMem *scratch = nullptr;
-  unsigned *ticket = nullptr, *err = nullptr;
+  unsigned *ticket = nullptr, *err = nullptr;  // ticket: the SB scheduler queue's head and tail
+  unsigned *qitems = nullptr;                  // the queue's slots, one per SB of the batch
+  size_t qcap = 0;
   TeJob *jobs = nullptr;
   long long *scan = nullptr;
   size_t scan_n = 0;
@@ -386,7 +441,7 @@ static EncPool &pool_for(int device) {
 }
 
 // (the caller holds P.mu and has made P's device current)
-static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n) {
+static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n, size_t nsb_total) {
   if (!P.ticket) {
     EHIP(hipMalloc(&P.ticket, 64));
     EHIP(hipMalloc(&P.err, 64));
@@ -403,6 +458,13 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n) {
     P.nwork = 0;
     EHIP(hipMalloc(&P.scratch, nwork * sizeof(TeScratchMem)));
     P.nwork = nwork;
+  }
+  if (nsb_total > P.qcap) {
+    if (P.qitems) (void)hipFree(P.qitems);
+    P.qitems = nullptr;
+    P.qcap = 0;
+    EHIP(hipMalloc(&P.qitems, nsb_total * sizeof(unsigned)));
+    P.qcap = nsb_total;
   }
   if (scan_n > P.scan_n) {
     if (P.scan) (void)hipFree(P.scan);
@@ -468,7 +530,7 @@ void thor_enc_destroy(thor_enc_t *e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->progress,
+  void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->deps,
                   e->clpf_bits, e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_words2, e->out_bits};
   {  // a batch still pending with this context (begun, never ended) is dropped
     EncPool &P = pool_for(e->device);
@@ -594,7 +656,7 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   F.es_thr = e->es_thr;
   J.sb_words = e->sb_words;
   J.sb_nbits = e->sb_nbits;
-  J.progress = e->progress;
+  J.deps = e->deps;
   J.clpf_bits = e->clpf_bits;
   J.clpf_flags = e->clpf_flags;
   J.cellinfo = e->cellinfo;
@@ -680,7 +742,8 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
     for (thor_enc *x : q.es)
       for (int i = 0; i < n; i++)
         if (x == es[i] && q.st != lead->stream) return THOR_ERR_ARG;  // a context's frames stay on one batch stream
-  int rc = pool_reserve(P, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS), (size_t)n * (lead->nsb + 1));
+  int rc = pool_reserve(P, (size_t)(nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS), (size_t)n * (lead->nsb + 1),
+                        (size_t)n * lead->nsb);
   if (rc != THOR_OK) return rc;
   hipStream_t st = lead->stream;
   // the pool's workers and scratch are shared: a batch on another stream first waits for the pending ones
@@ -714,22 +777,21 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
         EHIP(hipStreamSynchronize(es[i]->stream));
         if ((rc = thor_ti_status(es[i]->ti)) != THOR_OK) return rc;
       }
+  for (int i = 0; i < n; i++) jobs[i].qbase = n + i * (lead->nsb - 1);  // slots [n, n * nsb): empty
   EHIP(hipMemcpyAsync(P.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
-  EHIP(hipMemsetAsync(P.ticket, 0, 4, st));
   {
     const long long cb = (long long)(W / 4) * (H / 4) * (long long)sizeof(TeCell);
     static_assert(sizeof(TeCell) % 4 == 0, "cells clear as words");
     const long long n16 = (cb + 15) / 16;
     const int gx = (int)((n16 + 255) / 256 < 1024 ? (n16 + 255) / 256 : 1024);
-    k_enc_clear<<<dim3(gx > 0 ? gx : 1, n), 256, 0, st>>>(P.jobs, ((cb + 15) / 16) * 16);
+    k_enc_clear<<<dim3(gx > 0 ? gx : 1, n), 256, 0, st>>>(P.jobs, ((cb + 15) / 16) * 16, P.ticket, P.qitems);
     EHIP(hipGetLastError());
   }
-  // persistent workers take row tickets until none are left: more workgroups
-  // than the chip holds at once (two per SIMD at this kernel's register and LDS
-  // use) would only start as the first ones run out of work
-  k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(P.jobs, n, P.ticket, nrows,
-                                                                         P.scratch, P.err, g_spin_limit.load(),
-                                                                         g_stall_row.load());
+  // persistent workers take SBs from the queue until every slot is taken:
+  // more workgroups than the chip holds at once (two per SIMD at this kernel's
+  // register and LDS use) would only start as the first ones run out of work
+  k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(
+      P.jobs, (unsigned)(n * lead->nsb), P.ticket, P.qitems, P.scratch, P.err, g_spin_limit.load(), g_stall_row.load());
   EHIP(hipGetLastError());
   const int ncell = (W / 4) * (H / 4);
   k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(P.jobs);
