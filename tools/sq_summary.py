@@ -17,6 +17,16 @@ for d in dirs:
     for disp, cs in by.items():
         for cn, v in cs.items():
             res.setdefault(cn, []).append(v)
-json.dump({"kernel": kern, "counters": {k: sum(v) for k, v in res.items()}, "dispatches": {k: len(v) for k, v in res.items()}},
-          open(out, "w"), indent=1)
+per = {}  # counter -> values in dispatch order (e.g. an I-frame batch, then a P-frame batch)
+for d in dirs:
+    c = sqlite3.connect(d + "/run_results.db")
+    rows = sorted(c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection"))
+    acc = defaultdict(lambda: defaultdict(float))
+    for disp, n, cn, v in rows:
+        if n.split("(")[0] == kern:
+            acc[cn][disp] += float(v)
+    for cn, byd in acc.items():
+        per[cn] = [byd[k] for k in sorted(byd)]
+json.dump({"kernel": kern, "counters": {k: sum(v) for k, v in res.items()}, "dispatches": {k: len(v) for k, v in res.items()},
+           "per_dispatch": per}, open(out, "w"), indent=1)
 print(json.dumps({k: "%.4g" % sum(v) for k, v in sorted(res.items())}))
