@@ -325,235 +325,6 @@ TE_NOINL int te_enc_inter_comp(const TeFrame &F_, const uint8_t *org, int os, in
   return cbp;
 }
 
-// encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
-// component.  rf / fs: the frame being reconstructed at the CU origin.
-TE_FN int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs,
-                               int ypos, int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
-                               int tb_split, int mode, int ur, int dl, int ts) {
-  const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_here();
-  uint8_t *pb = te_lds(pb_);
-  TE_P(TP_INTRA_COMP);
-  TeTx &X = *S.tx;
-  const int fast = F.speed > 1;
-  if (tb_split) {
-    const int s2 = size / 2;
-    int cbp = 0;
-    for (int t = 0; t < 4; t++) {
-      const int i = (t >> 1) * s2, j = (t & 1) * s2;
-      te_make_top_and_left(*S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
-      te_intra_pred(*S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
-      te_residual_tx(X, org + i * os + j, os, pb, s2, s2, fast);
-      te_fwd_tx(X, s2, fast);
-      const int bit = te_quant_chain(X, qp, s2, type, coef + t * ts);
-      if (bit) te_inv_tx(X, s2);
-      te_recon(rec + i * size + j, size, pb, s2, X, s2, bit);
-      cbp = (cbp << 1) + bit;
-    }
-    return cbp;
-  }
-  te_make_top_and_left(*S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
-  te_intra_pred(*S.nb, ypos, xpos, size, pb, mode, 0);
-  te_residual_tx(X, org, os, pb, size, size, fast);
-  te_fwd_tx(X, size, fast);
-  const int cbp = te_quant_chain(X, qp, size, type, coef);
-  if (cbp) te_inv_tx(X, size);
-  te_recon(rec, size, pb, size, X, size, cbp);
-  return cbp;
-}
-
-// The candidate just written (its nbits end at b.pos) became the best: keep
-// its syntax bits, so that the final encode of the block (re-use, the same
-// parameters and contexts) copies them instead of running write_block again.
-TE_FN void te_keep_best_bits(TeBits &b, TeBlockInfo &bi, int nbits) {
-  if (nbits > bi.best_cap * 32 || b.pos > b.cap) {
-    bi.best_nbits = -1;
-    return;
-  }
-  if ((b.pos & 31) && TE_LANE == 0) b.w[b.pos >> 5] = b.cur;  // the register word (stored again when complete)
-  te_sync();
-  const int start = b.pos - nbits, nw = (nbits + 31) >> 5, cw = b.cap >> 5;
-  for (int i = TE_LANE; i < nw; i += TE_NL) {
-    const int p = start + 32 * i, wi = p >> 5, sh = p & 31;
-    uint32_t v = b.w[wi] << sh;
-    if (sh && wi + 1 < cw) v |= b.w[wi + 1] >> (32 - sh);
-    bi.best_bits[i] = v;
-  }
-  te_sync();
-  bi.best_nbits = nbits;
-}
-// put nbits kept by te_keep_best_bits
-TE_FN void te_put_kept(TeBits &b, const uint32_t *w, int nbits) {
-#if !defined(TE_HOST)
-  for (int base = 0; base * 32 < nbits; base += 64) {
-    const int nw = TE_MIN(64, ((nbits + 31) >> 5) - base);
-    const uint32_t wl = TE_LANE < nw ? w[base + TE_LANE] : 0u;
-    for (int i = 0; i < nw; i++) {
-      const int n = TE_MIN(32, nbits - 32 * (base + i));
-      const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)wl, i);
-      te_put(b, n, n == 32 ? v : v >> (32 - n));
-    }
-  }
-#else
-  for (int i = 0; 32 * i < nbits; i++) {
-    const int n = TE_MIN(32, nbits - 32 * i);
-    te_put(b, n, n == 32 ? w[i] : w[i] >> (32 - n));
-  }
-#endif
-}
-
-// encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
-// bi.rec, write the block's syntax.  Returns the bit count.
-// One out-of-line copy of the intra chain for the P / B frames' copy of
-// te_encode_block below.
-TE_NOINL int te_enc_intra_comp_nc(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos,
-                                  int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
-                                  int tb_split, int mode, int ur, int dl, int ts) {
-  return te_enc_intra_comp(F_, org, os, rf, fs, ypos, xpos, size, qp, pb_, coef, rec, type, tb_split, mode, ur, dl, ts);
-}
-// IFR: the I-frame copy, with the intra chains inlined (no call per
-// component); P / B frames use the other, whose body stays small for the
-// inter candidates that dominate them.
-template <bool IFR>
-TE_FN int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
-  const TeFrame &F = *te_lds(&F_);
-  const TeScratch S = te_here();
-  TeBlockInfo &bi = *te_lds(&bi_);
-  TeBits &b = *te_lds(&b_);
-  TeParam &p = *te_lds(&p_);
-  TE_P(TP_ENC_BLOCK);
-  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, yC = ypos / 2, xC = xpos / 2, sC = size / 2;
-  const int mode = p.mode;
-  const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
-  uint8_t *recY = bi.rec, *recU = te_pu(bi.rec, size), *recV = te_pv(bi.rec, size);
-  const int tb_split = TE_MAX(0, p.tb_param), zero_block = p.tb_param == -1;
-  p.tb_split = tb_split;
-  const uint8_t *oY = F.oy + ypos * F.osy + xpos, *oU = F.ou + yC * F.osc + xC, *oV = F.ov + yC * F.osc + xC;
-  int cy = 0, cu = 0, cv = 0;
-  const int itype = (F.frame_type == TE_I) << 1;  // quantisation type follows the frame type (:1764)
-  if (mode == TE_INTRA) {
-    const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
-#define TE_INTRA_CHAINS(fn)                                                                                        \
-  cy = fn(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb, p.coeff, recY, itype | 0,    \
-          tb_split, p.intra_mode, ur, dl, p.ts);                                                                   \
-  cu = fn(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb, p.coeff + p.cs, recU, itype | 1,     \
-          tb_split && size > 8, p.intra_mode, ur, dl, p.ts);                                                       \
-  cv = fn(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb, p.coeff + 2 * p.cs, recV, itype | 1, \
-          tb_split && size > 8, p.intra_mode, ur, dl, p.ts);
-    if constexpr (IFR) {
-      TE_INTRA_CHAINS(te_enc_intra_comp)
-    } else {
-      TE_INTRA_CHAINS(te_enc_intra_comp_nc)
-    }
-#undef TE_INTRA_CHAINS
-  } else {
-    const int bip = F.enable_bipred;
-    if (mode == TE_SKIP) {
-      if (p.dir == 2) {
-        te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, 0);
-        te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, 0);
-        te_avg_yuv(bi.rec, S.pb0, S.pb1, bi);
-      } else {
-        te_pred_yuv(F, p.ref_idx0, bi.rec, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, 0);
-      }
-    } else if (mode == TE_MERGE) {
-      if (p.dir == 2) {
-        te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, 0);
-        te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, 0);
-        te_avg_yuv(S.pb, S.pb0, S.pb1, bi);
-      } else {
-        te_pred_yuv(F, p.ref_idx0, S.pb, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, 0);
-      }
-    } else if (mode == TE_INTER) {
-      te_pred_yuv(F, p.ref_idx0, S.pb, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, F.enable_pb_split);
-    } else if (mode == TE_BIPRED) {
-      te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, F.enable_pb_split);
-      te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, F.enable_pb_split);
-      te_avg_yuv(S.pb, S.pb0, S.pb1, bi);
-    }
-    if (mode != TE_SKIP) {
-      if (zero_block) {
-        te_copy_bytes(bi.rec, S.pb, size * size + 2 * sC * sC);
-      } else {
-        cy = te_enc_inter_comp(F, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
-        cu = te_enc_inter_comp(F, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1,
-                               tb_split && size > 8, p.ts);
-        cv = te_enc_inter_comp(F, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV,
-                               itype | 1, tb_split && size > 8, p.ts);
-      }
-    }
-  }
-  p.cbp_y = cy;
-  p.cbp_u = cu;
-  p.cbp_v = cv;
-  const int nbits = te_write_block(b, F, bi, p, S.tx->scan);
-  TE_TR(F.frame_num, 2, bi.ypos, bi.xpos, bi.size | p.mode << 8 | (p.tb_param + 1) << 12 | p.skip_idx << 16,
-        p.ref_idx0 | p.ref_idx1 << 4 | p.pb_part << 8 | p.intra_mode << 12, nbits, cy | cu << 1 | cv << 2);
-  if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
-  return nbits;
-}
-// The two out-of-line copies (one call frame each; the I-frame copy may also be
-// inlined where it has a single call site, TE_EB1_INLINE)
-TE_NOINL int te_encode_block_i(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
-  return te_encode_block_t<true>(F, b, bi, p);
-}
-TE_NOINL int te_encode_block_p(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
-  return te_encode_block_t<false>(F, b, bi, p);
-}
-TE_FN int te_encode_block(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
-  return te_lds(&F)->frame_type == TE_I ? te_encode_block_i(F, b, bi, p) : te_encode_block_p(F, b, bi, p);
-}
-#ifdef TE_EB1_INLINE
-#define TE_ENCODE_I te_encode_block_t<true>
-#else
-#define TE_ENCODE_I te_encode_block_i
-#endif
-// The final encode of a block with its best parameters bi.bp (process_block,
-// enc/encode_block.c:2953-2962 / 3012-3018).  Without tb-split the best
-// candidate's reconstruction is in rec_best and (usually) its syntax bits in
-// best_bits: copy them here, inline, so this common case makes no call -- a
-// call of te_encode_block_t saves and restores ~100 callee-saved VGPRs through
-// scratch.  Otherwise it is a full encode.
-TE_FN int te_encode_final(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_) {
-  const TeFrame &F = *te_lds(&F_);
-  TeBlockInfo &bi = *te_lds(&bi_);
-  TeBits &b = *te_lds(&b_);
-  if (!F.enable_tb_split) {  // re_use: the best candidate's reconstruction becomes rec (a swap, as copy_best does)
-    uint8_t *t = bi.rec;
-    bi.rec = bi.rec_best;
-    bi.rec_best = t;
-    if (bi.best_nbits >= 0) {  // the best candidate's own syntax bits
-      te_put_kept(b, bi.best_bits, bi.best_nbits);
-      return bi.best_nbits;
-    }
-    return te_write_block(b, F, bi, bi.bp, te_here().tx->scan);
-  }
-  return te_encode_block(F, b, bi, bi.bp);
-}
-
-// cost_calc, enc/encode_block.c:1218-1228
-TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *rec, int w, int h, int nbits) {
-  TE_P(TP_COST);
-  const int size = bi.size, sC = size / 2;
-  const int ypos = bi.ypos, xpos = bi.xpos;
-  const uint32_t sy = te_ssd(F.oy + ypos * F.osy + xpos, F.osy, rec, size, w, h);
-  const uint32_t su = te_ssd(F.ou + (ypos / 2) * F.osc + xpos / 2, F.osc, te_pu((uint8_t *)rec, size), sC, w / 2, h / 2);
-  const uint32_t sv = te_ssd(F.ov + (ypos / 2) * F.osc + xpos / 2, F.osc, te_pv((uint8_t *)rec, size), sC, w / 2, h / 2);
-  const double prod = F.lambda * (double)nbits;
-  uint32_t cost = sy + su + sv + (uint32_t)(int32_t)(prod + 0.5);
-  if (cost > (1u << 30)) cost = 1u << 30;
-  TE_TR(F.frame_num, 3, ypos, xpos, size, sy, su + sv, cost);
-  return cost;
-}
-
-// search orders (constant memory: local arrays indexed at run time would be
-// built on the stack on every call)
-TE_CONST int8_t te_intra_order[10] = {TE_DC,      TE_HOR,       TE_VER,       TE_PLANAR,     TE_UPLEFT,
-                                      TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT, TE_UPLEFTLEFT, TE_DOWNLEFTLEFT};
-TE_CONST int8_t te_hex_dy[6] = {1, 2, 1, -1, -2, -1}, te_hex_dx[6] = {-1, 0, 1, 1, 0, -1};  // enc/encode_block.c:908-909
-TE_CONST int8_t te_hp_m[9] = {0, 0, -2, 2, 0, -2, -2, 2, 2}, te_hp_n[9] = {0, -2, 0, 0, 2, -2, 2, -2, 2};  // :942-943
-TE_CONST int8_t te_qp_m[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, te_qp_n[9] = {0, -1, 0, 0, 1, -1, 1, -1, 1};
-
 #if !defined(TE_HOST)
 // The search's predictions without a prediction buffer: pixel (i, j) of
 // `mode` straight from the neighbour arrays (the same formulas as
@@ -650,6 +421,393 @@ TE_FN TeIpc te_ipx_setup(TeNbr &nb, int n) {
   return c;
 }
 #endif
+
+#ifndef TE_C4
+#if defined(TE_HOST)
+#define TE_C4 0
+#else
+#define TE_C4 1
+#endif
+#endif
+// encode_and_reconstruct_block_intra, enc/encode_block.c:1398-1467, one
+// component.  rf / fs: the frame being reconstructed at the CU origin.
+TE_FN int te_enc_intra_comp(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs,
+                               int ypos, int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
+                               int tb_split, int mode, int ur, int dl, int ts) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_here();
+  uint8_t *pb = te_lds(pb_);
+  TE_P(TP_INTRA_COMP);
+  TeTx &X = *S.tx;
+  const int fast = F.speed > 1;
+  if (tb_split) {
+    const int s2 = size / 2;
+    int cbp = 0;
+    for (int t = 0; t < 4; t++) {
+      const int i = (t >> 1) * s2, j = (t & 1) * s2;
+      te_make_top_and_left(*S.nb, rf, fs, rec + i * size + j, size, i, j, ypos, xpos, s2, ur, dl, 1);
+      te_intra_pred(*S.nb, ypos + i, xpos + j, s2, pb, mode, 0);
+      te_residual_tx(X, org + i * os + j, os, pb, s2, s2, fast);
+      te_fwd_tx(X, s2, fast);
+      const int bit = te_quant_chain(X, qp, s2, type, coef + t * ts);
+      if (bit) te_inv_tx(X, s2);
+      te_recon(rec + i * size + j, size, pb, s2, X, s2, bit);
+      cbp = (cbp << 1) + bit;
+    }
+    return cbp;
+  }
+  te_make_top_and_left(*S.nb, rf, fs, nullptr, 0, 0, 0, ypos, xpos, size, ur, dl, 0);
+  te_intra_pred(*S.nb, ypos, xpos, size, pb, mode, 0);
+  te_residual_tx(X, org, os, pb, size, size, fast);
+  te_fwd_tx(X, size, fast);
+  const int cbp = te_quant_chain(X, qp, size, type, coef);
+  if (cbp) te_inv_tx(X, size);
+  te_recon(rec, size, pb, size, X, size, cbp);
+  return cbp;
+}
+
+#if !defined(TE_HOST)
+// te_enc_intra_comp for a 4 x 4 block (the chroma of an 8 x 8 CU: 2 of the 3
+// chains of the commonest CU) with every step in registers: lane r < 16 holds
+// pixel / coefficient r (raster) of the block; the transforms' row and column
+// passes gather their four inputs with ds_bpermute (no LDS round trip, no
+// barrier); quantize's last position and the RDOQ-light masks are wave
+// reductions, its candidate loop scalar.  The same arithmetic as the generic
+// chain: te_fwd_gen<4>, te_quant_t, te_inv_gen<4>, te_recon (enc_pix.h).
+TE_FN int te_d4(uint32_t w, int k) { return __builtin_amdgcn_sbfe((int)w, 8 * k, 8); }
+TE_FN uint32_t te_or16(uint32_t v) {  // OR over lanes 0..15 (lanes >= 16 contribute 0), uniform
+  v |= (uint32_t)TE_DPP(v, 0xB1);
+  v |= (uint32_t)TE_DPP(v, 0x4E);
+  v |= (uint32_t)TE_DPP(v, 0x141);
+  v |= (uint32_t)TE_DPP(v, 0x140);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+}
+// residual -> levels (into coef) -> reconstruction (into rec, stride 4) of the
+// 4 x 4 block whose prediction lane r < 16 holds in p; returns cbp
+TE_FN int te_c4_code(int p, const uint8_t *org, int os, int qp, int16_t *coef, uint8_t *rec, int type) {
+  const int lane = TE_LANE, r = lane & 15, i = r >> 2, j = r & 3, base = lane & ~15;
+  const bool act = lane < 16;
+  // HEVC 4-point basis rows (D[i][k]) and columns (D[k][j]) as packed int8
+  const uint32_t rowD = i == 0 ? 0x40404040u : (i == 1 ? 0xADDC2453u : (i == 2 ? 0x40C0C040u : 0xDC53AD24u));
+  const uint32_t colD = j == 0 ? 0x24405340u : (j == 1 ? 0xADC02440u : (j == 2 ? 0x53C0DC40u : 0xDC40AD40u));
+  const int R = (int)org[i * os + j] - p;
+  // transform (common/transform.c:309-327): T = D R^T, C = D T^T, 16-bit wraps; N = 4: shifts 2, 7
+  int t = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) t += te_d4(rowD, k) * __shfl(R, base + 4 * j + k);
+  t = te_wrap16((t + 2) >> 2);
+  int C = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) C += te_d4(rowD, k) * __shfl(t, base + 4 * j + k);
+  C = te_wrap16((C + 64) >> 7);
+  // quantize (enc/encode_block.c:75-172, rdoq 0), q = 4
+  const int intra = (type >> 1) & 1, chroma = type & 1;
+  const int scale = te_gquant[qp % 6], shift2 = 21 - 2 + qp / 6;
+  const int offset = (intra ? 38 : -26) * (1 << (shift2 - 8));
+  const int pos = (int)((0xfea9db83c7426510ull >> (4 * r)) & 15);  // te_zz(4, r)
+  const int lp = (act && (te_abs(te_abs(C) * scale + offset) >> shift2) != 0) ? pos : -1;
+  const int last_pos = te_maxi(lp);
+  const int off0 = (intra ? 102 : 51) * (1 << (shift2 - 8)), off1 = (intra ? 115 : 90) * (1 << (shift2 - 8));
+  int lev = 0;
+  if (act && pos <= last_pos) {
+    const int ac = scale * te_abs(C);
+    const int l0 = ac >> shift2;
+    const int l = (ac + ((l0 == 0 || chroma) ? off0 : off1)) >> shift2;
+    lev = C < 0 ? -l : l;
+  }
+  const int cbp = te_any(lev != 0);
+  if (cbp) {  // RDOQ light (:134-168) on the scan-order masks, as te_quant_t
+    const int n = chroma ? last_pos + 1 : 16;
+    const int thr = (73 * te_gdequant[qp % 6] << (qp / 6)) >> (4 + 2);
+    uint32_t big = te_or16(act && te_abs(lev) > 1 ? 1u << pos : 0u);
+    uint32_t nzm = te_or16(act && lev != 0 ? 1u << pos : 0u);
+    uint32_t chg = 0, neg = 0;
+    uint32_t m = big & (n >= 16 ? 0xffffu : ((1u << n) - 1)) & ~3u;
+    while (m) {
+      const int q = __builtin_ctz(m);
+      m &= m - 1;
+      int flag = 1;
+      if (q > 2 && ((big >> (q - 3)) & 1)) flag = 0;
+      if (q > 3 && ((big >> (q - 4)) & 1) && ((nzm >> (q - 3)) & 1)) flag = 0;
+      if (q == 2 && (chroma == 0 || last_pos >= 6)) flag = 0;
+      if (flag && !((nzm >> (q - 2)) & 1) && !((nzm >> (q - 1)) & 1) && ((big >> q) & 1)) {
+        // coefficients at scan positions q, q - 1, q - 2: their raster lanes (te_izz(4, .))
+        const int c1 = __builtin_amdgcn_readlane(C, (int)((0xfeb7adc963258410ull >> (4 * q)) & 15));
+        const int c2 = __builtin_amdgcn_readlane(C, (int)((0xfeb7adc963258410ull >> (4 * (q - 1))) & 15));
+        const int c3 = __builtin_amdgcn_readlane(C, (int)((0xfeb7adc963258410ull >> (4 * (q - 2))) & 15));
+        const int K1 = te_abs(c1), K2 = te_abs(c2), K3 = te_abs(c3), K4 = TE_MAX(K2, K3);
+        int at, v;
+        if (K1 + K4 < thr) {
+          at = q;
+          v = c1 < 0 ? -1 : 1;
+        } else if (K2 > K3) {
+          at = q - 1;
+          v = c2 < 0 ? -1 : 1;
+        } else {
+          at = q - 2;
+          v = c3 < 0 ? -1 : 1;
+        }
+        chg |= 1u << at;
+        neg = v < 0 ? neg | (1u << at) : neg & ~(1u << at);
+        big &= ~(1u << at);
+        nzm |= 1u << at;
+      }
+    }
+    if ((chg >> pos) & 1) lev = ((neg >> pos) & 1) ? -1 : 1;
+  }
+  if (act) coef[r] = (int16_t)lev;
+  int v = p;
+  if (cbp) {
+    // dequantize (common/common_block.c:132-146): rshift 1, add 1
+    const int d = te_wrap16(((lev * te_gdequant[qp % 6]) * (1 << (qp / 6)) + 1) >> 1);
+    // inverse transform (common/transform.c:432-518): T'[k][y] = D^T C ..., R = D^T C D, clips
+    int t2 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) t2 += te_d4(colD, k) * __shfl(d, base + 4 * k + i);
+    t2 = te_clip16((t2 + 64) >> 7);
+    int res = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) res += te_d4(colD, k) * __shfl(t2, base + 4 * k + i);
+    res = te_clip16((res + 2048) >> 12);
+    v = te_clip255(res + p);
+  }
+  if (act) rec[r] = (uint8_t)v;
+  te_sync();
+  return cbp;
+}
+TE_FN int te_enc_intra_c4(const TeFrame &F, const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos, int xpos,
+                          int qp, int16_t *coef, uint8_t *rec, int type, int mode, int ur, int dl) {
+  TE_P(TP_INTRA_COMP);
+  (void)F;
+  const TeScratch S = te_here();
+  TeNbr &nbw = *S.nb;
+  te_make_top_and_left(nbw, rf, fs, nullptr, 0, 0, 0, ypos, xpos, 4, ur, dl, 0);
+  TeIpc c = te_ipx_setup(nbw, 4);
+  const TeNbr &nb = nbw;
+  {  // DC of get_intra_prediction (position-aware, common/intra_prediction.c:145-160)
+    const int sl = nb.left[0] + nb.left[1] + nb.left[2] + nb.left[3], st = nb.top[0] + nb.top[1] + nb.top[2] + nb.top[3];
+    c.dc = ((xpos != 0 ? sl : st) + (ypos != 0 ? st : sl) + 4) / 8;
+  }
+  const int r = TE_LANE & 15;
+  return te_c4_code(te_ipx(nb, c, 4, mode, r >> 2, r & 3), org, os, qp, coef, rec, type);
+}
+// te_enc_inter_comp for a 4 x 4 block: the prediction from the compact buffer (stride 4)
+TE_FN int te_enc_inter_c4(const uint8_t *org, int os, int qp, const uint8_t *pb, int16_t *coef, uint8_t *rec, int type) {
+  TE_P(TP_INTER_COMP);
+  return te_c4_code(te_lds(pb)[TE_LANE & 15], org, os, qp, coef, rec, type);
+}
+#else
+TE_FN int te_enc_inter_c4(const uint8_t *, int, int, const uint8_t *, int16_t *, uint8_t *, int) { return 0; }
+TE_FN int te_enc_intra_c4(const TeFrame &, const uint8_t *, int, const uint8_t *, int, int, int, int, int16_t *, uint8_t *,
+                          int, int, int, int) {
+  return 0;  // (TE_C4 is 0 on the host: the generic chain runs)
+}
+#endif
+
+// The candidate just written (its nbits end at b.pos) became the best: keep
+// its syntax bits, so that the final encode of the block (re-use, the same
+// parameters and contexts) copies them instead of running write_block again.
+TE_FN void te_keep_best_bits(TeBits &b, TeBlockInfo &bi, int nbits) {
+  if (nbits > bi.best_cap * 32 || b.pos > b.cap) {
+    bi.best_nbits = -1;
+    return;
+  }
+  if ((b.pos & 31) && TE_LANE == 0) b.w[b.pos >> 5] = b.cur;  // the register word (stored again when complete)
+  te_sync();
+  const int start = b.pos - nbits, nw = (nbits + 31) >> 5, cw = b.cap >> 5;
+  for (int i = TE_LANE; i < nw; i += TE_NL) {
+    const int p = start + 32 * i, wi = p >> 5, sh = p & 31;
+    uint32_t v = b.w[wi] << sh;
+    if (sh && wi + 1 < cw) v |= b.w[wi + 1] >> (32 - sh);
+    bi.best_bits[i] = v;
+  }
+  te_sync();
+  bi.best_nbits = nbits;
+}
+// put nbits kept by te_keep_best_bits
+TE_FN void te_put_kept(TeBits &b, const uint32_t *w, int nbits) {
+#if !defined(TE_HOST)
+  for (int base = 0; base * 32 < nbits; base += 64) {
+    const int nw = TE_MIN(64, ((nbits + 31) >> 5) - base);
+    const uint32_t wl = TE_LANE < nw ? w[base + TE_LANE] : 0u;
+    for (int i = 0; i < nw; i++) {
+      const int n = TE_MIN(32, nbits - 32 * (base + i));
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)wl, i);
+      te_put(b, n, n == 32 ? v : v >> (32 - n));
+    }
+  }
+#else
+  for (int i = 0; 32 * i < nbits; i++) {
+    const int n = TE_MIN(32, nbits - 32 * i);
+    te_put(b, n, n == 32 ? w[i] : w[i] >> (32 - n));
+  }
+#endif
+}
+
+// encode_block, enc/encode_block.c:1590-1800: predict, code the residual into
+// bi.rec, write the block's syntax.  Returns the bit count.
+// One out-of-line copy of the intra chain for the P / B frames' copy of
+// te_encode_block below.
+TE_NOINL int te_enc_intra_comp_nc(const TeFrame &F_, const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos,
+                                  int xpos, int size, int qp, uint8_t *pb_, int16_t *coef, uint8_t *rec, int type,
+                                  int tb_split, int mode, int ur, int dl, int ts) {
+  return te_enc_intra_comp(F_, org, os, rf, fs, ypos, xpos, size, qp, pb_, coef, rec, type, tb_split, mode, ur, dl, ts);
+}
+// IFR: the I-frame copy, with the intra chains inlined (no call per
+// component); P / B frames use the other, whose body stays small for the
+// inter candidates that dominate them.
+template <bool IFR>
+TE_FN int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeParam &p_) {
+  const TeFrame &F = *te_lds(&F_);
+  const TeScratch S = te_here();
+  TeBlockInfo &bi = *te_lds(&bi_);
+  TeBits &b = *te_lds(&b_);
+  TeParam &p = *te_lds(&p_);
+  TE_P(TP_ENC_BLOCK);
+  const int size = bi.size, ypos = bi.ypos, xpos = bi.xpos, yC = ypos / 2, xC = xpos / 2, sC = size / 2;
+  const int mode = p.mode;
+  const int qpY = F.qp + bi.delta_qp, qpC = te_chroma_qp(qpY);
+  uint8_t *recY = bi.rec, *recU = te_pu(bi.rec, size), *recV = te_pv(bi.rec, size);
+  const int tb_split = TE_MAX(0, p.tb_param), zero_block = p.tb_param == -1;
+  p.tb_split = tb_split;
+  const uint8_t *oY = F.oy + ypos * F.osy + xpos, *oU = F.ou + yC * F.osc + xC, *oV = F.ov + yC * F.osc + xC;
+  int cy = 0, cu = 0, cv = 0;
+  const int itype = (F.frame_type == TE_I) << 1;  // quantisation type follows the frame type (:1764)
+  if (mode == TE_INTRA) {
+    const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
+#define TE_INTRA_CHAINS(fn)                                                                                        \
+  cy = fn(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb, p.coeff, recY, itype | 0,    \
+          tb_split, p.intra_mode, ur, dl, p.ts);                                                                   \
+  if (TE_C4 && sC == 4) {                                                                                         \
+    cu = te_enc_intra_c4(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + p.cs, recU, itype | 1,  \
+                         p.intra_mode, ur, dl);                                                                    \
+    cv = te_enc_intra_c4(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + 2 * p.cs, recV,        \
+                         itype | 1, p.intra_mode, ur, dl);                                                         \
+  } else {                                                                                                         \
+    cu = fn(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb, p.coeff + p.cs, recU, itype | 1,   \
+            tb_split && size > 8, p.intra_mode, ur, dl, p.ts);                                                     \
+    cv = fn(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, sC, qpC, S.pb, p.coeff + 2 * p.cs, recV,          \
+            itype | 1, tb_split && size > 8, p.intra_mode, ur, dl, p.ts);                                          \
+  }
+    if constexpr (IFR) {
+      TE_INTRA_CHAINS(te_enc_intra_comp)
+    } else {
+      TE_INTRA_CHAINS(te_enc_intra_comp_nc)
+    }
+#undef TE_INTRA_CHAINS
+  } else {
+    const int bip = F.enable_bipred;
+    if (mode == TE_SKIP) {
+      if (p.dir == 2) {
+        te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, 0);
+        te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, 0);
+        te_avg_yuv(bi.rec, S.pb0, S.pb1, bi);
+      } else {
+        te_pred_yuv(F, p.ref_idx0, bi.rec, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, 0);
+      }
+    } else if (mode == TE_MERGE) {
+      if (p.dir == 2) {
+        te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, 0);
+        te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, 0);
+        te_avg_yuv(S.pb, S.pb0, S.pb1, bi);
+      } else {
+        te_pred_yuv(F, p.ref_idx0, S.pb, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, 0);
+      }
+    } else if (mode == TE_INTER) {
+      te_pred_yuv(F, p.ref_idx0, S.pb, bi, p.mv0, te_sign_of(F, p.ref_idx0, 0), bip, F.enable_pb_split);
+    } else if (mode == TE_BIPRED) {
+      te_pred_yuv(F, p.ref_idx0, S.pb0, bi, p.mv0, te_sign_of(F, p.ref_idx0, 1), bip, F.enable_pb_split);
+      te_pred_yuv(F, p.ref_idx1, S.pb1, bi, p.mv1, te_sign_of(F, p.ref_idx1, 1), bip, F.enable_pb_split);
+      te_avg_yuv(S.pb, S.pb0, S.pb1, bi);
+    }
+    if (mode != TE_SKIP) {
+      if (zero_block) {
+        te_copy_bytes(bi.rec, S.pb, size * size + 2 * sC * sC);
+      } else {
+        cy = te_enc_inter_comp(F, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
+        if (TE_C4 && sC == 4) {
+          cu = te_enc_inter_c4(oU, F.osc, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1);
+          cv = te_enc_inter_c4(oV, F.osc, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV, itype | 1);
+        } else {
+          cu = te_enc_inter_comp(F, oU, F.osc, sC, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1,
+                                 tb_split && size > 8, p.ts);
+          cv = te_enc_inter_comp(F, oV, F.osc, sC, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV,
+                                 itype | 1, tb_split && size > 8, p.ts);
+        }
+      }
+    }
+  }
+  p.cbp_y = cy;
+  p.cbp_u = cu;
+  p.cbp_v = cv;
+  const int nbits = te_write_block(b, F, bi, p, S.tx->scan);
+  TE_TR(F.frame_num, 2, bi.ypos, bi.xpos, bi.size | p.mode << 8 | (p.tb_param + 1) << 12 | p.skip_idx << 16,
+        p.ref_idx0 | p.ref_idx1 << 4 | p.pb_part << 8 | p.intra_mode << 12, nbits, cy | cu << 1 | cv << 2);
+  if (tb_split) p.cbp_y = p.cbp_u = p.cbp_v = 1;  // deblocking only (:1781-1784)
+  return nbits;
+}
+// The two out-of-line copies (one call frame each; the I-frame copy may also be
+// inlined where it has a single call site, TE_EB1_INLINE)
+TE_NOINL int te_encode_block_i(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_encode_block_t<true>(F, b, bi, p);
+}
+TE_NOINL int te_encode_block_p(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_encode_block_t<false>(F, b, bi, p);
+}
+TE_FN int te_encode_block(const TeFrame &F, TeBits &b, TeBlockInfo &bi, TeParam &p) {
+  return te_lds(&F)->frame_type == TE_I ? te_encode_block_i(F, b, bi, p) : te_encode_block_p(F, b, bi, p);
+}
+#ifdef TE_EB1_INLINE
+#define TE_ENCODE_I te_encode_block_t<true>
+#else
+#define TE_ENCODE_I te_encode_block_i
+#endif
+// The final encode of a block with its best parameters bi.bp (process_block,
+// enc/encode_block.c:2953-2962 / 3012-3018).  Without tb-split the best
+// candidate's reconstruction is in rec_best and (usually) its syntax bits in
+// best_bits: copy them here, inline, so this common case makes no call -- a
+// call of te_encode_block_t saves and restores ~100 callee-saved VGPRs through
+// scratch.  Otherwise it is a full encode.
+TE_FN int te_encode_final(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_) {
+  const TeFrame &F = *te_lds(&F_);
+  TeBlockInfo &bi = *te_lds(&bi_);
+  TeBits &b = *te_lds(&b_);
+  if (!F.enable_tb_split) {  // re_use: the best candidate's reconstruction becomes rec (a swap, as copy_best does)
+    uint8_t *t = bi.rec;
+    bi.rec = bi.rec_best;
+    bi.rec_best = t;
+    if (bi.best_nbits >= 0) {  // the best candidate's own syntax bits
+      te_put_kept(b, bi.best_bits, bi.best_nbits);
+      return bi.best_nbits;
+    }
+    return te_write_block(b, F, bi, bi.bp, te_here().tx->scan);
+  }
+  return te_encode_block(F, b, bi, bi.bp);
+}
+
+// cost_calc, enc/encode_block.c:1218-1228
+TE_FN uint32_t te_cost(const TeFrame &F, const TeBlockInfo &bi, const uint8_t *rec, int w, int h, int nbits) {
+  TE_P(TP_COST);
+  const int size = bi.size, sC = size / 2;
+  const int ypos = bi.ypos, xpos = bi.xpos;
+  const uint32_t sy = te_ssd(F.oy + ypos * F.osy + xpos, F.osy, rec, size, w, h);
+  const uint32_t su = te_ssd(F.ou + (ypos / 2) * F.osc + xpos / 2, F.osc, te_pu((uint8_t *)rec, size), sC, w / 2, h / 2);
+  const uint32_t sv = te_ssd(F.ov + (ypos / 2) * F.osc + xpos / 2, F.osc, te_pv((uint8_t *)rec, size), sC, w / 2, h / 2);
+  const double prod = F.lambda * (double)nbits;
+  uint32_t cost = sy + su + sv + (uint32_t)(int32_t)(prod + 0.5);
+  if (cost > (1u << 30)) cost = 1u << 30;
+  TE_TR(F.frame_num, 3, ypos, xpos, size, sy, su + sv, cost);
+  return cost;
+}
+
+// search orders (constant memory: local arrays indexed at run time would be
+// built on the stack on every call)
+TE_CONST int8_t te_intra_order[10] = {TE_DC,      TE_HOR,       TE_VER,       TE_PLANAR,     TE_UPLEFT,
+                                      TE_UPRIGHT, TE_UPUPRIGHT, TE_UPUPLEFT, TE_UPLEFTLEFT, TE_DOWNLEFTLEFT};
+TE_CONST int8_t te_hex_dy[6] = {1, 2, 1, -1, -2, -1}, te_hex_dx[6] = {-1, 0, 1, 1, 0, -1};  // enc/encode_block.c:908-909
+TE_CONST int8_t te_hp_m[9] = {0, 0, -2, 2, 0, -2, -2, 2, 2}, te_hp_n[9] = {0, -2, 0, 0, 2, -2, 2, -2, 2};  // :942-943
+TE_CONST int8_t te_qp_m[9] = {0, 0, -1, 1, 0, -1, -1, 1, 1}, te_qp_n[9] = {0, -1, 0, 0, 1, -1, 1, -1, 1};
+
 
 #if !defined(TE_HOST)
 // blocks of 16 x 16 and up: T 4-pixel chunks per lane, the original in registers, one mode after the other
