@@ -575,6 +575,157 @@ TE_FN int te_c4_code(int p, const uint8_t *org, int os, int qp, int16_t *coef, u
   te_sync();
   return cbp;
 }
+// The same for an 8 x 8 block: lane r holds pixel / coefficient r (raster).
+// The forward passes are the reference SIMD transform8 (te_fwd8: 16-bit
+// wrapping butterflies), output (k, row) in lane 8k + row, its input row
+// gathered with eight ds_bpermute; the inverse passes take the 8-point basis
+// column from the worker's LDS copy (X.M).
+TE_FN uint32_t te_or_wave(uint32_t v) {  // OR over the wave, uniform
+  v |= (uint32_t)TE_DPP(v, 0xB1);
+  v |= (uint32_t)TE_DPP(v, 0x4E);
+  v |= (uint32_t)TE_DPP(v, 0x141);
+  v |= (uint32_t)TE_DPP(v, 0x140);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+TE_FN int te_fwd8r(const int *s, int k, int shift) {  // te_fwd8 (enc_pix.h) on a register row
+  int E[4], O[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    E[m] = te_wrap16(s[m] + s[7 - m]);
+    O[m] = te_wrap16(s[m] - s[7 - m]);
+  }
+  const int EO0 = te_wrap16(E[0] - E[3]), EO1 = te_wrap16(E[1] - E[2]);
+  int v;
+  switch (k) {
+    case 0: v = 64 * E[0] + 64 * E[1] + 64 * E[2] + 64 * E[3]; break;
+    case 4: v = 64 * E[0] - 64 * E[1] - 64 * E[2] + 64 * E[3]; break;
+    case 2: v = 83 * EO0 + 36 * EO1; break;
+    case 6: v = 36 * EO0 - 83 * EO1; break;
+    case 1: v = 89 * O[0] + 75 * O[1] + 50 * O[2] + 18 * O[3]; break;
+    case 3: v = 75 * O[0] - 18 * O[1] - 89 * O[2] - 50 * O[3]; break;
+    case 5: v = 50 * O[0] - 89 * O[1] + 18 * O[2] + 75 * O[3]; break;
+    default: v = 18 * O[0] - 50 * O[1] + 75 * O[2] - 89 * O[3]; break;
+  }
+  return te_wrap16((v + (1 << (shift - 1))) >> shift);
+}
+TE_FN int te_c8_code(int p, const uint8_t *org, int os, int qp, int16_t *coef, uint8_t *rec, int type) {
+  const TeScratch S = te_here();
+  const TeTx &X = *S.tx;
+  const int L = TE_LANE, hi = L >> 3, lo = L & 7;
+  const int R = (int)org[hi * os + lo] - p;
+  // transform8 (common/common_kernels.c:1887-1967): T[k][row] from row `row` of R, then C[k][row] from row `row` of T
+  int x[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) x[m] = __shfl(R, 8 * lo + m);
+  const int t = te_fwd8r(x, hi, 3);
+#pragma unroll
+  for (int m = 0; m < 8; m++) x[m] = __shfl(t, 8 * lo + m);
+  const int C = te_fwd8r(x, hi, 8);
+  // quantize (enc/encode_block.c:75-172, rdoq 0), q = 8
+  const int intra = (type >> 1) & 1, chroma = type & 1;
+  const int scale = te_gquant[qp % 6], shift2 = 21 - 3 + qp / 6;
+  const int offset = (intra ? 38 : -26) * (1 << (shift2 - 8));
+  const int pos = te_zz(8, L);
+  const int lp = (te_abs(te_abs(C) * scale + offset) >> shift2) != 0 ? pos : -1;
+  const int last_pos = te_maxi(lp);
+  const int off0 = (intra ? 102 : 51) * (1 << (shift2 - 8)), off1 = (intra ? 115 : 90) * (1 << (shift2 - 8));
+  int lev = 0;
+  if (pos <= last_pos) {
+    const int ac = scale * te_abs(C);
+    const int l0 = ac >> shift2;
+    const int l = (ac + ((l0 == 0 || chroma) ? off0 : off1)) >> shift2;
+    lev = C < 0 ? -l : l;
+  }
+  const int cbp = te_any(lev != 0);
+  if (cbp) {  // RDOQ light (:134-168) on the scan-order masks, as te_quant_t
+    const int n = chroma ? last_pos + 1 : 64;
+    const int thr = (73 * te_gdequant[qp % 6] << (qp / 6)) >> (4 + 3);
+    const bool b1 = te_abs(lev) > 1, b0 = lev != 0;
+    uint64_t big = (uint64_t)te_or_wave(b1 && pos < 32 ? 1u << pos : 0u) |
+                   (uint64_t)te_or_wave(b1 && pos >= 32 ? 1u << (pos - 32) : 0u) << 32;
+    uint64_t nzm = (uint64_t)te_or_wave(b0 && pos < 32 ? 1u << pos : 0u) |
+                   (uint64_t)te_or_wave(b0 && pos >= 32 ? 1u << (pos - 32) : 0u) << 32;
+    uint64_t chg = 0, neg = 0;
+    uint64_t m = big & (n >= 64 ? ~0ull : ((1ull << n) - 1)) & ~3ull;
+    while (m) {
+      const int q = __builtin_ctzll(m);
+      m &= m - 1;
+      int flag = 1;
+      if (q > 2 && ((big >> (q - 3)) & 1)) flag = 0;
+      if (q > 3 && ((big >> (q - 4)) & 1) && ((nzm >> (q - 3)) & 1)) flag = 0;
+      if (q == 2 && (chroma == 0 || last_pos >= 6)) flag = 0;
+      if (flag && !((nzm >> (q - 2)) & 1) && !((nzm >> (q - 1)) & 1) && ((big >> q) & 1)) {
+        const int c1 = __builtin_amdgcn_readlane(C, te_izz(8, q));
+        const int c2 = __builtin_amdgcn_readlane(C, te_izz(8, q - 1));
+        const int c3 = __builtin_amdgcn_readlane(C, te_izz(8, q - 2));
+        const int K1 = te_abs(c1), K2 = te_abs(c2), K3 = te_abs(c3), K4 = TE_MAX(K2, K3);
+        int at, v;
+        if (K1 + K4 < thr) {
+          at = q;
+          v = c1 < 0 ? -1 : 1;
+        } else if (K2 > K3) {
+          at = q - 1;
+          v = c2 < 0 ? -1 : 1;
+        } else {
+          at = q - 2;
+          v = c3 < 0 ? -1 : 1;
+        }
+        chg |= 1ull << at;
+        neg = v < 0 ? neg | (1ull << at) : neg & ~(1ull << at);
+        big &= ~(1ull << at);
+        nzm |= 1ull << at;
+      }
+    }
+    if ((chg >> pos) & 1) lev = ((neg >> pos) & 1) ? -1 : 1;
+  }
+  coef[L] = (int16_t)lev;
+  int v = p;
+  if (cbp) {
+    // dequantize (common/common_block.c:132-146): rshift 2, add 2
+    const int d = te_wrap16(((lev * te_gdequant[qp % 6]) * (1 << (qp / 6)) + 2) >> 2);
+    // inverse transform (common/transform.c:432-518), te_inv_gen<8>: basis column `lo` from X.M
+    int dc[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) dc[k] = TE_DCT(X, 8, k, lo);
+    int t2 = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) t2 += dc[k] * __shfl(d, 8 * k + hi);
+    t2 = te_clip16((t2 + 64) >> 7);
+    int res = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) res += dc[k] * __shfl(t2, 8 * k + hi);
+    res = te_clip16((res + 2048) >> 12);
+    v = te_clip255(res + p);
+  }
+  rec[L] = (uint8_t)v;
+  te_sync();
+  return cbp;
+}
+TE_FN int te_enc_intra_c8(const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos, int xpos, int qp,
+                          int16_t *coef, uint8_t *rec, int type, int mode, int ur, int dl) {
+  TE_P(TP_INTRA_COMP);
+  const TeScratch S = te_here();
+  TeNbr &nbw = *S.nb;
+  te_make_top_and_left(nbw, rf, fs, nullptr, 0, 0, 0, ypos, xpos, 8, ur, dl, 0);
+  TeIpc c = te_ipx_setup(nbw, 8);
+  const TeNbr &nb = nbw;
+  {  // DC of get_intra_prediction (position-aware, common/intra_prediction.c:145-160)
+    int sl = 0, st = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      sl += nb.left[k];
+      st += nb.top[k];
+    }
+    c.dc = ((xpos != 0 ? sl : st) + (ypos != 0 ? st : sl) + 8) / 16;
+  }
+  const int L = TE_LANE;
+  return te_c8_code(te_ipx(nb, c, 8, mode, L >> 3, L & 7), org, os, qp, coef, rec, type);
+}
+TE_FN int te_enc_inter_c8(const uint8_t *org, int os, int qp, const uint8_t *pb, int16_t *coef, uint8_t *rec, int type) {
+  TE_P(TP_INTER_COMP);
+  return te_c8_code(te_lds(pb)[TE_LANE], org, os, qp, coef, rec, type);
+}
 TE_FN int te_enc_intra_c4(const TeFrame &F, const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos, int xpos,
                           int qp, int16_t *coef, uint8_t *rec, int type, int mode, int ur, int dl) {
   TE_P(TP_INTRA_COMP);
@@ -597,6 +748,11 @@ TE_FN int te_enc_inter_c4(const uint8_t *org, int os, int qp, const uint8_t *pb,
   return te_c4_code(te_lds(pb)[TE_LANE & 15], org, os, qp, coef, rec, type);
 }
 #else
+TE_FN int te_enc_inter_c8(const uint8_t *, int, int, const uint8_t *, int16_t *, uint8_t *, int) { return 0; }
+TE_FN int te_enc_intra_c8(const uint8_t *, int, const uint8_t *, int, int, int, int, int16_t *, uint8_t *, int, int, int,
+                          int) {
+  return 0;
+}
 TE_FN int te_enc_inter_c4(const uint8_t *, int, int, const uint8_t *, int16_t *, uint8_t *, int) { return 0; }
 TE_FN int te_enc_intra_c4(const TeFrame &, const uint8_t *, int, const uint8_t *, int, int, int, int, int16_t *, uint8_t *,
                           int, int, int, int) {
@@ -676,9 +832,18 @@ TE_FN int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeP
   if (mode == TE_INTRA) {
     const int ur = te_upright_avail(ypos, xpos, size, F.W), dl = te_downleft_avail(ypos, xpos, size, F.H);
 #define TE_INTRA_CHAINS(fn)                                                                                        \
-  cy = fn(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb, p.coeff, recY, itype | 0,    \
-          tb_split, p.intra_mode, ur, dl, p.ts);                                                                   \
-  if (TE_C4 && sC == 4) {                                                                                         \
+  if (TE_C4 && size == 8 && !tb_split)                                                                             \
+    cy = te_enc_intra_c8(oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, qpY, p.coeff, recY, itype | 0,   \
+                         p.intra_mode, ur, dl);                                                                    \
+  else                                                                                                             \
+    cy = fn(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb, p.coeff, recY, itype | 0,  \
+            tb_split, p.intra_mode, ur, dl, p.ts);                                                                 \
+  if (TE_C4 && sC == 8 && !(tb_split && size > 8)) {                                                              \
+    cu = te_enc_intra_c8(oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + p.cs, recU, itype | 1,     \
+                         p.intra_mode, ur, dl);                                                                    \
+    cv = te_enc_intra_c8(oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + 2 * p.cs, recV, itype | 1, \
+                         p.intra_mode, ur, dl);                                                                    \
+  } else if (TE_C4 && sC == 4) {                                                                                  \
     cu = te_enc_intra_c4(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + p.cs, recU, itype | 1,  \
                          p.intra_mode, ur, dl);                                                                    \
     cv = te_enc_intra_c4(F, oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + 2 * p.cs, recV,        \
@@ -724,8 +889,14 @@ TE_FN int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeP
       if (zero_block) {
         te_copy_bytes(bi.rec, S.pb, size * size + 2 * sC * sC);
       } else {
-        cy = te_enc_inter_comp(F, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
-        if (TE_C4 && sC == 4) {
+        if (TE_C4 && size == 8 && !tb_split)
+          cy = te_enc_inter_c8(oY, F.osy, qpY, S.pb, p.coeff, recY, itype | 0);
+        else
+          cy = te_enc_inter_comp(F, oY, F.osy, size, qpY, S.pb, p.coeff, recY, itype | 0, tb_split, p.ts);
+        if (TE_C4 && sC == 8 && !(tb_split && size > 8)) {
+          cu = te_enc_inter_c8(oU, F.osc, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1);
+          cv = te_enc_inter_c8(oV, F.osc, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV, itype | 1);
+        } else if (TE_C4 && sC == 4) {
           cu = te_enc_inter_c4(oU, F.osc, qpC, te_pu(S.pb, size), p.coeff + p.cs, recU, itype | 1);
           cv = te_enc_inter_c4(oV, F.osc, qpC, te_pv(S.pb, size), p.coeff + 2 * p.cs, recV, itype | 1);
         } else {
