@@ -509,9 +509,26 @@ struct TeNbr {
   int T[64], L[64];                        // planar edge sums
   int tl, tlF, TL;
 };
+#if !defined(TE_HOST)
+// The luma block whose neighbour arrays and search setup the worker's TeNbr
+// holds (set by te_search_intra after te_ipx_setup, 0: none): the block's
+// 8 x 8 register chain then skips rebuilding them.  Every writer of the
+// arrays forgets it first.
+__shared__ int g_te_nb_key;
+#define TE_NB_FORGET()                 \
+  do {                                 \
+    if (TE_LANE == 0) g_te_nb_key = 0; \
+  } while (0)
+#else
+#define TE_NB_FORGET() \
+  do {                 \
+  } while (0)
+#endif
+TE_FN int te_nb_key(int ypos, int xpos, int size) { return ((ypos << 16) | (xpos << 3) | te_log2(size)) + 1; }
 TE_FN void te_make_top_and_left(TeNbr &nb, const uint8_t *rf, int fs, const uint8_t *rb, int rbs, int i, int j, int ypos,
                                 int xpos, int size, int cb_ur, int cb_dl, int tb_split) {
   TE_P(TP_TOPLEFT);
+  TE_NB_FORGET();
   int dl, ur;
   if (!tb_split) {
     dl = cb_dl;
@@ -564,6 +581,7 @@ TE_FN void te_f121(const uint8_t *in, uint8_t *out, int len) {
 // (enc/encode_block.c:1250, always (left, top)) instead of the position-aware one.
 TE_FN void te_intra_pred(TeNbr &nb, int ypos, int xpos, int n, uint8_t *pb, int mode, int search_dc) {
   TE_P(TP_IPRED);
+  TE_NB_FORGET();
   // four horizontally adjacent pixels per lane and step (n >= 4), one dword store
   const int n4 = (n * n) >> 2;
   auto quad = [&](auto px) {

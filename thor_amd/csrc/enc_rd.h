@@ -387,6 +387,18 @@ TE_FN uint32_t te_ipx4(const TeNbr &nb, const TeIpc &c, int n, int mode, int i, 
                   te_ipx(nb, c, n, mode, i, j + 3));
 }
 // the arrays and constants te_ipx reads, for the n x n block whose edges are in nb
+TE_FN TeIpc te_ipx_consts(const TeNbr &nb, int n) {  // (reads only)
+  uint32_t sum = 0;
+  for (int k = TE_LANE; k < n; k += TE_NL) sum += nb.left[k] + nb.top[k];
+  sum = te_sum(sum);
+  TeIpc c;
+  c.dc = ((int)sum + n) / (2 * n);
+  c.TL = nb.left[1] + 2 * nb.left[0] + 2 * nb.tl + 2 * nb.top[0] + nb.top[1];
+  c.tlF = (2 * nb.tl + nb.left[0] + nb.top[0] + 2) >> 2;
+  c.tFe = (nb.top[n - 2] + 3 * nb.top[n - 1] + 2) >> 2;
+  c.lFe = (nb.left[n - 2] + 3 * nb.left[n - 1] + 2) >> 2;
+  return c;
+}
 TE_FN TeIpc te_ipx_setup(TeNbr &nb, int n) {
   for (int k = TE_LANE; k < 2 * n; k += TE_NL) {
     // 1-2-1 filters of both edges over 2n (filter_121, common/intra_prediction.c:39-48)
@@ -408,17 +420,8 @@ TE_FN TeIpc te_ipx_setup(TeNbr &nb, int n) {
     else v = a[jj - 2] + 2 * a[jj - 1] + 2 * a[jj] + 2 * a[jj + 1] + a[jj + 2];
     (s ? nb.L : nb.T)[jj] = v;
   }
-  uint32_t sum = 0;
-  for (int k = TE_LANE; k < n; k += TE_NL) sum += nb.left[k] + nb.top[k];
-  sum = te_sum(sum);
-  TeIpc c;
-  c.dc = ((int)sum + n) / (2 * n);
-  c.TL = nb.left[1] + 2 * nb.left[0] + 2 * nb.tl + 2 * nb.top[0] + nb.top[1];
-  c.tlF = (2 * nb.tl + nb.left[0] + nb.top[0] + 2) >> 2;
-  c.tFe = (nb.top[n - 2] + 3 * nb.top[n - 1] + 2) >> 2;
-  c.lFe = (nb.left[n - 2] + 3 * nb.left[n - 1] + 2) >> 2;
   te_sync();
-  return c;
+  return te_ipx_consts(nb, n);
 }
 #endif
 
@@ -703,12 +706,17 @@ TE_FN int te_c8_code(int p, const uint8_t *org, int os, int qp, int16_t *coef, u
   return cbp;
 }
 TE_FN int te_enc_intra_c8(const uint8_t *org, int os, const uint8_t *rf, int fs, int ypos, int xpos, int qp,
-                          int16_t *coef, uint8_t *rec, int type, int mode, int ur, int dl) {
+                          int16_t *coef, uint8_t *rec, int type, int mode, int ur, int dl, int key) {
   TE_P(TP_INTRA_COMP);
   const TeScratch S = te_here();
   TeNbr &nbw = *S.nb;
-  te_make_top_and_left(nbw, rf, fs, nullptr, 0, 0, 0, ypos, xpos, 8, ur, dl, 0);
-  TeIpc c = te_ipx_setup(nbw, 8);
+  TeIpc c;
+  if (key && __builtin_amdgcn_readfirstlane(g_te_nb_key) == key) {  // the search just built them for this block
+    c = te_ipx_consts(nbw, 8);
+  } else {
+    te_make_top_and_left(nbw, rf, fs, nullptr, 0, 0, 0, ypos, xpos, 8, ur, dl, 0);
+    c = te_ipx_setup(nbw, 8);
+  }
   const TeNbr &nb = nbw;
   {  // DC of get_intra_prediction (position-aware, common/intra_prediction.c:145-160)
     int sl = 0, st = 0;
@@ -750,7 +758,7 @@ TE_FN int te_enc_inter_c4(const uint8_t *org, int os, int qp, const uint8_t *pb,
 #else
 TE_FN int te_enc_inter_c8(const uint8_t *, int, int, const uint8_t *, int16_t *, uint8_t *, int) { return 0; }
 TE_FN int te_enc_intra_c8(const uint8_t *, int, const uint8_t *, int, int, int, int, int16_t *, uint8_t *, int, int, int,
-                          int) {
+                          int, int) {
   return 0;
 }
 TE_FN int te_enc_inter_c4(const uint8_t *, int, int, const uint8_t *, int16_t *, uint8_t *, int) { return 0; }
@@ -834,15 +842,15 @@ TE_FN int te_encode_block_t(const TeFrame &F_, TeBits &b_, TeBlockInfo &bi_, TeP
 #define TE_INTRA_CHAINS(fn)                                                                                        \
   if (TE_C4 && size == 8 && !tb_split)                                                                             \
     cy = te_enc_intra_c8(oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, qpY, p.coeff, recY, itype | 0,   \
-                         p.intra_mode, ur, dl);                                                                    \
+                         p.intra_mode, ur, dl, te_nb_key(ypos, xpos, 8));                                          \
   else                                                                                                             \
     cy = fn(F, oY, F.osy, F.ry + ypos * F.rsy + xpos, F.rsy, ypos, xpos, size, qpY, S.pb, p.coeff, recY, itype | 0,  \
             tb_split, p.intra_mode, ur, dl, p.ts);                                                                 \
   if (TE_C4 && sC == 8 && !(tb_split && size > 8)) {                                                              \
     cu = te_enc_intra_c8(oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + p.cs, recU, itype | 1,     \
-                         p.intra_mode, ur, dl);                                                                    \
+                         p.intra_mode, ur, dl, 0);                                                                 \
     cv = te_enc_intra_c8(oV, F.osc, F.rv + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + 2 * p.cs, recV, itype | 1, \
-                         p.intra_mode, ur, dl);                                                                    \
+                         p.intra_mode, ur, dl, 0);                                                                 \
   } else if (TE_C4 && sC == 4) {                                                                                  \
     cu = te_enc_intra_c4(F, oU, F.osc, F.ru + yC * F.rsc + xC, F.rsc, yC, xC, qpC, p.coeff + p.cs, recU, itype | 1,  \
                          p.intra_mode, ur, dl);                                                                    \
@@ -1032,6 +1040,8 @@ TE_NOINL int te_search_intra(const TeFrame &F_, const TeBlockInfo &bi_, int num_
 #if !defined(TE_HOST)
   const TeNbr &nb = *S.nb;
   const TeIpc c = te_ipx_setup(*S.nb, size);
+  if (TE_LANE == 0) g_te_nb_key = te_nb_key(ypos, xpos, size);  // (te_intra_pred below forgets it, sizes 32 / 64)
+  te_sync();
   if (size == 8) {
     const int ch = TE_LANE & 15, row = TE_LANE >> 4, i = ch >> 1, j = (ch & 1) * 4;
     const uint32_t org = te_ld4(o + i * F.osy + j);
