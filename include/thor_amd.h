@@ -403,11 +403,12 @@ int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
  * window emptied, the sequence header due again): a server re-using a
  * context for the next clip of the same parameters. */
 int thor_enc_reset(thor_enc_t *e);
-/* Diagnostics only: superblock row `row` of every stream never reports its
- * progress (-1: off), and a WPP wait gives up after `spin_ms` milliseconds
- * (<= 0: the 5-minute default).  Each wave gives up at most once and then
- * waits no more, so the launch drains in bounded time and the call returns
- * THOR_ERR_HIP. */
+/* Diagnostics only: superblock row `row` of every stream never releases the
+ * row below it (-1: off) -- its SBs are coded, the next row's never become
+ * ready -- and a worker's wait for its next superblock gives up after
+ * `spin_ms` milliseconds (<= 0: the 5-minute default).  Each worker gives up
+ * at most once and then exits, so the launch drains in bounded time and the
+ * call returns THOR_ERR_HIP (the SBs never coded pack as nothing). */
 int thor_enc_debug_stall(int row, int spin_ms);
 
 /* ---- temporal interpolation: luma down-sampling pyramid ----------------- */

@@ -476,7 +476,7 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n, size_t nsb_tota
   return THOR_OK;
 }
 
-// diagnostics (thor_enc_debug_stall): the WPP wait bound and a row that never publishes
+// diagnostics (thor_enc_debug_stall): the scheduler's wait bound and a row that never releases the next
 // thor_enc_debug_stall's settings, read by every thor_enc_frames call: atomics,
 // so a call on another thread sees either the old or the new value, never a torn one
 static std::atomic<unsigned long long> g_spin_limit{30000000000ULL};  // s_memrealtime ticks (100 MHz): 5 minutes
@@ -585,8 +585,8 @@ int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords) {
   return THOR_OK;
 }
 
-// One context's frame job.  Its device setup (cell and progress resets) is
-// enqueued on the batch stream `st`; its header words go to `hw` (host), which
+// One context's frame job.  Its device setup (cells, SB dependency counters,
+// scheduler queue: k_enc_clear) runs on the batch stream `st`; its header words go to `hw` (host), which
 // the caller uploads with every context's in one copy to `hdr_dev`.
 static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob &J, TeFramePlan &pl, int &cur_slot,
                        hipStream_t st, uint32_t *hw, uint32_t *hdr_dev) {
@@ -675,7 +675,7 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
     if (hb.bytes[i >> 3] & (0x80 >> (i & 7))) hw[i >> 5] |= 0x80000000u >> (i & 31);
   J.hdr_bits = (int)hb.nbits;
   J.hdr_words = hdr_dev;
-  return THOR_OK;  // the cells and progress words are cleared by k_enc_clear (one launch for the batch)
+  return THOR_OK;  // the cells, SB dependency counters and queue are set up by k_enc_clear (one launch for the batch)
 }
 
 static thor_yuv_planes_t enc_slot_planes(const thor_enc *e, int slot) {
@@ -968,9 +968,9 @@ int thor_enc_reset(thor_enc_t *e) {
   return THOR_OK;
 }
 
-// Diagnostics: superblock row `row` of every stream never reports progress
-// (-1: off) and a WPP wait gives up after `spin_ms` (<= 0: the 5-minute
-// default), so the bounded-time failure path can be exercised.
+// Diagnostics: superblock row `row` of every stream never releases the row
+// below (-1: off) and a worker's wait for its next SB gives up after `spin_ms`
+// (<= 0: the 5-minute default), so the bounded-time failure path can be exercised.
 int thor_enc_debug_stall(int row, int spin_ms) {
   g_stall_row.store(row);
   g_spin_limit.store(spin_ms > 0 ? (unsigned long long)spin_ms * 100000ULL : 30000000000ULL);
