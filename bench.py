@@ -554,6 +554,206 @@ def roofline_pass(lib, decs, groups, devs, frames_of, seq, isteps):
     return stage_ms, recon_ms, alg, B, prep_ms
 
 
+ROWS_STREAM = "k4_med"  # BASELINE config 4: 4K config_LDB_medium_complexity, SB rows sharded across the GPUs
+
+
+def band_kernel_ms(lib, seq, frames, world: int, rank: int, reps: int = 3):
+    """Per-frame stage times (ms: prep, inter, intra, deblock, clpf, pad,
+    interp) of rank `rank`'s share of a `world`-way row split, run alone on
+    this GPU: a boundary-mode context (the band's k_frame_prep cells and TUs,
+    band k_recon, band intra chains, band-local deblock / CLPF, band pad) with
+    no exchange -- the rows outside the band are not final, so nothing is
+    checked; each kernel does exactly the band's work.  Also the wall time of
+    the rank's kernels per frame (one stream, host enqueue included)."""
+    from thor_amd.decoder import GpuDecoder
+    from thor_amd.shard import band_of
+
+    dec = GpuDecoder(seq)
+    try:
+        b0, b1 = band_of(seq.height, world, rank)
+        dec.set_band(b0, b1)
+        dec.set_band_local(True)
+        dec.set_band_intra(True)
+        dec.set_band_pad(True)
+        devs = [dec.upload(fr) for fr in frames]
+
+        def one():
+            for d in devs:
+                dec.begin(d)
+                dec.intra()
+                dec.end()
+                dec.finish()
+
+        one()
+        dec.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            one()
+        dec.sync()
+        wall = (time.perf_counter() - t0) / (reps * len(frames)) * 1e3
+        lib.thor_dec_set_timing(dec.h, 1)
+        ms = (C.c_double * 7)()
+        lib.thor_dec_stage_ms(dec.h, ms, 7)  # (clears)
+        for _ in range(reps):
+            one()
+        lib.thor_dec_stage_ms(dec.h, ms, 7)
+        lib.thor_dec_set_timing(dec.h, 0)
+        return [ms[i] / (reps * len(frames)) for i in range(7)], wall
+    finally:
+        dec.close()
+
+
+def rows_leg(torch, dist, rank: int, world: int, local: int, passes: int = 5):
+    """The north star's row split at this run's N (BASELINE config 4): ONE 4K
+    LDB-medium stream (tests/golden/k4_med.bit, the reference Thorenc's) decoded
+    by all ranks together, its SB rows in balanced bands (thor_amd/shard.py
+    boundary mode: band k_recon, band intra with edge rows from the band above,
+    8-row deblocking halos, band-local deblock / CLPF / pad, MV-reach halo
+    fetch of reference rows; point-to-point over RCCL, device buffers).
+    Strong scaling: the same stream whatever N.  Every frame is put together
+    from its band owners and md5-checked against the reference decoder after
+    the warmup pass and after the timed passes.  Returns the `rows` object
+    (rank 0) or None."""
+    from thor_amd import lib as L
+    from thor_amd.bitstream import parse_stream
+    from thor_amd.decoder import GpuDecoder
+    from thor_amd.shard import RowShard, band_of
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold, "streams.json")))[ROWS_STREAM]
+    seq, frames = parse_stream(open(os.path.join(gold, ROWS_STREAM + ".bit"), "rb").read())
+    own = dist is None
+    if own:  # a one-rank group keeps the same code path
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 300)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+    lib = L.load()
+    dec = GpuDecoder(seq, device=local)
+    dev = torch.device("cuda", local)
+    try:
+        sh = RowShard(dec, dist, seq.width, seq.height, device_exchange=True, band_local=True, halo=True,
+                      boundary=True)
+        devs = [dec.upload(fr) for fr in frames]
+
+        def step():
+            for d, fr in zip(devs, frames):
+                sh.decode(d, fr.frame_num, fr)
+
+        def check():
+            got = {fr.frame_num: sh.assemble(fr.frame_num) for fr in frames}
+            return hashlib.md5(b"".join(got[k] for k in sorted(got))).hexdigest() == meta["dec_md5"]
+
+        step()
+        torch.cuda.synchronize(local)
+        ok = check()
+        dist.barrier()
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            step()
+        torch.cuda.synchronize(local)
+        elapsed = time.perf_counter() - t0
+        dist.barrier()
+        ok &= check()
+        # this rank's kernel time per stage: one more pass with stage events on the decoder's stream
+        lib.thor_dec_set_timing(dec.h, 1)
+        ms = (C.c_double * 7)()
+        lib.thor_dec_stage_ms(dec.h, ms, 7)
+        step()
+        lib.thor_dec_stage_ms(dec.h, ms, 7)
+        lib.thor_dec_set_timing(dec.h, 0)
+        mine = torch.tensor([ms[i] / len(frames) for i in range(7)] + [float(sum(sh.boundary_bytes)),
+                                                                         float(sum(sh.halo_bytes))],
+                            dtype=torch.float64, device=dev)
+        every = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, ok = float(t[0].item()), t[1].item() == 0.0
+        every = [e.cpu().tolist() for e in every]
+    finally:
+        dec.close()
+        if own:
+            dist.destroy_process_group()
+    if rank != 0:
+        return None
+    nfr = len(frames) * passes
+    px = seq.width * seq.height
+    nbytes_frames = len(frames) * (passes + 2)  # the warmup, timed and stage passes
+    out = {
+        "workload": "BASELINE config 4: ONE 4K (3840x2160) config_LDB_medium_complexity stream (%s: %d frames, "
+                    "the reference Thorenc's .bit), SB rows in balanced bands over %d rank(s), boundary exchange "
+                    "over RCCL (thor_amd/shard.py): band k_recon + intra + deblock + CLPF + pad per rank, edge "
+                    "rows + 8-row deblocking halos + MV-reach reference halos point to point" % (
+                        ROWS_STREAM, len(frames), world),
+        "n_ranks": world,
+        "scaling": "strong",
+        "passes": passes,
+        "ms_per_frame": round(elapsed / nfr * 1e3, 4),
+        "mpx_s": round(px * nfr / elapsed / 1e6, 2),
+        "bit_exact": ok,
+        "bit_exact_scope": "every frame assembled from its band owners == the reference Thordec (md5 of the "
+                           "sequence), after the warmup pass and after the timed passes",
+        "bands_sb_rows": [list(band_of(seq.height, world, r)) for r in range(world)],
+        "per_rank_stage_ms_per_frame": [{k: round(v, 4) for k, v in zip(STAGES + ["interp"], e[:7])}
+                                        for e in every],
+        "per_rank_kernel_ms_per_frame": [round(sum(e[:7]), 4) for e in every],
+        "per_rank_exchange_kb_per_frame": [round((e[7] + e[8]) / nbytes_frames / 1e3, 1) for e in every],
+        "note": "ms_per_frame: wall clock of the timed passes, max over ranks, host parse excluded (resident "
+                "parse output), the exchange and its host-side protocol included",
+    }
+    if world == 1:  # the 8-way split's per-rank kernel work, each rank's band run alone on this GPU
+        per = [band_kernel_ms(lib, seq, frames, 8, r) for r in range(8)]
+        whole, wall1 = band_kernel_ms(lib, seq, frames, 1, 0)
+        t1, t8 = sum(whole), max(sum(p[0]) for p in per)
+        out["split8_on_one_gpu"] = {
+            "what": "each of the 8 ranks' bands decoded alone on this GPU (boundary-mode context, no exchange): "
+                    "per-rank kernel ms per frame, against the whole frame in the same mode",
+            "whole_frame_stage_ms": {k: round(v, 4) for k, v in zip(STAGES + ["interp"], whole)},
+            "whole_frame_kernel_ms": round(t1, 4),
+            "whole_frame_wall_ms": round(wall1, 4),
+            "rank_stage_ms": [{k: round(v, 4) for k, v in zip(STAGES + ["interp"], p[0])} for p in per],
+            "rank_kernel_ms": [round(sum(p[0]), 4) for p in per],
+            "rank_wall_ms": [round(p[1], 4) for p in per],
+            "kernel_speedup_bound": round(t1 / t8, 3) if t8 > 0 else None,
+            "wall_speedup_bound": round(wall1 / max(p[1] for p in per), 3),
+            "prep_ratio_max_rank_vs_whole": round(max(p[0][0] for p in per) / whole[0], 4) if whole[0] > 0 else None,
+        }
+    return out
+
+
+ROWS_TIMEOUT_S = 240
+
+
+def rows_guarded(a, torch, dist, rank, world, local, out):
+    """rows_leg on every rank under a watchdog: the row split's collectives
+    must not hang the streams measurement -- past ROWS_TIMEOUT_S rank 0 prints
+    `out` with a rows error and every rank exits."""
+    done = threading.Event()
+
+    def fire():
+        if done.is_set():
+            return
+        if rank == 0 and out is not None:
+            out["rows"] = {"error": "the rows leg did not finish within %d s" % ROWS_TIMEOUT_S}
+            print(json.dumps(out), flush=True)
+        os._exit(0)
+
+    tm = threading.Timer(ROWS_TIMEOUT_S, fire)
+    tm.daemon = True
+    tm.start()
+    try:
+        return rows_leg(torch, dist, rank, world, local, a.rows_passes)
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        progress("rows leg failed: %r" % (e,))
+        return {"error": repr(e)[:400]} if rank == 0 else None
+    finally:
+        done.set()
+        tm.cancel()
+
+
 def launch_ranks(n: int) -> int:
     """bench.py --gpus N run directly (no torch.distributed.run): start N ranks
     of this script, one per GPU, before anything here touches a GPU, with the
@@ -636,6 +836,8 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per k_recon launch (default tools/traffic_latest.json, "
                          "copied from profiles/<tag>_traffic.json by tools/prof_summary.py)")
+    ap.add_argument("--no-rows", action="store_true", help="skip the config-4 row-split leg (the `rows` object)")
+    ap.add_argument("--rows-passes", type=int, default=5, help="timed passes of the row-split leg's 8-frame stream")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
 
@@ -950,6 +1152,7 @@ def main():
     if os.path.exists(tj):
         traffic = json.load(open(tj)).get("recon_hbm_bytes_per_p_launch")
 
+    out = None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -1037,6 +1240,12 @@ def main():
                                         "object is k_recon, the north star's inter-reconstruction kernel",
             },
         }
+    if not a.no_rows:  # every rank: the north star's row split of ONE config-4 stream at this N
+        progress("rows leg: config 4 over %d rank(s)" % world)
+        rows = rows_guarded(a, torch, dist, rank, world, local, out)
+        if rank == 0:
+            out["rows"] = rows
+    if rank == 0:
         if world == 1 and not a.no_legs:
             progress("legs")
             out["encoder_tu_chain"] = encoder_leg(torch, lib)

@@ -151,7 +151,10 @@ typedef struct thor_frame_in {
   /* k_recon units (128x16 luma) that hold several (MV, reference) keys in a
    * half SB (thor_build_slow_list): dispatched first, so their long per-cell
    * path overlaps the planned units instead of forming the launch's tail.
-   * NULL: no list (every unit in planned order, same output). */
+   * When given, it must be exactly thor_build_slow_list's output for THIS
+   * frame's blocks: k_frame_prep then writes per-cell MC words only for the
+   * listed halves, and a multi-key half that is not listed is not
+   * reconstructed.  NULL: no list (every unit in planned order, same output). */
   const uint32_t *slow_list;
   int32_t n_slow;
 } thor_frame_in_t;
@@ -188,6 +191,11 @@ int thor_dec_put_rows(thor_dec_t *d, int frame_num, int y0, int nrows, const voi
  * rank's loop filters then cover 1/N of the frame instead of all of it. */
 int thor_dec_set_band_local(thor_dec_t *d, int on);
 int thor_dec_frame_finish(thor_dec_t *d);
+/* Band-local contexts whose frames are never whole on this rank (the halo and
+ * boundary exchanges of thor_amd/shard.py): thor_dec_frame_finish pads only
+ * the band's rows (the top / bottom pad rows only on the first / last band);
+ * a reference row fetched later is re-padded by thor_dec_pad_frame. */
+int thor_dec_set_band_pad(thor_dec_t *d, int on);
 /* Band-local intra (on = 1, with a band set; the boundary exchange of
  * thor_amd/shard.py, which replaces the pre-deblock all-gather): the intra
  * chains of the band's SB rows only, the first of them reading the row above
@@ -373,8 +381,9 @@ void *thor_enc_stream(thor_enc_t *e);
 int thor_enc_set_cu_mask(thor_enc_t *e, const uint32_t *mask, int nwords);
 /* Code the next frame of each of `n` DIFFERENT contexts (same device and
  * size, n <= 512) with one launch per stage.  Thread-safe: calls on the same
- * device are serialised (they share that device's work pool); a context must
- * not be used by two calls at once.  On THOR_ERR_HIP (a device error flag,
+ * device are serialised (they share that device's work pool; begin and end of
+ * one call run under one hold of its lock); a context must not be used by two
+ * calls at once.  On THOR_ERR_HIP (a device error flag,
  * e.g. a WPP wait that gave up) no context advances: the frame can be coded
  * again.  orig[i]: DEVICE pointer to the
  * context's input frame thor_enc_next_input(es[i]), planar I420, luma stride
@@ -383,13 +392,16 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
 /* thor_enc_frames in two halves, so the device codes the next frame while the
  * host collects the last one: _begin enqueues every stage of the batch and
  * advances the contexts (the next frame may be begun at once: up to two
- * batches in flight per device, a context's frames on one stream); _end waits
- * for the OLDEST batch begun (the same es / n), reads its coded words back and
- * makes them the contexts' chunks (thor_enc_frame_bytes).  On a device error
- * _end drops every batch in flight and returns the failed batch's contexts to
- * their state before it (that frame can be coded again; contexts only in a
- * later dropped batch must be reset).  thor_enc_reset / _destroy refuse /
- * drop a context with a batch in flight. */
+ * batches in flight per device, a context's frames on one stream; a frame with
+ * an interpolated reference waits for the batches in flight before its
+ * interpolation); _end waits for the oldest batch begun with exactly these
+ * contexts (the same es / n), reads its coded words back and makes them the
+ * contexts' chunks (thor_enc_frame_bytes).  On a device error _end drops every
+ * batch in flight and returns every dropped batch's contexts to their state
+ * before the oldest of them (those frames can be coded again).
+ * thor_enc_reset refuses a context with a batch in flight; thor_enc_destroy
+ * drops its batches and returns their other contexts to their state before
+ * them. */
 int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride);
 int thor_enc_frames_end(thor_enc_t *const *es, int n);
 int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride);
@@ -399,6 +411,17 @@ int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride);
 long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap);
 /* The last coded frame's reconstruction (deblocked, CLPF'd), host planes. */
 int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
+/* Per-superblock RD costs (parity instrumentation, tests/golden/rd_costs.npz):
+ * with on = 1 the context records, for every 64x64 superblock of each frame it
+ * codes from then on, the cost each top-level process_block call returns
+ * (enc/encode_frame.c:133-145) -- every delta-QP trial (qp - max_delta_qp ..
+ * qp + max_delta_qp in delta_qp_step steps), then the final encode; without
+ * delta QP the one call.  thor_enc_sb_costs copies the last ended frame's
+ * records (raster SB order, *per_sb int32 per SB) to dst (min(count, cap))
+ * and returns their count; call it before a later frame of the context is
+ * begun.  THOR_ERR_ARG when recording is off. */
+int thor_enc_record_sb_costs(thor_enc_t *e, int on);
+long long thor_enc_sb_costs(thor_enc_t *e, int32_t *dst, size_t cap, int *per_sb);
 /* Restart the context at the first frame of its sequence (the reference
  * window emptied, the sequence header due again): a server re-using a
  * context for the next clip of the same parameters. */

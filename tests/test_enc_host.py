@@ -39,3 +39,30 @@ def test_host_build_of_the_rd_source_matches_reference(enc_host, streams, tmp_pa
     got = out.read_bytes()
     want = open(os.path.join(ROOT, "tests", "golden", name + ".bit"), "rb").read()
     assert len(got) > 0 and want.startswith(got)
+
+
+@pytest.mark.parametrize("name,nframes", [("cif_low", 3), ("cif_high", 2)])
+def test_host_build_rd_costs_match_reference(enc_host, streams, tmp_path, name, nframes):
+    """The per-superblock RD costs of the shared RD source (te_encode_sb's cost
+    record: every delta-QP trial, then the final encode) == the reference
+    encoder's process_block returns (tests/golden/rd_costs.npz, recorded with
+    -Wl,--wrap=process_block), call by call.  cif_high: speed 0 with delta-QP
+    trials (qp - 1, qp, qp + 1) per superblock."""
+    import numpy as np
+
+    meta = streams[name]
+    w, h = meta["width"], meta["height"]
+    yuv = tmp_path / "in.yuv"
+    synth.synth_frames(w, h, nframes, meta["seed"], workers=1).tofile(yuv)
+    rd = tmp_path / "costs.bin"
+    subprocess.run([enc_host, "-if", str(yuv), "-of", str(tmp_path / "out.bit"), "-rdlog", str(rd)] +
+                   configs.flags(meta["config"], w, h, nframes, meta["extra"]), check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    got = np.fromfile(rd, dtype="<i4").reshape(-1, 6)
+    want = np.load(os.path.join(ROOT, "tests", "golden", "rd_costs.npz"))[name][:len(got)]
+    assert len(got) == len(want) and len(got) > 0
+    assert (got[:, :4] == want[:, :4]).all()
+    trial = got[:, 4] >= 0
+    assert (got[trial, 4] == want[trial, 4]).all()
+    bad = np.nonzero(got[:, 5] != want[:, 5])[0]
+    assert bad.size == 0, ("first differing call", want[bad[0]].tolist(), int(got[bad[0], 5]))

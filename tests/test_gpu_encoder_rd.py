@@ -23,6 +23,36 @@ def _frames(b):
     return out
 
 
+def _rd_frames(name):
+    """The reference encoder's per-superblock RD costs for `name`
+    (tests/golden/rd_costs.npz, tools/make_rd_goldens.py: -Wl,--wrap=process_block
+    on the reference Thorenc), grouped per coded frame in coding order: int32
+    rows (frame_num, size, ypos, xpos, qp, cost), one per top-level
+    process_block call -- every delta-QP trial, then the final encode -- in
+    raster SB order.  None when the stream has no RD golden."""
+    z = np.load(os.path.join("tests", "golden", "rd_costs.npz"))
+    if name not in z.files:
+        return None
+    r = z[name]
+    order = []
+    for f in r[:, 0]:
+        if not order or order[-1] != f:
+            order.append(int(f))
+    return [r[r[:, 0] == f] for f in order]
+
+
+def _check_rd(enc, want, i, name):
+    """Coded frame i's per-SB RD costs (thor_enc_sb_costs) == the reference's."""
+    if want is None or i >= len(want):
+        return
+    got = enc.sb_costs()
+    w = want[i]
+    assert got.size == len(w), (name, i, got.shape, len(w))
+    bad = np.nonzero(got.reshape(-1) != w[:, 5])[0]
+    assert bad.size == 0, (name, i, "first differing call (frame, size, y, x, qp, ref cost), device cost",
+                           w[bad[0]].tolist(), int(got.reshape(-1)[bad[0]]), "of", bad.size)
+
+
 def _input(meta, n):
     # serial: no fork from a process that has initialised the GPU
     return synth.synth_frames(meta["width"], meta["height"], n, meta["seed"], workers=1)
@@ -35,12 +65,16 @@ def test_device_encoder_matches_reference_bitstream(name, nframes, streams):
     meta = streams[name]
     p = params_for(meta["config"], meta["width"], meta["height"], nframes, meta["extra"])
     enc = GpuEncoder(p)
+    rd = _rd_frames(name)
     try:
         enc.upload_sequence(_input(meta, nframes))
+        if rd is not None:
+            enc.record_sb_costs()
         want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
         for i in range(enc.num_frames()):
             got = enc.encode_next()
             assert got == want[i], (name, i, len(got), len(want[i]))
+            _check_rd(enc, rd, i, name)
     finally:
         enc.close()
 
@@ -97,12 +131,16 @@ def test_device_encoder_more_configs(name, nframes, streams):
     meta = streams[name]
     p = params_for(meta["config"], meta["width"], meta["height"], nframes, meta["extra"])
     enc = GpuEncoder(p)
+    rd = _rd_frames(name)
     try:
         enc.upload_sequence(_input(meta, nframes))
+        if rd is not None:  # per-SB RD costs == the reference's (every delta-QP trial and final encode)
+            enc.record_sb_costs()
         want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
         for i in range(enc.num_frames()):
             got = enc.encode_next()
             assert got == want[i], (name, i, len(got), len(want[i]))
+            _check_rd(enc, rd, i, name)
     finally:
         enc.close()
 
@@ -147,8 +185,11 @@ def _encode_and_compare(name, nframes, streams, limit=None):
     meta = streams[name]
     p = params_for(meta["config"], meta["width"], meta["height"], nframes, meta["extra"])
     enc = GpuEncoder(p)
+    rd = _rd_frames(name)
     try:
         enc.upload_sequence(_input(meta, nframes))
+        if rd is not None:
+            enc.record_sb_costs()
         want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
         assert enc.num_frames() == len(want)
         for i in range(enc.num_frames() if limit is None else limit):
@@ -157,6 +198,7 @@ def _encode_and_compare(name, nframes, streams, limit=None):
             print("%s frame %d: %d bytes, %.2f s" % (name, i, len(got), time.perf_counter() - t0),
                   flush=True)  # progress (long speed-0 clips)
             assert got == want[i], (name, i, len(got), len(want[i]))
+            _check_rd(enc, rd, i, name)
     finally:
         enc.close()
 
@@ -241,3 +283,111 @@ def test_wpp_wait_gives_up_once_per_wave(streams):
     finally:
         lib.thor_enc_debug_stall(-1, 0)
         enc.close()
+
+
+def test_pipelined_batches_with_interpolated_references(streams):
+    """thor_enc_frames_begin / _end on a stream whose B frames interpolate a
+    reference from frames the previous batch is still filtering (HDB16 coding
+    order 0, 16, 8, ...: frame 8 interpolates from frame 16), two contexts --
+    the second on its own stream, so its interpolation must wait for the
+    pending batch -- byte-equal to the reference encoder."""
+    from thor_amd.encoder import GpuEncoder, encode_batch_begin, encode_batch_end, params_for
+
+    name = "cif_hdbi"
+    meta = streams[name]
+    nf = meta["frames"]
+    want = _frames(open("tests/golden/%s.bit" % name, "rb").read())
+    encs = []
+    try:
+        for _ in range(2):
+            e = GpuEncoder(params_for(meta["config"], meta["width"], meta["height"], nf, meta["extra"]))
+            e.upload_sequence(_input(meta, nf))
+            encs.append(e)
+        n = encs[0].num_frames()
+        got = [[] for _ in encs]
+        encode_batch_begin(encs)
+        for i in range(n):
+            if i + 1 < n:
+                encode_batch_begin(encs)
+            for k, ch in enumerate(encode_batch_end(encs)):
+                got[k].append(ch)
+        for k in range(len(encs)):
+            assert got[k] == want[:n], k
+    finally:
+        for e in encs:
+            e.close()
+
+
+def test_concurrent_enc_frames_calls_on_one_device(streams):
+    """thor_enc_frames from two threads at once (the GIL is released inside the
+    call): each call's begin and end run under one hold of the device pool's
+    lock, so neither thread's end meets the other's batch -- both
+    sequences byte-equal to the reference."""
+    import threading
+
+    from thor_amd.encoder import GpuEncoder, encode_batch, params_for
+
+    meta = streams["cif_low"]
+    want = _frames(open("tests/golden/cif_low.bit", "rb").read())
+    groups = []
+    try:
+        for _ in range(2):
+            g = []
+            for _ in range(2):
+                e = GpuEncoder(params_for(meta["config"], meta["width"], meta["height"], 10, meta["extra"]))
+                e.upload_sequence(_input(meta, 10))
+                g.append(e)
+            groups.append(g)
+        res, errs = [[] for _ in groups], []
+
+        def run(j):
+            try:
+                for _ in range(10):
+                    res[j].append(encode_batch(groups[j]))
+            except Exception as ex:  # pragma: no cover - reported below
+                errs.append(repr(ex))
+
+        ts = [threading.Thread(target=run, args=(j,)) for j in range(len(groups))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=100)
+        assert not errs, errs
+        for j in range(len(groups)):
+            assert len(res[j]) == 10
+            for i in range(10):
+                assert res[j][i] == [want[i]] * len(groups[j]), (j, i)
+    finally:
+        for g in groups:
+            for e in g:
+                e.close()
+
+
+def test_encoder_frame_wider_than_256_superblocks():
+    """A 16 448 x 64 frame (257 SB columns): the SB scheduler's queue items code
+    the SB column in 11 bits (8 bits spilled into the row field past
+    256 columns, so workers coded the wrong SB or waited until the spin limit).
+    The I frame must code without a device error, and its reconstruction must
+    equal the oracle decoder's reconstruction of the .bit it wrote."""
+    import ctypes as C
+
+    from oracle import OracleDecoder
+    from thor_amd.bitstream import parse_stream
+    from thor_amd.encoder import GpuEncoder, params_for
+
+    W, H = 16448, 64
+    p = params_for("config_LDB_low_complexity.txt", W, H, 1)
+    enc = GpuEncoder(p)
+    try:
+        enc.upload_sequence(synth.synth_frames(W, H, 1, 5, workers=1))
+        bits = enc.encode_next()
+        y = np.empty(W * H, np.uint8)
+        u = np.empty(W * H // 4, np.uint8)
+        v = np.empty(W * H // 4, np.uint8)
+        assert enc.lib.thor_enc_read_recon(enc.h, y.ctypes.data, u.ctypes.data, v.ctypes.data) == 0
+    finally:
+        enc.close()
+    seq, frames = parse_stream(bits)
+    assert len(frames) == 1 and seq.width == W
+    (fr, cur), = list(OracleDecoder(seq).run(frames))
+    assert cur.i420() == y.tobytes() + u.tobytes() + v.tobytes()

@@ -80,7 +80,9 @@ def test_row_sharded_decode_matches_reference(name, nframes, world, local):
 # MV-reach halo exchange (band-local, no second all-gather): every rank fetches only the
 # reference rows its band's vectors reach (thor_amd/shard.py halo mode)
 @pytest.mark.parametrize("name,nframes,world", [("k4_med", 8, 2), ("k4_med", 8, 3), ("cif_high", 10, 3),
-                                                ("hd_low", 6, 2), ("cif_hdbi", 9, 2)])
+                                                ("hd_low", 6, 2), ("cif_hdbi", 9, 2),
+                                                # the north star's 8-way split (BASELINE config 4)
+                                                ("k4_med", 8, 8)])
 def test_row_sharded_halo_exchange_matches_reference(name, nframes, world):
     _run_sharded(name, nframes, world, True, True)
 
@@ -89,7 +91,13 @@ def test_row_sharded_halo_exchange_matches_reference(name, nframes, world):
 # chains from the band above, 8 deblocking halo rows either side (thor_amd/shard.py)
 @pytest.mark.parametrize("name,nframes,world", [("k4_med", 8, 2), ("k4_med", 8, 3), ("k4_med", 8, 4),
                                                 ("cif_high", 10, 3), ("hd_low", 6, 2), ("cif_hdbi", 9, 2),
-                                                ("k4_hdbi", 9, 3)])
+                                                ("k4_hdbi", 9, 3),
+                                                # BASELINE config 4 at its stated partition: 4K LDB-medium,
+                                                # SB rows over 8 ranks (bands of 5, 5, 4 x 6 SB rows)
+                                                ("k4_med", 8, 8),
+                                                # config 5's stream (4K HDB16 high efficiency, interpolated
+                                                # references: both sources fetched whole) over 8 ranks
+                                                ("k4_hdbi_high", 9, 8)])
 def test_row_sharded_boundary_exchange_matches_reference(name, nframes, world):
     _run_sharded(name, nframes, world, True, True, True)
 
@@ -108,7 +116,7 @@ def _run_sharded(name, nframes, world, local, halo, boundary=False):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=110) for _ in procs)
+    res = sorted(q.get(timeout=110 if world < 8 else 240) for _ in procs)
     for p in procs:
         p.join(timeout=30)
     assert res == [(r, []) for r in range(world)], res
@@ -148,7 +156,8 @@ def test_row_shard_device_exchange_rccl(local):
 THREAD_CASES = [("k4_med", 8, 2, "gather"), ("cif_med", 10, 3, "gather"),
                 ("k4_med", 8, 3, "local"), ("cif_hdbi", 9, 2, "local"),
                 ("k4_med", 8, 3, "halo"), ("cif_high", 10, 3, "halo"), ("cif_hdbi", 9, 2, "halo"),
-                ("k4_med", 8, 4, "boundary"), ("k4_hdbi", 9, 3, "boundary"), ("hd_low", 6, 2, "boundary")]
+                ("k4_med", 8, 4, "boundary"), ("k4_hdbi", 9, 3, "boundary"), ("hd_low", 6, 2, "boundary"),
+                ("k4_med", 8, 8, "boundary")]
 
 
 def test_row_shard_device_exchange_threads():
@@ -158,7 +167,7 @@ def test_row_shard_device_exchange_threads():
     here = os.path.dirname(os.path.abspath(__file__))
     args = [",".join(map(str, c)) for c in THREAD_CASES]
     r = subprocess.run([sys.executable, "-u", os.path.join(here, "shard_threads_case.py")] + args, capture_output=True,
-                       text=True, timeout=240, cwd=os.path.dirname(here))
+                       text=True, timeout=300, cwd=os.path.dirname(here))
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert len(res) == len(THREAD_CASES), res

@@ -71,6 +71,9 @@ class NumpyContext:
     def set_band_local(self, on):
         self.local = on
 
+    def set_band_pad(self, on):  # halo modes: finish() pads only the band (nothing to model here)
+        self.band_pad = on
+
     def begin(self, fnum):  # the "device frame" is the frame number here
         if self.halo and fnum in self.frames:  # every reference row the band's vectors reach is final
             from thor_amd.shard import halo_requests

@@ -20,7 +20,7 @@ __global__ void k_intra(const FrameBatch, unsigned long long *, int);
 __global__ void k_deblock_v(const FrameBatch, int, int);
 __global__ void k_deblock_h(const FrameBatch, int, int);
 __global__ void k_clpf(const FrameBatch);
-__global__ void k_pad(const FrameBatch);
+__global__ void k_pad(const FrameBatch, int, int);
 
 #define HIPCHK(x)                                                                               \
   do {                                                                                          \
@@ -63,6 +63,7 @@ struct thor_dec {
   int band0, band1;    // SB rows k_recon reconstructs (row sharding); band1 0 = all
   int band_intra;      // row sharding: the intra chains of the band's rows only (thor_dec_set_band_intra)
   int band_local;      // phase B filters only the band's rows (thor_dec_set_band_local)
+  int band_pad;        // band-local: thor_dec_frame_finish pads only the band's rows (thor_dec_set_band_pad)
   void *pending;       // Batch of a thor_dec_frame_begin awaiting its _end (or, band-local, its _finish)
   int pending_ended;   // band-local: _end done, _finish (pad + commit) due
   // temporal-interpolated references (seq.interp_ref): slot `islot` after the
@@ -196,6 +197,7 @@ thor_dec_t *thor_dec_create(const thor_seq_t *seq, int device, int num_slots) {
   d->xev[0] = d->xev[1] = nullptr;
   d->band0 = d->band1 = 0;
   d->band_local = 0;
+  d->band_pad = 0;
   d->band_intra = 0;
   d->pending_ended = 0;
   d->pending = nullptr;
@@ -526,7 +528,7 @@ static int batch_interp(thor_dec_t *const *ds, const Batch &b) {
     fb.f[0].sc = d->sc;
     fb.f[0].W = d->seq.width;
     fb.f[0].H = d->seq.height;
-    k_pad<<<dim3((pad_chunks(d->seq.width, d->seq.height) + 255) / 256, 1), 256, 0, st>>>(fb);
+    k_pad<<<dim3((pad_chunks(d->seq.width, d->seq.height) + 255) / 256, 1), 256, 0, st>>>(fb, 0, 0);
     HIPCHK(hipGetLastError());
   }
   return THOR_OK;
@@ -606,7 +608,7 @@ static int batch_phase_b(thor_dec *lead, const Batch &b, int pad = 1) {
   }
   if (pad) {
     StageMark m(lead, ST_PAD);
-    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(b.fb);
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(b.fb, 0, 0);
     HIPCHK(hipGetLastError());
   }
   return THOR_OK;
@@ -665,6 +667,12 @@ int thor_dec_set_band_local(thor_dec_t *d, int on) {
   return THOR_OK;
 }
 
+int thor_dec_set_band_pad(thor_dec_t *d, int on) {
+  if (!d || d->pending) return THOR_ERR_ARG;
+  d->band_pad = on != 0;
+  return THOR_OK;
+}
+
 int thor_dec_set_band_intra(thor_dec_t *d, int on) {
   if (!d || d->pending) return THOR_ERR_ARG;
   d->band_intra = on != 0;
@@ -720,9 +728,12 @@ int thor_dec_frame_finish(thor_dec_t *d) {
   HIPCHK(hipSetDevice(d->device));
   const int W = d->seq.width, H = d->seq.height;
   int rc = THOR_OK;
-  {
+  // the whole frame, or (thor_dec_set_band_pad) only the band's rows -- the only ones final here
+  const FrameCtx &f = b->fb.f[0];
+  const int r0 = d->band_pad ? f.pb0 : 0, r1 = d->band_pad ? f.pb1 : 0;
+  if (!d->band_pad || r1 > r0) {
     StageMark m(d, ST_PAD);
-    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(b->fb);
+    k_pad<<<dim3((pad_chunks(W, H, r0, r1) + 255) / 256, 1), 256, 0, d->stream>>>(b->fb, r0, r1);
     if (hipGetLastError() != hipSuccess) rc = THOR_ERR_HIP;
   }
   thor_dec_t *ds[1] = {d};
@@ -914,7 +925,7 @@ int thor_dec_pad_frame(thor_dec_t *d, int frame_num) {
   hp->W = W;
   hp->H = H;
   HIPCHK(hipSetDevice(d->device));
-  k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(fb);
+  k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(fb, 0, 0);
   HIPCHK(hipGetLastError());
   return THOR_OK;
 }
@@ -941,7 +952,7 @@ int thor_dec_write_frame(thor_dec_t *d, int frame_num, const uint8_t *y, const u
     hp->sc = d->sc;
     hp->W = W;
     hp->H = H;
-    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(fb);
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, 1), 256, 0, d->stream>>>(fb, 0, 0);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipStreamSynchronize(d->stream));

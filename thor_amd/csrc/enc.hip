@@ -26,14 +26,14 @@
 #include <map>
 #include <mutex>
 
-#define THOR_ENC_MAX_BATCH 512
+#define THOR_ENC_MAX_BATCH 512  // te_q_item codes the job in 9 bits
 #define TE_MAX_WORKERS 4096  // k_enc_rows workgroups per launch (4 x 1 024 SIMDs)
 #define THOR_ENC_SB_WORDS 4096  // 131072 bits of one SB's stream (trial writes included)
 
 __global__ void k_deblock_v(const FrameBatch, int, int);
 __global__ void k_deblock_h(const FrameBatch, int, int);
 __global__ void k_clpf(const FrameBatch);
-__global__ void k_pad(const FrameBatch);
+__global__ void k_pad(const FrameBatch, int, int);
 
 // One stream's frame job (device memory, one per stream of a launch).
 struct TeJob {
@@ -50,6 +50,8 @@ struct TeJob {
   uint32_t *out_words;  // packed frame
   int *out_bits;
   int nsbh, nsbv, clpf;
+  int32_t *sb_costs;    // optional [nsb][cost_stride]: each SB's delta-QP trial costs, then its final cost
+  int cost_stride;
 };
 
 // Poll with a relaxed device-coherent load; the acquire fence follows once,
@@ -83,7 +85,10 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 #endif
 #define TE_WPE __attribute__((amdgpu_waves_per_eu(THOR_ENC_WPE)))
 #define TE_Q_EMPTY 0xffffffffu
-__device__ __forceinline__ unsigned te_q_item(int s, int k, int l) { return (unsigned)s << 16 | (unsigned)k << 8 | (unsigned)l; }
+// A queue item: job s (< THOR_ENC_MAX_BATCH = 512: 9 bits), SB row k and column l
+// (11 bits each: frames up to 65 535 px, te_check_params' limit, have <= 1 024
+// SB rows / columns).  The top bit stays clear, so no item equals TE_Q_EMPTY.
+__device__ __forceinline__ unsigned te_q_item(int s, int k, int l) { return (unsigned)s << 22 | (unsigned)k << 11 | (unsigned)l; }
 // (lane 0) one more finished dependency of SB (k, l) of job s; queue it when that was its last.
 // Relaxed atomics: the worker's release fence after its SB already wrote its
 // results back to device scope (every dependency's did, before its count), and
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     item = __builtin_amdgcn_readfirstlane(item);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const int s = (int)(item >> 16), k = (int)((item >> 8) & 255), l = (int)(item & 255);
+    const int s = (int)(item >> 22), k = (int)((item >> 11) & 2047), l = (int)(item & 2047);
     const TeJob &J = jobs[s];
     if (s != cur) {  // the job's frame parameters into LDS
       const uint32_t *src = (const uint32_t *)&J.F;
@@ -148,7 +153,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     const int sbi = k * J.nsbh + l;
     sb.bits.w = J.sb_words + (size_t)sbi * THOR_ENC_SB_WORDS;
     sb.bits.cap = THOR_ENC_SB_WORDS * 32;
-    te_encode_sb(s_F, sb, k, l);
+    te_encode_sb(s_F, sb, k, l, J.sb_costs ? J.sb_costs + (size_t)sbi * J.cost_stride : nullptr);
     if (lane == 0) {
       J.sb_nbits[sbi] = sb.bits.pos;
       if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
@@ -338,6 +343,8 @@ struct thor_enc {
   int opar;              // which of the two the next frame packs into
   int out_cap_words;
   int *out_bits;         // device
+  int32_t *sb_costs;     // device, thor_enc_record_sb_costs: per SB its top-level process_block costs
+  int cost_stride;       // per SB: the delta-QP trials + the final encode
   // last coded frame
   int last_slot, last_frame_num;
   std::vector<uint8_t> chunk;  // 4-byte length + bytes of the last frame
@@ -420,7 +427,6 @@ struct EncPool {
     std::vector<Snap> snap;
   };
   std::deque<Pending> pending;
-  int next_buf = 0;
 };
 static std::mutex g_pools_mu;
 static std::map<int, EncPool *> g_pools;
@@ -438,6 +444,22 @@ static EncPool &pool_for(int device) {
   EncPool *&p = g_pools[device];
   if (!p) p = new EncPool();
   return *p;
+}
+
+// A pending batch's contexts back to their state before it (except `skip`,
+// a context being destroyed).
+static void pending_restore(const EncPool::Pending &q, const thor_enc *skip) {
+  for (size_t i = 0; i < q.es.size(); i++) {
+    thor_enc *e = q.es[i];
+    if (e == skip) continue;
+    const EncPool::Pending::Snap &sn = q.snap[i];
+    e->pos = sn.pos;
+    e->first = sn.first;
+    e->last_slot = sn.last_slot;
+    e->last_frame_num = sn.last_frame_num;
+    e->opar = sn.opar;
+    e->slot_of_window = sn.window;
+  }
 }
 
 // (the caller holds P.mu and has made P's device current)
@@ -530,19 +552,20 @@ void thor_enc_destroy(thor_enc_t *e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->deps,
-                  e->clpf_bits, e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_words2, e->out_bits};
-  {  // a batch still pending with this context (begun, never ended) is dropped
+  void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->deps,   e->clpf_bits,
+                  e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_words2, e->out_bits, e->sb_costs};
+  {  // a batch still pending with this context (begun, never ended) is dropped; the
+     // batch's other contexts return to their state before it (newest batch first,
+     // so a context in two dropped batches ends at the older one's snapshot)
     EncPool &P = pool_for(e->device);
     std::lock_guard<std::mutex> lk(P.mu);
-    for (size_t b = 0; b < P.pending.size();) {
+    for (size_t b = P.pending.size(); b-- > 0;) {
       bool has = false;
       for (thor_enc *x : P.pending[b].es) has |= x == e;
       if (has) {
         (void)hipStreamSynchronize(P.pending[b].st);
+        pending_restore(P.pending[b], e);
         P.pending.erase(P.pending.begin() + b);
-      } else {
-        b++;
       }
     }
   }
@@ -665,6 +688,8 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   J.nsbh = e->nsbh;
   J.nsbv = e->nsbv;
   J.clpf = P.clpf;
+  J.sb_costs = e->sb_costs;
+  J.cost_stride = e->cost_stride;
   // header bits (sequence header before the first frame)
   TeHostBits hb;
   if (e->first) te_seq_header(hb, P);
@@ -704,7 +729,7 @@ static int enc_interp(thor_enc *e, const TeFramePlan &pl) {
   fb.f[0].sc = e->sc;
   fb.f[0].W = e->W;
   fb.f[0].H = e->H;
-  k_pad<<<dim3((pad_chunks(e->W, e->H) + 255) / 256, 1), 256, 0, e->stream>>>(fb);
+  k_pad<<<dim3((pad_chunks(e->W, e->H) + 255) / 256, 1), 256, 0, e->stream>>>(fb, 0, 0);
   EHIP(hipGetLastError());
   return THOR_OK;
 }
@@ -721,22 +746,27 @@ static int enc_interp(thor_enc *e, const TeFramePlan &pl) {
 // input frame thor_enc_next_input(es[i]) as planar I420 (luma stride
 // orig_stride[i], chroma stride / 2).  All contexts must share device and frame
 // size.  thor_enc_frames = begin + end.
-int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
+static int frames_args_ok(thor_enc_t *const *es, int n, const uint8_t *const *orig) {
   if (!es || !orig || n <= 0 || n > THOR_ENC_MAX_BATCH) return THOR_ERR_ARG;
   thor_enc *lead = es[0];
   for (int i = 0; i < n; i++) {
     if (!es[i] || !orig[i] || es[i]->device != lead->device || es[i]->W != lead->W || es[i]->H != lead->H)
       return THOR_ERR_ARG;
-    if (es[i]->pos >= es[i]->gop->plans.size()) return THOR_ERR_ARG;
     for (int j = 0; j < i; j++)
       if (es[j] == es[i]) return THOR_ERR_ARG;
   }
-  EHIP(hipSetDevice(lead->device));
+  return THOR_OK;
+}
+
+// thor_enc_frames_begin with P.mu held and the device current.
+static int frames_begin_locked(EncPool &P, thor_enc_t *const *es, int n, const uint8_t *const *orig,
+                               const int *orig_stride) {
+  thor_enc *lead = es[0];
+  for (int i = 0; i < n; i++)
+    if (es[i]->pos >= es[i]->gop->plans.size()) return THOR_ERR_ARG;
   const int W = lead->W, H = lead->H;
   const int nrows = lead->nsbv;
   const int nwork = n * nrows;
-  EncPool &P = pool_for(lead->device);
-  std::lock_guard<std::mutex> pool_lock(P.mu);
   if (P.pending.size() >= 2) return THOR_ERR_ARG;  // end the oldest batch first
   for (const EncPool::Pending &q : P.pending)
     for (thor_enc *x : q.es)
@@ -764,10 +794,14 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
       return rc;
   }
   EHIP(hipMemcpyAsync(P.hdr_all, hdr.data(), hdr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  // interpolated references: each context's on its own stream (they overlap), all done before the RD loop
+  // interpolated references: each context's on its own stream (they overlap), all done before the RD loop;
+  // each after every pending batch (their loop filters still write the slots the interpolation reads,
+  // their RD loops may still read the interpolation slot it overwrites)
   bool any_interp = false;
   for (int i = 0; i < n; i++)
     if (plans[i].interp_ref) {
+      for (const EncPool::Pending &q : P.pending)
+        if (q.st != es[i]->stream) EHIP(hipStreamWaitEvent(es[i]->stream, P.ev[q.buf], 0));
       if ((rc = enc_interp(es[i], plans[i])) != THOR_OK) return rc;
       any_interp = true;
     }
@@ -833,14 +867,16 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
       k_clpf<<<dim3(lead->nsb_full, m), 256, 0, st>>>(fb);
       EHIP(hipGetLastError());
     }
-    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, m), 256, 0, st>>>(fb);
+    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, m), 256, 0, st>>>(fb, 0, 0);
     EHIP(hipGetLastError());
   }
   k_enc_pack<<<n, 256, 0, st>>>(P.jobs, P.scan, lead->out_cap_words);
   EHIP(hipGetLastError());
-  // the bit counts in one copy into pinned memory, an event behind it
-  const int buf = P.next_buf;
-  P.next_buf ^= 1;
+  // the bit counts in one copy into pinned memory, an event behind it: in the
+  // buffer no pending batch holds (at most one is pending here)
+  int buf = 0;
+  for (const EncPool::Pending &q : P.pending)
+    if (q.buf == 0) buf = 1;
   int *nb_dev = P.nb_all + buf * THOR_ENC_MAX_BATCH, *nb_host = P.nb_host + buf * THOR_ENC_MAX_BATCH;
   k_enc_nbits<<<1, 512, 0, st>>>(P.jobs, n, nb_dev);
   EHIP(hipGetLastError());
@@ -870,20 +906,31 @@ int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *or
   return THOR_OK;
 }
 
-// End the oldest batch begun on these contexts (es / n as passed to the begin).
-// On a device error (e.g. a WPP wait that gave up) every pending batch is
-// dropped and the contexts return to their state before the failed one: that
-// frame can be coded again.
-int thor_enc_frames_end(thor_enc_t *const *es, int n) {
-  if (!es || n <= 0) return THOR_ERR_ARG;
+int thor_enc_frames_begin(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
+  int rc = frames_args_ok(es, n, orig);
+  if (rc != THOR_OK) return rc;
   EHIP(hipSetDevice(es[0]->device));
   EncPool &P = pool_for(es[0]->device);
   std::lock_guard<std::mutex> pool_lock(P.mu);
-  if (P.pending.empty() || (int)P.pending.front().es.size() != n) return THOR_ERR_ARG;
-  for (int i = 0; i < n; i++)
-    if (P.pending.front().es[i] != es[i]) return THOR_ERR_ARG;
-  EncPool::Pending q = std::move(P.pending.front());
-  P.pending.pop_front();
+  return frames_begin_locked(P, es, n, orig, orig_stride);
+}
+
+// thor_enc_frames_end with P.mu held and the device current: the oldest pending
+// batch of exactly these contexts (es / n as passed to its begin).  On a device
+// error (e.g. a WPP wait that gave up) every pending batch is dropped and the
+// contexts return to their state before the failed one: that frame can be
+// coded again.
+static int frames_end_locked(EncPool &P, thor_enc_t *const *es, int n) {
+  size_t qi = 0;
+  for (; qi < P.pending.size(); qi++) {
+    const EncPool::Pending &c = P.pending[qi];
+    bool same = (int)c.es.size() == n;
+    for (int i = 0; same && i < n; i++) same = c.es[i] == es[i];
+    if (same) break;
+  }
+  if (qi == P.pending.size()) return THOR_ERR_ARG;
+  EncPool::Pending q = std::move(P.pending[qi]);
+  P.pending.erase(P.pending.begin() + qi);
   hipStream_t st = q.st;
   EHIP(hipEventSynchronize(P.ev[q.buf]));
   const int *nbits = P.nb_host + q.buf * THOR_ENC_MAX_BATCH;
@@ -891,21 +938,15 @@ int thor_enc_frames_end(thor_enc_t *const *es, int n) {
   EHIP(hipMemcpy(&err, P.err, sizeof(unsigned), hipMemcpyDeviceToHost));
   bool bad = err != 0;
   for (int i = 0; i < n && !bad; i++) bad = nbits[i] < 0;
-  if (bad) {  // drop what is in flight, restore the contexts to before this batch
+  if (bad) {  // drop what is in flight, restore the contexts to before this batch (and the other pending ones)
     EHIP(hipStreamSynchronize(st));
     for (const EncPool::Pending &r : P.pending) EHIP(hipStreamSynchronize(r.st));
     std::deque<EncPool::Pending> later;
     later.swap(P.pending);
-    for (int i = 0; i < n; i++) {
-      thor_enc *e = q.es[i];
-      const EncPool::Pending::Snap &sn = q.snap[i];
-      e->pos = sn.pos;
-      e->first = sn.first;
-      e->last_slot = sn.last_slot;
-      e->last_frame_num = sn.last_frame_num;
-      e->opar = sn.opar;
-      e->slot_of_window = sn.window;
-    }
+    // newest first, so a context in several batches ends at its oldest snapshot (q was at index qi)
+    for (size_t b = later.size(); b-- > qi;) pending_restore(later[b], nullptr);
+    pending_restore(q, nullptr);
+    for (size_t b = qi; b-- > 0;) pending_restore(later[b], nullptr);
     if (err) {
       fprintf(stderr, "thor_amd enc: device error flags 0x%x\n", err);
       EHIP(hipMemset(P.err, 0, 4));
@@ -942,10 +983,24 @@ int thor_enc_frames_end(thor_enc_t *const *es, int n) {
   return THOR_OK;
 }
 
+int thor_enc_frames_end(thor_enc_t *const *es, int n) {
+  if (!es || n <= 0 || !es[0]) return THOR_ERR_ARG;
+  EHIP(hipSetDevice(es[0]->device));
+  EncPool &P = pool_for(es[0]->device);
+  std::lock_guard<std::mutex> pool_lock(P.mu);
+  return frames_end_locked(P, es, n);
+}
+
+// begin + end under one hold of the pool lock: a concurrent call on another
+// thread cannot interleave its batch between this call's two halves.
 int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, const int *orig_stride) {
-  const int rc = thor_enc_frames_begin(es, n, orig, orig_stride);
+  int rc = frames_args_ok(es, n, orig);
   if (rc != THOR_OK) return rc;
-  return thor_enc_frames_end(es, n);
+  EHIP(hipSetDevice(es[0]->device));
+  EncPool &P = pool_for(es[0]->device);
+  std::lock_guard<std::mutex> pool_lock(P.mu);
+  if ((rc = frames_begin_locked(P, es, n, orig, orig_stride)) != THOR_OK) return rc;
+  return frames_end_locked(P, es, n);
 }
 
 int thor_enc_reset(thor_enc_t *e) {
@@ -988,6 +1043,41 @@ long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap) {
   if (!e) return THOR_ERR_ARG;
   if (dst) memcpy(dst, e->chunk.data(), e->chunk.size() < cap ? e->chunk.size() : cap);
   return (long long)e->chunk.size();
+}
+
+// Per-superblock RD costs (parity instrumentation): from the next frame on,
+// every SB's top-level process_block costs go to a device buffer (on = 1).
+int thor_enc_record_sb_costs(thor_enc_t *e, int on) {
+  if (!e) return THOR_ERR_ARG;
+  EHIP(hipSetDevice(e->device));
+  EHIP(hipStreamSynchronize(e->stream));
+  if (!on) {
+    if (e->sb_costs) EHIP(hipFree(e->sb_costs));
+    e->sb_costs = nullptr;
+    return THOR_OK;
+  }
+  if (e->sb_costs) return THOR_OK;
+  // encode_frame's trial loop (enc/encode_frame.c:133): qp - d .. qp + d in steps of delta_qp_step
+  const int d = e->p.max_delta_qp, step = e->p.delta_qp_step > 0 ? e->p.delta_qp_step : 1;
+  e->cost_stride = (d ? (2 * d) / step + 1 : 0) + 1;
+  EHIP(hipMalloc(&e->sb_costs, (size_t)e->nsb * e->cost_stride * sizeof(int32_t)));
+  EHIP(hipMemset(e->sb_costs, 0, (size_t)e->nsb * e->cost_stride * sizeof(int32_t)));
+  return THOR_OK;
+}
+
+// The last ended frame's per-SB costs (raster SB order, cost_stride int32 per
+// SB: the delta-QP trials in order, then the final encode).  Returns the count
+// (nsb x per_sb), copies min(count, cap); *per_sb = cost_stride.
+long long thor_enc_sb_costs(thor_enc_t *e, int32_t *dst, size_t cap, int *per_sb) {
+  if (!e || !e->sb_costs) return THOR_ERR_ARG;
+  const size_t n = (size_t)e->nsb * e->cost_stride;
+  if (per_sb) *per_sb = e->cost_stride;
+  if (dst && cap) {
+    EHIP(hipSetDevice(e->device));
+    EHIP(hipDeviceSynchronize());
+    EHIP(hipMemcpy(dst, e->sb_costs, (n < cap ? n : cap) * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  return (long long)n;
 }
 
 // The reconstruction of the last coded frame (deblocked, CLPF'd), host planes.

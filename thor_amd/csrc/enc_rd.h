@@ -2629,7 +2629,11 @@ TE_FN uint32_t te_process_block_b(const TeFrame &F_, TeSB &sb_, int ypos, int xp
 // the ME candidate lists, then process_block(64) -- with the delta-qp RD
 // search when max_delta_qp is set (trials leave their candidates behind, as
 // there).  Returns the SB's bit count in sb.bits.
-TE_FN void te_encode_sb(const TeFrame &F, TeSB &sb, int k, int l) {
+// costs (optional, nullptr: off): the returned cost of each top-level
+// process_block call of the SB -- every delta-QP trial in order, then the final
+// encode (enc/encode_frame.c:133-145) -- for the per-SB RD-cost parity check
+// (thor_enc_sb_costs, tests/golden/rd_costs.npz).
+TE_FN void te_encode_sb(const TeFrame &F, TeSB &sb, int k, int l, int32_t *costs = nullptr) {
   TE_P(TP_SB);
   const int ypos = k * 64, xpos = l * 64;
   for (int r = 0; r < F.num_ref; r++) {
@@ -2640,18 +2644,22 @@ TE_FN void te_encode_sb(const TeFrame &F, TeSB &sb, int k, int l) {
   te_bits_start(sb.bits);
   if (F.max_delta_qp) {
     int min_cost = 1 << 30, best_qp = F.qp;
-    for (int q = F.qp - F.max_delta_qp; q <= F.qp + F.max_delta_qp; q += F.delta_qp_step) {
+    int t = 0;
+    for (int q = F.qp - F.max_delta_qp; q <= F.qp + F.max_delta_qp; q += F.delta_qp_step, t++) {
       const int cost = (int)te_process_block<64>(F, sb, ypos, xpos, q);
       TE_TR(F.frame_num, 6, ypos, xpos, q, cost, 0, 0);
+      if (costs && TE_LANE == 0) costs[t] = cost;
       if (cost < min_cost) {
         min_cost = cost;
         best_qp = q;
       }
     }
     te_rewind(sb.bits, 0);
-    te_process_block<64>(F, sb, ypos, xpos, best_qp);
+    const int cost = (int)te_process_block<64>(F, sb, ypos, xpos, best_qp);
+    if (costs && TE_LANE == 0) costs[t] = cost;
   } else {
-    te_process_block<64>(F, sb, ypos, xpos, F.qp);
+    const int cost = (int)te_process_block<64>(F, sb, ypos, xpos, F.qp);
+    if (costs && TE_LANE == 0) costs[0] = cost;
   }
   te_bits_flush(sb.bits);
 }

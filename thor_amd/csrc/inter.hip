@@ -954,10 +954,18 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
   const bool bex = 2 * pr + 1 < sbw;  // the pair's right SB exists
   const bool last = qtr == 3;         // the unit holds SB row 63: the edge rows k_intra reads
 
-  // ---- fast path: both halves planned (k_frame_prep: one 64x64 inter CU, one
-  // key per pass) -- no per-cell resolution (P0): scalar loads, then straight
-  // to the window staging ----
-  if (f.hplan && !listed) {
+  // ---- fast path: the unit's planned halves (k_frame_prep: one 64x64 inter
+  // CU, one key per pass) -- no per-cell resolution (P0): scalar loads, then
+  // straight to the window staging ----
+  // The halves' plan records: current (tag == gen) and planned, current and
+  // tagged multi-key (PLAN_SLOW), or not current -- with a slow list, a half
+  // with no inter pixels (intra only, or below the frame).  With a list, the
+  // planned-order workgroup reconstructs the unit's planned halves (a multi-key
+  // or empty neighbour half is masked) and the list's workgroup the multi-key
+  // halves on the per-cell path (the planned neighbour masked); without one,
+  // a unit whose two halves are not both planned takes the per-cell path whole.
+  bool keep_a = true, keep_b = true;  // per-cell path: the halves whose cells it reconstructs
+  if (f.hplan) {
     typedef unsigned u32x16 __attribute__((ext_vector_type(16)));
     u32x16 pv;  // plans of halves hsb and hsb + 2 (scalar, uniform loads through the constant cache)
     const int hsb = 2 * (sby * sbw + 2 * pr) + h;
@@ -965,12 +973,27 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
     STAMP(1);
     const uint4 pa = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 pb = bex ? make_uint4(pv[8], pv[9], pv[10], pv[11]) : pa;
-    const bool cura = (int)pa.w == f.gen, curb = (int)pb.w == f.gen;
-    if ((cura && (pa.y & PLAN_SLOW)) || (curb && (pb.y & PLAN_SLOW))) return;  // a slow-list block has it
-    if (cura && curb) {
+    const bool cura = (int)pa.w == f.gen, curb = bex && (int)pb.w == f.gen;
+    const bool sla = cura && (pa.y & PLAN_SLOW), slb = curb && (pb.y & PLAN_SLOW);
+    bool doa, dob;  // halves this workgroup reconstructs on the planned path
+    if (f.slow) {
+      if (listed) {
+        keep_a = sla;
+        keep_b = slb;
+        doa = dob = false;
+      } else {
+        doa = cura && !sla;
+        dob = curb && !slb;
+        if (!doa && !dob) return;  // nothing planned: empty, or the list's workgroup has it
+      }
+    } else {
+      doa = cura && (curb || !bex);
+      dob = doa && bex;
+    }
+    if (doa || dob) {
       const __amdgpu_buffer_rsrc_t ring =
           __builtin_amdgcn_make_buffer_rsrc((void *)f.slots, 0, (int)f.ring_bytes, 0x00020000);
-      const unsigned ma = pa.y, mb = pb.y;
+      const unsigned ma = doa ? pa.y : 0u, mb = dob ? pb.y : 0u;
 #if RECON_RES_PREFETCH
       if ((ma | mb) & (CELL_RES(0) | CELL_RES(1) | CELL_RES(2))) {
         // The unit's residual lines into L2 now, so the reads after the filter
@@ -996,11 +1019,11 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
       {  // pass 0: mv0 (one window when both SBs share the key, else one per SB)
         const Key KA = make_key((int)pa.x, (int)(ma & 255)), KB = make_key((int)pb.x, (int)(mb & 255));
         STAMP(2);
-        if (KA.mv == KB.mv && KA.slot == KB.slot) {
+        if (doa && dob && KA.mv == KB.mv && KA.slot == KB.slot) {
           plan_pass(L, f, ring, KA, x0, y0, ly, lc, false, true);
         } else {
-          plan_pass(L, f, ring, KA, x0, y0, ly, lc, false, mine_a);
-          plan_pass(L, f, ring, KB, x0, y0, ly, lc, false, !mine_a);
+          if (doa) plan_pass(L, f, ring, KA, x0, y0, ly, lc, false, mine_a);
+          if (dob) plan_pass(L, f, ring, KB, x0, y0, ly, lc, false, !mine_a);
         }
         STAMP(4);
       }
@@ -1078,15 +1101,16 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
 #if RECON_PROBE == 3  // timing probe: no pixel stores (wrong output)
       if (f.W > 0) return;
 #endif
-      if (bex || !(lane & 4)) {
+      const bool sty = (lane & 4) ? dob : doa, stc = (lane & 2) ? dob : doa;  // the lane's chunks' halves are ours
+      if (sty) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, py0), cur, oy, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, py1), cur, oy, 8 * f.sy, 0);
       }
-      if (bex || !(lane & 2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pc), cur, oc, 0, 0);
+      if (stc) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pc), cur, oc, 0, 0);
       if (last) {  // SB row 63 / chroma SB row 31: the edge rows k_intra's next SB row reads
-        if (r == 7 && y0 + 15 < f.H && xl < f.W)
+        if (sty && r == 7 && y0 + 15 < f.H && xl < f.W)
           *(uint4 *)(f.edge + (long long)sby * f.ewy + EDGE_MARGIN + xl) = py1;
-        if (rc == 7 && yc < (f.H >> 1) && xcl < (f.W >> 1))
+        if (stc && rc == 7 && yc < (f.H >> 1) && xcl < (f.W >> 1))
           *(uint4 *)(f.edge + (long long)f.nsbrows * f.ewy + (long long)(pl1 * f.nsbrows + sby) * f.ewc + EDGE_MARGIN +
                      xcl) = pc;
       }
@@ -1115,7 +1139,7 @@ __global__ __launch_bounds__(64, RECON_WPE) void k_recon(const FrameBatch fb_, c
   const int lrow = 2 * ur + cr;  // cell row inside the unit
   uint4 mc = make_uint4(0, 0, 0, 0);
   const int cidx = ((uy >> 2) + cr) * cs + (ux >> 2);
-  if (uy < f.H && ux < f.W) mc = *(const uint4 *)&f.cellmc[cidx];
+  if (uy < f.H && ux < f.W && (uc < 8 ? keep_a : keep_b)) mc = *(const uint4 *)&f.cellmc[cidx];
   bool inter = false, bi_any = false;
 #pragma unroll
   for (int c = 0; c < 2; c++) {

@@ -642,8 +642,13 @@ __global__ __launch_bounds__(256) void k_frame_prep(const FrameBatch fb_) {
   if (f.nblocks <= 0) return;
   if (b < f.nprep) prep_body(b, f);
   else if (b < f.nprep + f.nres) {
-    const int w = threadIdx.x >> 6;
-    resid_tu(RL[w], (b - f.nprep) * 4 + w, f.tus, f.ntus, f.coeffs, f.resid, f.W, f.H);
+    const int w = threadIdx.x >> 6, idx = (b - f.nprep) * 4 + w;
+    if (f.ir1 > 0 && idx < f.ntus) {  // band-local intra (row sharding): only the band's rows are reconstructed here
+      const thor_tu_t T = f.tus[idx];
+      const int y = T.comp ? 2 * T.y : T.y, n = T.comp ? 2 * T.size : T.size;
+      if (y + n <= 64 * f.ir0 || y >= 64 * f.ir1) return;
+    }
+    resid_tu(RL[w], idx, f.tus, f.ntus, f.coeffs, f.resid, f.W, f.H);
   } else if (b == f.nprep + f.nres && f.nintra > 0) {
     intra_setup_body(f.blk, f.ilist, f.nintra, f.ctl, f.progress, f.rowstart, f.nsbrows);
   }

@@ -443,15 +443,20 @@ __global__ __launch_bounds__(256) void k_clpf(const FrameBatch fb_) {
 // edge keeps its interior bytes), then the top / bottom pad rows over
 // [-pad, w + pad) rounded up to 16 (still inside the stride).  Rows start
 // 16-byte aligned at x = -pad (create_yuv_frame's strides and pads).
+// Row sharding pads only the rows a rank holds final: interior rows [r0, r1),
+// the top pad rows when r0 == 0 and the bottom ones when r1 == h (the whole
+// plane: r0 = 0, r1 = h).
 struct PadPlane {
   uint8_t *P;
-  int s, w, h, pad, nl, nr, rc, sides, total;
-  __device__ __forceinline__ PadPlane(uint8_t *P_, int s_, int w_, int h_, int pad_) : P(P_), s(s_), w(w_), h(h_), pad(pad_) {
+  int s, w, h, pad, nl, nr, rc, r0, ntop, sides, total;
+  __device__ __forceinline__ PadPlane(uint8_t *P_, int s_, int w_, int h_, int pad_, int r0_, int r1_)
+      : P(P_), s(s_), w(w_), h(h_), pad(pad_), r0(r0_) {
     nl = pad >> 4;
     nr = (w + pad - (w & ~15) + 15) >> 4;
     rc = (w + 2 * pad + 15) >> 4;
-    sides = h * (nl + nr);
-    total = sides + 2 * pad * rc;
+    sides = (r1_ - r0_) * (nl + nr);
+    ntop = r0_ == 0 ? pad : 0;
+    total = sides + (ntop + (r1_ == h ? pad : 0)) * rc;
   }
   __device__ __forceinline__ void chunk(int e) const {
     int row, x0;
@@ -459,13 +464,14 @@ struct PadPlane {
     if (e < sides) {
       row = e / (nl + nr);
       const int k = e - row * (nl + nr);
+      row += r0;
       src = P + (long long)row * s;
       x0 = k < nl ? -pad + 16 * k : (w & ~15) + 16 * (k - nl);
     } else {
       const int e2 = e - sides, r = e2 / rc;
       x0 = -pad + 16 * (e2 - r * rc);
-      row = r < pad ? r - pad : h + (r - pad);
-      src = P + (long long)(r < pad ? 0 : h - 1) * s;
+      row = r < ntop ? r - pad : h + (r - ntop);
+      src = P + (long long)(r < ntop ? 0 : h - 1) * s;
     }
     uint8_t *dst = P + (long long)row * s + x0;
     uint4 v;
@@ -492,33 +498,38 @@ struct PadPlane {
     *(uint4 *)dst = v;
   }
 };
-__device__ __forceinline__ void k_pad_body(int e, uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H) {
-  const PadPlane py(Y, sy, W, H, THOR_PAD_Y);
+__device__ __forceinline__ void k_pad_body(int e, uint8_t *Y, uint8_t *U, uint8_t *V, int sy, int sc, int W, int H,
+                                           int r0, int r1) {
+  const PadPlane py(Y, sy, W, H, THOR_PAD_Y, r0, r1);
   if (e < py.total) {
     py.chunk(e);
     return;
   }
   e -= py.total;
-  const PadPlane pu(U, sc, W >> 1, H >> 1, THOR_PAD_C);
+  const PadPlane pu(U, sc, W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
   if (e < pu.total) {
     pu.chunk(e);
     return;
   }
   e -= pu.total;
-  const PadPlane pv(V, sc, W >> 1, H >> 1, THOR_PAD_C);
+  const PadPlane pv(V, sc, W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
   if (e < pv.total) pv.chunk(e);
 }
-// every frame of a batch (grid z); also used on one frame by thor_dec_write_frame
-__global__ __launch_bounds__(256) void k_pad(const FrameBatch fb_) {
+// every frame of a batch (grid z); also used on one frame by thor_dec_write_frame.
+// Luma rows [r0, r1) of each frame (even; r1 <= 0: the whole frame).
+__global__ __launch_bounds__(256) void k_pad(const FrameBatch fb_, int r0, int r1) {
   const FrameCtx *__restrict__ F = FRAME_BATCH_CTX();
   const FrameCtx &f = F[blockIdx.y];
-  k_pad_body(blockIdx.x * 256 + threadIdx.x, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H);
+  if (r1 <= 0) r0 = 0, r1 = f.H;
+  k_pad_body(blockIdx.x * 256 + threadIdx.x, f.cy, f.cu, f.cv, f.sy, f.sc, f.W, f.H, r0, r1);
 }
-// 16-byte chunks of padding of one frame (host-side copy of PadPlane's count)
-static inline int pad_chunks(int W, int H) {
-  auto plane = [](int w, int h, int pad) {
+// 16-byte chunks of padding of one frame (host-side copy of PadPlane's count),
+// luma rows [r0, r1) (r1 <= 0: all)
+static inline int pad_chunks(int W, int H, int r0 = 0, int r1 = 0) {
+  if (r1 <= 0) r0 = 0, r1 = H;
+  auto plane = [](int w, int h, int pad, int a, int b) {
     const int nl = pad >> 4, nr = (w + pad - (w & ~15) + 15) >> 4, rc = (w + 2 * pad + 15) >> 4;
-    return h * (nl + nr) + 2 * pad * rc;
+    return (b - a) * (nl + nr) + ((a == 0 ? pad : 0) + (b == h ? pad : 0)) * rc;
   };
-  return plane(W, H, THOR_PAD_Y) + 2 * plane(W >> 1, H >> 1, THOR_PAD_C);
+  return plane(W, H, THOR_PAD_Y, r0, r1) + 2 * plane(W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
 }

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void k_down_pyramid(const int ss, int W, int H
 __global__ __launch_bounds__(256) void k_pad_pyramid(const PyrJob J) {
   const PyrLevels &L = J.L[blockIdx.z];
   const int l = blockIdx.y;
-  const PadPlane p(L.y[l], L.s[l], L.w[l], L.h[l], THOR_PYR_PAD);
+  const PadPlane p(L.y[l], L.s[l], L.w[l], L.h[l], THOR_PYR_PAD, 0, L.h[l]);
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e < p.total) p.chunk(e);
 }

@@ -30,6 +30,11 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   const thor_block_t &B = f.blk[b];
   int S = B.size;
   int mode = B.mode;
+  // Band-local loop filters (row sharding, pb1 > 0): the cells of luma rows
+  // [pb0 - 8, pb1 + 8) are all anyone here reads -- the band's deblocking with
+  // its 8-row halo groups, its CLPF, its k_recon units -- so CUs wholly outside
+  // them write nothing (each rank preps ~1/N of the frame, not all of it).
+  if (f.pb1 > 0 && (B.ypos + S <= f.pb0 - 8 || B.ypos >= f.pb1 + 8)) return;
   int bw = B.bwidth >> 2, bh = B.bheight >> 2;
   int pb = mode == M_INTER ? B.pb_part : 0;
   int tb = B.tb_split > 0;
@@ -57,6 +62,24 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   if (lane == 0 && mode != M_INTRA && (s0 < 0 || (bi && s1 < 0))) atomicOr(&f.ctl[2], 1u);
   const unsigned resbits = mode == M_SKIP ? 0u : ((unsigned)(B.coeff_mask & 7) << 18);
   const bool quarters = mode == M_INTER || mode == M_BIPRED;  // four size/2 quarters with mv_arr[i], :381-392
+  // Per-cell MC words are read only by k_recon's per-cell path.  With a slow
+  // list that path runs only for the listed (multi-key) halves, masking every
+  // other half's cells, so the words are written only for CUs that can lie in
+  // one: inter CUs under 64x64 (they make their half multi-key), 64x64 INTER /
+  // BIPRED CUs with differing quarters, and -- when the frame lists any unit --
+  // intra CUs under 64x64 (inactive words for a multi-key half's intra cells).
+  // A planned 64x64 CU's or an intra SB's words are never read: 4K P frames
+  // wrote 8 B per 4x4 cell (33 MB per 8-frame launch) for nothing.  Without a
+  // list every unit that is not planned on both halves takes the per-cell path,
+  // so every CU writes them.
+  bool need_mc = !f.slow;
+  if (!need_mc) {
+    if (S < 64) need_mc = mode != M_INTRA || f.nslow > 0;
+    else if (quarters)
+      need_mc = B.mv0[0] != B.mv0[2] || B.mv0[1] != B.mv0[3] || B.mv0[4] != B.mv0[6] || B.mv0[5] != B.mv0[7] ||
+                (mode == M_BIPRED && (B.mv1[0] != B.mv1[2] || B.mv1[1] != B.mv1[3] || B.mv1[4] != B.mv1[6] ||
+                                      B.mv1[5] != B.mv1[7]));
+  }
   int div = S >> 3;
   int y4 = B.ypos >> 2, x4 = B.xpos >> 2;
   for (int c = lane; c < bw * bh; c += 64) {
@@ -66,6 +89,7 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
     int big = (abs(a0) >= 4) | (abs(a1) >= 4) | (abs(a2) >= 4) | (abs(a3) >= 4);
     int idx = (y4 + m) * cstride + x4 + n;
     f.cellinfo[idx] = base | (uint16_t)(big << 6);
+    if (!need_mc) continue;
     // MC word (the SKIP rectangle is already clipped to the frame: bwidth / bheight)
     const int qq = quarters ? q : 0;
     int m0x = B.mv0[2 * qq], m0y = B.mv0[2 * qq + 1], m1x = B.mv1[2 * qq], m1y = B.mv1[2 * qq + 1];

@@ -232,6 +232,10 @@ class GpuDecoder:
     def set_band_local(self, on: bool):
         L.check(self.lib.thor_dec_set_band_local(self.h, 1 if on else 0), "thor_dec_set_band_local")
 
+    def set_band_pad(self, on: bool):
+        """thor_dec_set_band_pad: finish() pads only the band's rows (halo / boundary modes)."""
+        L.check(self.lib.thor_dec_set_band_pad(self.h, 1 if on else 0), "thor_dec_set_band_pad")
+
     def set_band_intra(self, on: bool):
         L.check(self.lib.thor_dec_set_band_intra(self.h, 1 if on else 0), "thor_dec_set_band_intra")
 

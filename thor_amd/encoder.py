@@ -118,6 +118,23 @@ class GpuEncoder:
         self.lib.thor_enc_frame_bytes(self.h, buf, n)
         return buf.raw
 
+    def record_sb_costs(self, on: bool = True):
+        """thor_enc_record_sb_costs: keep every superblock's top-level
+        process_block costs (delta-QP trials, then the final encode)."""
+        L.check(self.lib.thor_enc_record_sb_costs(self.h, 1 if on else 0), "thor_enc_record_sb_costs")
+
+    def sb_costs(self) -> np.ndarray:
+        """The last coded frame's per-SB costs: int32 (nsb, trials + 1), raster SB order."""
+        per = C.c_int(0)
+        n = self.lib.thor_enc_sb_costs(self.h, None, 0, C.byref(per))
+        if n < 0:
+            raise RuntimeError("thor_enc_sb_costs: %d" % n)
+        out = np.empty(n, np.int32)
+        got = self.lib.thor_enc_sb_costs(self.h, out.ctypes.data, n, C.byref(per))
+        if got != n:
+            raise RuntimeError("thor_enc_sb_costs: %d" % got)
+        return out.reshape(-1, per.value)
+
     def encode_all(self) -> bytes:
         return b"".join(self.encode_next() for _ in range(self.num_frames()))
 

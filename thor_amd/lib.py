@@ -63,12 +63,12 @@ class ThorParsedFrame(C.Structure):
 # Every symbol the public headers declare (checked by tests/test_capi.py).
 BATCHED_SYMBOLS = [
     "thor_dec_create", "thor_dec_destroy", "thor_dec_frame", "thor_dec_frames", "thor_dec_frame_begin",
-    "thor_dec_frame_end", "thor_dec_set_band", "thor_dec_set_band_local", "thor_dec_frame_finish", "thor_dec_set_band_intra", "thor_dec_frame_intra", "thor_dec_get_rows", "thor_dec_put_rows", "thor_dec_put_ref_rows", "thor_dec_pad_frame", "thor_build_intra_list", "thor_build_tu_list", "thor_build_clpf_list", "thor_build_slow_list", "thor_dec_set_stop_stage",
+    "thor_dec_frame_end", "thor_dec_set_band", "thor_dec_set_band_local", "thor_dec_frame_finish", "thor_dec_set_band_intra", "thor_dec_set_band_pad", "thor_dec_frame_intra", "thor_dec_get_rows", "thor_dec_put_rows", "thor_dec_put_ref_rows", "thor_dec_pad_frame", "thor_build_intra_list", "thor_build_tu_list", "thor_build_clpf_list", "thor_build_slow_list", "thor_dec_set_stop_stage",
     "thor_dec_read_frame", "thor_dec_write_frame", "thor_dec_set_timing", "thor_dec_stage_ms", "thor_dec_stage_marks", "thor_dec_sync", "thor_dec_stream", "thor_dec_set_stream",
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_set_cu_mask", "thor_enc_frames", "thor_enc_frames_begin", "thor_enc_frames_end", "thor_enc_frame", "thor_enc_frame_bytes",
-    "thor_enc_read_recon", "thor_enc_reset", "thor_enc_debug_stall",
+    "thor_enc_read_recon", "thor_enc_reset", "thor_enc_debug_stall", "thor_enc_record_sb_costs", "thor_enc_sb_costs",
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame", "thor_frame_image",
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
     "thor_dev_alloc", "thor_dev_free", "thor_h2d", "thor_d2h", "thor_device_count", "thor_version",
@@ -117,6 +117,8 @@ def load(path: str = LIB_PATH):
     L.thor_dec_set_band_local.restype = i
     L.thor_dec_set_band_intra.argtypes = [P, i]
     L.thor_dec_set_band_intra.restype = i
+    L.thor_dec_set_band_pad.argtypes = [P, i]
+    L.thor_dec_set_band_pad.restype = i
     L.thor_dec_frame_intra.argtypes = [P]
     L.thor_dec_frame_intra.restype = i
     L.thor_dec_frame_finish.argtypes = [P]
@@ -187,6 +189,10 @@ def load(path: str = LIB_PATH):
     L.thor_enc_frame_bytes.restype = C.c_longlong
     L.thor_enc_read_recon.argtypes = [P, P, P, P]
     L.thor_enc_read_recon.restype = i
+    L.thor_enc_record_sb_costs.argtypes = [P, i]
+    L.thor_enc_record_sb_costs.restype = i
+    L.thor_enc_sb_costs.argtypes = [P, P, C.c_size_t, C.POINTER(C.c_int)]
+    L.thor_enc_sb_costs.restype = C.c_longlong
     L.thor_parser_create.restype = P
     L.thor_parser_destroy.argtypes = [P]
     L.thor_parser_seq.argtypes = [P, C.POINTER(ThorSeq)]

@@ -159,6 +159,8 @@ class RowShard:
         self.band_local = band_local
         if band_local:
             dec.set_band_local(True)
+        if halo and hasattr(dec, "set_band_pad"):  # only the band's rows are final here: pad just those
+            dec.set_band_pad(True)
         if boundary:
             if any(self.owned(q)[1] - self.owned(q)[0] < 8 for q in range(self.world)):
                 raise ValueError("the boundary exchange needs every band at least 8 rows high")

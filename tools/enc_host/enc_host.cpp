@@ -5,7 +5,13 @@
 // be checked bit for bit against the reference encoder's .bit on a CPU-only
 // box.  Frame loop filters come from the CPU oracle (oracle/thor_oracle.c).
 //
-//   enc_host -if in.yuv -of out.bit [-rf rec.yuv] [-dump_sb_bits f] -width W -height H -n N [-qp ..] ...
+//   enc_host -if in.yuv -of out.bit [-rf rec.yuv] [-rdlog costs.bin] -width W -height H -n N [-qp ..] ...
+//
+// -rdlog: every superblock's top-level process_block costs (te_encode_sb's
+// cost record: delta-QP trials, then the final encode) as int32 records
+// (frame_num, 64, ypos, xpos, qp or -1 for the final encode, cost) -- the
+// layout of tests/golden/rd_costs.npz, whose reference records carry the
+// final encode's QP instead of -1.
 #define TE_HOST 1
 #include <stdio.h>
 #include <stdlib.h>
@@ -35,7 +41,7 @@ struct HostFrame {
 int main(int argc, char **argv) {
   thor_enc_params_t P;
   te_default_params(&P);
-  const char *in = nullptr, *out = nullptr, *recf = nullptr;
+  const char *in = nullptr, *out = nullptr, *recf = nullptr, *rdlog = nullptr;
   const char *trace_out = nullptr;
   (void)trace_out;
   int verbose = 0;
@@ -43,6 +49,7 @@ int main(int argc, char **argv) {
     if (!strcmp(argv[i], "-if")) in = argv[i + 1];
     else if (!strcmp(argv[i], "-of")) out = argv[i + 1];
     else if (!strcmp(argv[i], "-rf")) recf = argv[i + 1];
+    else if (!strcmp(argv[i], "-rdlog")) rdlog = argv[i + 1];
     else if (!strcmp(argv[i], "-v")) verbose = atoi(argv[i + 1]);
 #if defined(THOR_ENC_TRACE)
     else if (!strcmp(argv[i], "-trace_frame")) te_trace_frame = atoi(argv[i + 1]);
@@ -65,7 +72,10 @@ int main(int argc, char **argv) {
   }
 #endif
   FILE *fi = fopen(in, "rb"), *fo = fopen(out, "wb"), *fr = recf ? fopen(recf, "wb") : nullptr;
-  if (!fi || !fo) return 3;
+  FILE *frd = rdlog ? fopen(rdlog, "wb") : nullptr;
+  if (!fi || !fo || (rdlog && !frd)) return 3;
+  const int ntrial = P.max_delta_qp ? (2 * P.max_delta_qp) / (P.delta_qp_step > 0 ? P.delta_qp_step : 1) + 1 : 0;
+  std::vector<int32_t> costs(ntrial + 1);
   const size_t fsz = (size_t)W * H * 3 / 2;
   std::vector<uint8_t> orig(fsz);
   TeGop gop(P);
@@ -143,8 +153,13 @@ int main(int argc, char **argv) {
     te_frame_header(fb, pl);
     for (int k = 0; k < nsbv; k++)
       for (int l = 0; l < nsbh; l++) {
-        te_encode_sb(F, sb, k, l);
+        te_encode_sb(F, sb, k, l, frd ? costs.data() : nullptr);
         fb.append_words(sb.bits.w, sb.bits.pos);
+        for (int t = 0; frd && t <= ntrial; t++) {
+          const int32_t r[6] = {pl.frame_num, 64, 64 * k, 64 * l,
+                                t < ntrial ? pl.qp - P.max_delta_qp + t * P.delta_qp_step : -1, costs[t]};
+          fwrite(r, sizeof(r), 1, frd);
+        }
         if (verbose > 1) fprintf(stderr, "frame %d sb %d,%d bits %d\n", pl.frame_num, k, l, sb.bits.pos);
       }
     for (size_t i = 0; i < cells.size(); i++) {
@@ -207,6 +222,7 @@ int main(int argc, char **argv) {
   fclose(fi);
   fclose(fo);
   if (fr) fclose(fr);
+  if (frd) fclose(frd);
   free(SM);
   return 0;
 }
