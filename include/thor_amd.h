@@ -409,6 +409,37 @@ int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride);
  * enc/putbits.c:57-95; the first chunk carries the sequence header):
  * returns its size, copies min(size, cap) bytes to dst when non-NULL. */
 long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap);
+/* Sequence launch (enc_seq.hip): the next `nframes` frames (coding order) of
+ * each of n contexts in ONE persistent launch.  Frame f + 1 of a context starts
+ * as soon as its frame f is a finished reference (RD loop, loop filters, CLPF,
+ * padding), independently of the other contexts, and each frame's bits go to
+ * page-locked host memory as soon as they are packed.  in[i * nframes + f]:
+ * context i's f-th input frame (I420, luma stride = width): a device pointer
+ * (fetch = 0), or a host pointer to page-locked, device-accessible memory
+ * (fetch = 1: the launch copies it to dev[i * nframes + f], W*H*3/2 bytes of
+ * device memory, one frame ahead of the RD loop).  arena_bytes: host space for
+ * the coded frames (<= 0: W*H/32 bytes per frame + 16 KB).  Contexts with
+ * interpolated references or SB-cost recording are refused (THOR_ERR_ARG:
+ * thor_enc_frames codes them), and so is a second launch, or a batch, while
+ * one is in flight on the device.  Returns at once with the launch in flight.
+ * thor_enc_seq_ready: out[i * nframes + f] = chunk size of that frame if it is
+ * final, else -1 (non-blocking); returns how many are final.
+ * thor_enc_seq_chunk: the chunk (4-byte big-endian length + payload) of
+ * context i's f-th frame, min(size, cap) bytes copied; returns its size.
+ * thor_enc_seq_end: waits; on a device error every context returns to its
+ * state before the launch (THOR_ERR_HIP, THOR_ERR_NOMEM when a frame outgrew
+ * the output buffer or the arena); else each context's last frame is also its
+ * thor_enc_frame_bytes chunk.  stats (optional, 4 values): workers launched,
+ * workers retired early (after the I frames, to free CU slots), tasks run,
+ * arena words used. */
+/* input frame index (display order) of the frame `ahead` frames after the next
+ * one in coding order (ahead = 0: thor_enc_next_input); -1 past the end */
+int thor_enc_plan_input(const thor_enc_t *e, int ahead);
+int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t *const *in, uint8_t *const *dev,
+                       int fetch, long long arena_bytes);
+int thor_enc_seq_ready(thor_enc_t *e0, long long *out, int count);
+long long thor_enc_seq_chunk(thor_enc_t *e0, int i, int f, uint8_t *dst, size_t cap);
+int thor_enc_seq_end(thor_enc_t *e0, long long *stats);
 /* The last coded frame's reconstruction (deblocked, CLPF'd), host planes. */
 int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
 /* Per-superblock RD costs (parity instrumentation, tests/golden/rd_costs.npz):

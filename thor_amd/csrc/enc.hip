@@ -343,6 +343,9 @@ struct thor_enc {
   int opar;              // which of the two the next frame packs into
   int out_cap_words;
   int *out_bits;         // device
+  uint32_t *sb_words2;   // device: the SB buffers of odd frames of a sequence launch (enc_seq.hip), on first use
+  int *sb_nbits2;
+  int8_t *clpf_bits2;
   int32_t *sb_costs;     // device, thor_enc_record_sb_costs: per SB its top-level process_block costs
   int cost_stride;       // per SB: the delta-QP trials + the final encode
   // last coded frame
@@ -377,8 +380,8 @@ static int enc_alloc(thor_enc *e) {
   if (!dev_alloc(&e->es_thr, 2 * 52 * 4 * sizeof(int), "thor_enc_create: early-skip thresholds")) return g_create_err.code;
   if (!dev_alloc(&e->hdr_words, 64 * 4, "thor_enc_create: header words")) return g_create_err.code;
   e->out_cap_words = (int)(((size_t)W * H * 2) / 4 + 1024);  // 16 bits per pixel: far above any real frame
-  if (!dev_alloc(&e->out_words, (size_t)e->out_cap_words * 4 + 8, "thor_enc_create: output words")) return g_create_err.code;
-  if (!dev_alloc(&e->out_words2, (size_t)e->out_cap_words * 4 + 8, "thor_enc_create: output words (2)")) return g_create_err.code;
+  if (!dev_alloc(&e->out_words, (size_t)e->out_cap_words * 4 + 64, "thor_enc_create: output words")) return g_create_err.code;
+  if (!dev_alloc(&e->out_words2, (size_t)e->out_cap_words * 4 + 64, "thor_enc_create: output words (2)")) return g_create_err.code;
   if (!dev_alloc(&e->out_bits, sizeof(int), "thor_enc_create: output bit count")) return g_create_err.code;
   std::vector<int> es(2 * 52 * 4);
   te_es_thresholds(e->p.early_skip_thr, es.data());
@@ -503,6 +506,10 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n, size_t nsb_tota
 // so a call on another thread sees either the old or the new value, never a torn one
 static std::atomic<unsigned long long> g_spin_limit{30000000000ULL};  // s_memrealtime ticks (100 MHz): 5 minutes
 static std::atomic<int> g_stall_row{-1};
+// sequence launches (enc_seq.hip): one in flight on the device? / a context leaving one
+static bool ts_active(int device);
+static bool ts_member(const thor_enc *e);
+static void ts_forget(thor_enc *e);
 
 extern "C" {
 
@@ -552,8 +559,10 @@ void thor_enc_destroy(thor_enc_t *e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  ts_forget(e);  // a sequence launch in flight with this context: waited for, the context dropped from it
   void *bufs[] = {e->slots,   e->cells,     e->cellinfo, e->sb_words,  e->sb_nbits, e->deps,   e->clpf_bits,
-                  e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_words2, e->out_bits, e->sb_costs};
+                  e->clpf_flags, e->es_thr, e->hdr_words, e->out_words, e->out_words2, e->out_bits, e->sb_costs,
+                  e->sb_words2, e->sb_nbits2, e->clpf_bits2};
   {  // a batch still pending with this context (begun, never ended) is dropped; the
      // batch's other contexts return to their state before it (newest batch first,
      // so a context in two dropped batches ends at the older one's snapshot)
@@ -582,6 +591,12 @@ int thor_enc_num_frames(const thor_enc_t *e) { return e ? (int)e->gop->plans.siz
 int thor_enc_next_input(const thor_enc_t *e) {
   if (!e) return THOR_ERR_ARG;
   return e->pos < e->gop->plans.size() ? e->gop->plans[e->pos].input_index : -1;
+}
+// input frame index of the frame `ahead` frames after the next one in coding order; -1 past the end
+int thor_enc_plan_input(const thor_enc_t *e, int ahead) {
+  if (!e || ahead < 0) return THOR_ERR_ARG;
+  const size_t q = e->pos + (size_t)ahead;
+  return q < e->gop->plans.size() ? e->gop->plans[q].input_index : -1;
 }
 void *thor_enc_stream(thor_enc_t *e) { return e ? (void *)e->stream : nullptr; }
 // Re-create the context's stream restricted to a set of CUs
@@ -768,6 +783,7 @@ static int frames_begin_locked(EncPool &P, thor_enc_t *const *es, int n, const u
   const int nrows = lead->nsbv;
   const int nwork = n * nrows;
   if (P.pending.size() >= 2) return THOR_ERR_ARG;  // end the oldest batch first
+  if (ts_active(lead->device)) return THOR_ERR_ARG;  // a sequence launch holds the pool's workers
   for (const EncPool::Pending &q : P.pending)
     for (thor_enc *x : q.es)
       for (int i = 0; i < n; i++)
@@ -1004,7 +1020,7 @@ int thor_enc_frames(thor_enc_t *const *es, int n, const uint8_t *const *orig, co
 }
 
 int thor_enc_reset(thor_enc_t *e) {
-  if (!e) return THOR_ERR_ARG;
+  if (!e || ts_member(e)) return THOR_ERR_ARG;
   {  // not with a batch begun and not ended
     EncPool &P = pool_for(e->device);
     std::lock_guard<std::mutex> lk(P.mu);

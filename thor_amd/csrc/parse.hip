@@ -605,9 +605,10 @@ int thor_parse_frame(thor_parser_t *P, const uint8_t *payload, size_t nbytes, th
     P->seq.clpf = (int)b.get(1);
     P->use_block_contexts = (int)b.get(1);
     P->seq.bipred = (int)b.get(1);
-    // 16-bit sizes; this build also caps them at 16384 (a corrupt header must not size GBs of side info)
+    // 16-bit sizes; this build also caps the area at 16384^2 pixels (a corrupt header must not size
+    // GBs of side info) -- not each side: the encoder codes frames up to 65 535 px wide (te_check_params)
     if (P->seq.width <= 0 || P->seq.height <= 0 || (P->seq.width & 7) || (P->seq.height & 7) ||
-        P->seq.width > 16384 || P->seq.height > 16384)
+        (long long)P->seq.width * P->seq.height > 16384LL * 16384)
       return THOR_ERR_ARG;
     P->have_seq = 1;
     P->cells.assign((size_t)(P->seq.width / 4) * (P->seq.height / 4), TeCell());

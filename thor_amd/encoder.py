@@ -169,3 +169,68 @@ def encode_batch_end(encs):
     hs = (C.c_void_p * n)(*[e.h for e in encs])
     L.check(lib.thor_enc_frames_end(hs, n), "thor_enc_frames_end")
     return [e.chunk() for e in encs]
+
+
+class SeqLaunch:
+    """One sequence launch (thor_enc_seq_begin): the next `nframes` frames of
+    every encoder in `encs` in ONE persistent launch, frame f + 1 of a stream
+    starting as soon as its frame f is a finished reference.  Inputs: each
+    encoder's device sequence (upload_sequence / use_device_sequence), or, with
+    `host`, page-locked host frames host(i, input_index) -> address that the
+    launch itself copies into the device sequence (fetch mode)."""
+
+    def __init__(self, encs, nframes=None, host=None, arena_bytes=0):
+        self.encs = encs
+        self.lib = encs[0].lib
+        n = len(encs)
+        if nframes is None:  # every frame each encoder has left
+            nframes = min(self._left(e) for e in encs)
+        self.n, self.nf = n, nframes
+        ins, devs = [], []
+        for i, e in enumerate(encs):
+            for f in range(nframes):
+                k = self.lib.thor_enc_plan_input(e.h, f)
+                if k < 0 or k >= e.nin:
+                    raise IndexError("input frame %d not available" % k)
+                devs.append(e.seq_dev + k * e.fsize)
+                ins.append(host(i, k) if host else e.seq_dev + k * e.fsize)
+        hs = (C.c_void_p * n)(*[e.h for e in encs])
+        self._ins = (C.c_void_p * len(ins))(*ins)
+        self._devs = (C.c_void_p * len(devs))(*devs)
+        L.check(self.lib.thor_enc_seq_begin(hs, n, nframes, self._ins, self._devs if host else None, 1 if host else 0,
+                                            arena_bytes), "thor_enc_seq_begin")
+        self.sizes = np.full(n * nframes, -1, np.int64)
+        self.stats = None
+
+    def _left(self, e):
+        f = 0
+        while self.lib.thor_enc_plan_input(e.h, f) >= 0:
+            f += 1
+        return f
+
+    def ready(self) -> np.ndarray:
+        """Chunk size per (encoder, frame) that is final, -1 otherwise (non-blocking)."""
+        self.lib.thor_enc_seq_ready(self.encs[0].h, self.sizes.ctypes.data, self.sizes.size)
+        return self.sizes.reshape(self.n, self.nf)
+
+    def chunk(self, i: int, f: int) -> bytes:
+        n = self.lib.thor_enc_seq_chunk(self.encs[0].h, i, f, None, 0)
+        if n < 0:
+            raise RuntimeError("thor_enc_seq_chunk(%d, %d): %d" % (i, f, n))
+        buf = C.create_string_buffer(n)
+        self.lib.thor_enc_seq_chunk(self.encs[0].h, i, f, buf, n)
+        return buf.raw
+
+    def end(self):
+        st = (C.c_longlong * 4)()
+        L.check(self.lib.thor_enc_seq_end(self.encs[0].h, st), "thor_enc_seq_end")
+        self.stats = {"workers": st[0], "retired": st[1], "tasks": st[2], "arena_words": st[3]}
+        return self.stats
+
+
+def encode_sequences(encs, nframes=None, host=None):
+    """Every remaining frame (or `nframes`) of every encoder in one sequence
+    launch; returns each encoder's .bit bytes for those frames."""
+    s = SeqLaunch(encs, nframes, host)
+    s.end()
+    return [b"".join(s.chunk(i, f) for f in range(s.nf)) for i in range(s.n)]
