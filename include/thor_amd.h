@@ -440,6 +440,11 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
 int thor_enc_seq_ready(thor_enc_t *e0, long long *out, int count);
 long long thor_enc_seq_chunk(thor_enc_t *e0, int i, int f, uint8_t *dst, size_t cap);
 int thor_enc_seq_end(thor_enc_t *e0, long long *stats);
+/* The last ended sequence launch's profile, summed over its workers (100 MHz
+ * ticks): per task type (RD, FETCH, DBV, DBH, FIN, PACK) the time in tasks,
+ * then the task counts, then idle time, time waiting for a claimed queue slot
+ * and failed claims.  Returns 15; copies min(15, n) values. */
+int thor_enc_seq_profile(thor_enc_t *e0, long long *out, int n);
 /* The last coded frame's reconstruction (deblocked, CLPF'd), host planes. */
 int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
 /* Per-superblock RD costs (parity instrumentation, tests/golden/rd_costs.npz):

@@ -85,8 +85,9 @@ def test_sequence_launch_matches_reference(streams, names, nframes):
 def test_sequence_launch_fetches_host_frames(streams):
     """Fetch mode: the launch copies each frame from page-locked host memory
     into HBM itself (FETCH tasks, one frame ahead of the RD loop); frames become
-    final (thor_enc_seq_ready) while it runs, and the .bit is the reference's."""
-    import torch
+    final (thor_enc_seq_ready) while it runs, and the .bit is the reference's.
+    (Page-locked memory from the HIP runtime the library uses, not torch's.)"""
+    import time
 
     from thor_amd.encoder import GpuEncoder, SeqLaunch, params_for
 
@@ -94,19 +95,23 @@ def test_sequence_launch_fetches_host_frames(streams):
     meta = streams[name]
     W, H = meta["width"], meta["height"]
     fsize = W * H * 3 // 2
-    host = torch.from_numpy(np.ascontiguousarray(synth.synth_frames(W, H, nframes, meta["seed"], workers=1))
-                            .reshape(nframes, fsize)).pin_memory()
-    dev = [torch.zeros((nframes, fsize), dtype=torch.uint8, device="cuda") for _ in range(n)]
-    torch.cuda.synchronize()
-    encs = []
+    frames = np.ascontiguousarray(synth.synth_frames(W, H, nframes, meta["seed"], workers=1)).reshape(nframes, fsize)
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+    hip.hipHostFree.argtypes = [C.c_void_p]
+    pinned = C.c_void_p()
+    assert hip.hipHostMalloc(C.byref(pinned), frames.nbytes, 0) == 0
+    encs, devs = [], []
     try:
+        C.memmove(pinned.value, frames.ctypes.data, frames.nbytes)
         for i in range(n):
             e = GpuEncoder(params_for(meta["config"], W, H, nframes, meta["extra"]))
-            e.use_device_sequence(dev[i].data_ptr(), nframes)
+            d = e.lib.thor_dev_alloc(frames.nbytes)
+            assert d
+            devs.append(d)
+            e.use_device_sequence(d, nframes)
             encs.append(e)
-        s = SeqLaunch(encs, host=lambda i, k: host[k].data_ptr())
-        import time
-
+        s = SeqLaunch(encs, host=lambda i, k: pinned.value + k * fsize)
         seen, t0 = 0, time.time()
         while seen < n * nframes and time.time() - t0 < 60:  # (a failed launch gives up after 20 s)
             seen = max(seen, int((s.ready() >= 0).sum()))
@@ -114,13 +119,18 @@ def test_sequence_launch_fetches_host_frames(streams):
         s.end()
         assert seen == n * nframes
         want = _golden(name)
+        back = np.empty_like(frames)
         for i in range(n):
             for f in range(nframes):
                 assert s.chunk(i, f) == want[f], (i, f)
-            assert torch.equal(dev[i].cpu(), host), i  # the fetched inputs are the host frames
+            assert encs[i].lib.thor_d2h(back.ctypes.data, devs[i], back.nbytes) == 0
+            assert np.array_equal(back, frames), i  # the fetched inputs are the host frames
     finally:
         for e in encs:
             e.close()
+        for d in devs:
+            encs[0].lib.thor_dev_free(d)
+        hip.hipHostFree(pinned)
 
 
 def test_sequence_launch_then_frame_batches(streams):

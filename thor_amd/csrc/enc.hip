@@ -218,13 +218,146 @@ __global__ __launch_bounds__(256) void k_enc_cellinfo(const TeJob *__restrict__ 
                              (big << 6) | (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
 }
 
+// CLPF of a full SB with one 8x8 block per lane (block b = lane: row b >> 3,
+// column b & 7), the side info from the 16-bit cell words -- te_clpf_decide's
+// and clpf_block's arithmetic (enc/encode_frame.c:50-63, common/common_block.c:
+// 180-197: the 4-neighbour majority vote, neighbours clamped at the SB border),
+// each lane holding its block and a one-pixel ring in registers.
+struct TeClpfBlk {
+  uint32_t cy[10][3];  // luma rows y0-1 .. y0+8: bytes x0-1 (word 0 byte 3), x0 .. x0+7 (words 1, 2), x0+8 (word 0 byte 0)
+};
+// luma pixel (r, c) of the block's ring, r, c in -1 .. 8, clamped to the SB (at the SB's edge the
+// neighbour is the pixel itself)
+__device__ __forceinline__ int te_clpf_ring(const uint32_t (&v)[10][3], int r, int c) {
+  const uint32_t *w = v[r + 1];
+  if (c < 0) return (int)(w[0] >> 24);
+  if (c > 7) return (int)(w[0] & 255);
+  return (int)((w[1 + (c >> 2)] >> (8 * (c & 3))) & 255);
+}
+// loads the ring of the lane's luma block (rows / columns outside the SB: clamped)
+__device__ __forceinline__ void te_clpf_load(uint32_t (&v)[10][3], const uint8_t *ry, int rsy, int k, int l) {
+  const int lane = threadIdx.x, br = lane >> 3, bc = lane & 7;
+  const int y0 = k * 64 + br * 8, x0 = l * 64 + bc * 8;
+#pragma unroll
+  for (int r = -1; r <= 8; r++) {
+    int y = y0 + r;
+    if (br == 0 && r < 0) y = y0;  // SB top: the row itself
+    if (br == 7 && r > 7) y = y0 + 7;
+    const uint8_t *row = ry + (long long)y * rsy + x0;
+    const uint2 m = *(const uint2 *)row;
+    const uint32_t lft = bc == 0 ? (m.x & 255) : row[-1], rgt = bc == 7 ? (m.y >> 24) : row[8];
+    v[r + 1][0] = (lft << 24) | rgt;
+    v[r + 1][1] = m.x;
+    v[r + 1][2] = m.y;
+  }
+}
+__device__ __forceinline__ int te_clpf_delta(const uint32_t (&v)[10][3], int r, int c, int X) {
+  const int A = te_clpf_ring(v, r - 1, c), B = te_clpf_ring(v, r, c - 1), C = te_clpf_ring(v, r, c + 1),
+            D = te_clpf_ring(v, r + 1, c);
+  return ((A > X) + (B > X) + (C > X) + (D > X) > 2) - ((A < X) + (B < X) + (C < X) + (D < X) > 2);
+}
+// te_clpf_decide from the cell words: -1 no candidate block, else the flag
+__device__ int te_clpf_decide_blk(const uint16_t *cellinfo, int W, const uint8_t *ry, int rsy, const uint8_t *oy,
+                                  int osy, int k, int l) {
+  const int lane = threadIdx.x, br = lane >> 3, bc = lane & 7;
+  const int y0 = k * 64 + br * 8, x0 = l * 64 + bc * 8;
+  const uint16_t ci = cellinfo[(y0 >> 2) * (W >> 2) + (x0 >> 2)];
+  const int cand = CI_MODE(ci) != 3 && (CI_CBPY(ci) | CI_CBPU(ci) | CI_CBPV(ci));
+  uint32_t s0 = 0, s1 = 0;
+  if (CI_MODE(ci) != 3 && CI_CBPY(ci)) {
+    uint32_t v[10][3];
+    te_clpf_load(v, ry, rsy, k, l);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const uint2 o = *(const uint2 *)(oy + (long long)(y0 + r) * osy + x0);
+#pragma unroll
+      for (int c = 0; c < 8; c++) {
+        const int X = te_clpf_ring(v, r, c), O = (int)(((c < 4 ? o.x : o.y) >> (8 * (c & 3))) & 255);
+        const int delta = te_clpf_delta(v, r, c, X);
+        s0 += (uint32_t)((O - X) * (O - X));
+        s1 += (uint32_t)((O - X - delta) * (O - X - delta));
+      }
+    }
+  }
+  const int any = te_any(cand);
+  s0 = te_sum(s0);
+  s1 = te_sum(s1);
+  if (!any) return -1;
+  return (int)s1 < (int)s0;
+}
+// CLPF of a flagged SB in place: every lane loads its ring (all loads before any store), then
+// writes its filtered luma block and its 4x4 chroma blocks where the plane has coded residual
+__device__ void te_clpf_apply_blk(const uint16_t *cellinfo, int W, uint8_t *ry, int rsy, uint8_t *ru, uint8_t *rv,
+                                  int rsc, int k, int l) {
+  const int lane = threadIdx.x, br = lane >> 3, bc = lane & 7;
+  const int y0 = k * 64 + br * 8, x0 = l * 64 + bc * 8;
+  const uint16_t ci = cellinfo[(y0 >> 2) * (W >> 2) + (x0 >> 2)];
+  const bool ny = CI_MODE(ci) != 3 && CI_CBPY(ci), nu = CI_MODE(ci) != 3 && CI_CBPU(ci),
+             nv = CI_MODE(ci) != 3 && CI_CBPV(ci);
+  uint32_t v[10][3];
+  te_clpf_load(v, ry, rsy, k, l);
+  // chroma 4x4 blocks with their rings (6 x 6), clamped to the SB's 32 x 32
+  uint32_t cu[6][2], cv[6][2];  // word 0: bytes c = -1 .. 2, word 1: c = 3, 4 (bytes 0, 1)
+  const int cy0 = k * 32 + br * 4, cx0 = l * 32 + bc * 4;
+#pragma unroll
+  for (int pl = 0; pl < 2; pl++) {
+    const uint8_t *P = pl ? rv : ru;
+    uint32_t (&w)[6][2] = pl ? cv : cu;
+#pragma unroll
+    for (int r = -1; r <= 4; r++) {
+      int y = cy0 + r;
+      if (br == 0 && r < 0) y = cy0;
+      if (br == 7 && r > 3) y = cy0 + 3;
+      const uint8_t *row = P + (long long)y * rsc + cx0;
+      const uint32_t m = *(const uint32_t *)row;
+      const uint32_t lft = bc == 0 ? (m & 255) : row[-1], rgt = bc == 7 ? (m >> 24) : row[4];
+      w[r + 1][0] = lft | (m << 8);
+      w[r + 1][1] = (m >> 24) | (rgt << 8);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // (every lane's loads are in registers before the first store)
+  if (ny) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      uint32_t o[2] = {0u, 0u};
+#pragma unroll
+      for (int c = 0; c < 8; c++) {
+        const int X = te_clpf_ring(v, r, c);
+        o[c >> 2] |= (uint32_t)((X + te_clpf_delta(v, r, c, X)) & 255) << (8 * (c & 3));
+      }
+      *(uint2 *)(ry + (long long)(y0 + r) * rsy + x0) = make_uint2(o[0], o[1]);
+    }
+  }
+#pragma unroll
+  for (int pl = 0; pl < 2; pl++) {
+    if (!(pl ? nv : nu)) continue;
+    const uint32_t (&w)[6][2] = pl ? cv : cu;
+    auto px = [&](int r, int c) -> int {  // r, c in -1 .. 4
+      const int b = c + 1;
+      return (int)((b < 4 ? w[r + 1][0] >> (8 * b) : w[r + 1][1] >> (8 * (b - 4))) & 255);
+    };
+    uint8_t *P = pl ? rv : ru;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int X = px(r, c), A = px(r - 1, c), B = px(r, c - 1), C = px(r, c + 1), D = px(r + 1, c);
+        const int delta = ((A > X) + (B > X) + (C > X) + (D > X) > 2) - ((A < X) + (B < X) + (C < X) + (D < X) > 2);
+        o |= (uint32_t)((X + delta) & 255) << (8 * c);
+      }
+      *(uint32_t *)(P + (long long)(cy0 + r) * rsc + cx0) = o;
+    }
+  }
+}
+
 // CLPF decision of every full SB (after deblocking), one wave per SB.
 __global__ __launch_bounds__(64) void k_enc_clpf(const TeJob *__restrict__ jobs) {
   const TeJob &J = jobs[blockIdx.y];
   const int nh = J.F.W >> 6, nv = J.F.H >> 6;
   const int sb = blockIdx.x;
   if (sb >= nh * nv || !J.clpf) return;
-  const int d = te_clpf_decide(J.F, sb / nh, sb % nh);
+  const int d = te_clpf_decide_blk(J.cellinfo, J.F.W, J.F.ry, J.F.rsy, J.F.oy, J.F.osy, sb / nh, sb % nh);
   if (threadIdx.x == 0) {
     J.clpf_bits[sb] = (int8_t)d;
     J.clpf_flags[sb] = (uint8_t)(d == 1);

@@ -41,7 +41,7 @@
 #define TS_NCLS 16
 #define TS_MAX_JOBS 4096          // 12 bits of a queue item
 #define TS_MAX_SB (1 << 17)       // 17 bits: SB index within a frame
-#define TS_CTL_WORDS (TS_NCLS * 64 + 256)
+#define TS_CTL_WORDS (TS_NCLS * 64 + 512)
 enum { TS_RD = 0, TS_FETCH = 1, TS_DBV = 2, TS_DBH = 3, TS_FIN = 4, TS_PACK = 5 };
 // control words (device): class c's head at [c * 64], tail at [c * 64 + 32]
 // (separate 128-byte lines), then the launch's counters
@@ -52,6 +52,10 @@ enum { TS_RD = 0, TS_FETCH = 1, TS_DBV = 2, TS_DBH = 3, TS_FIN = 4, TS_PACK = 5 
 #define TS_ARENA (TS_NCLS * 64 + 64)
 #define TS_IDONE (TS_NCLS * 64 + 96)
 #define TS_RETIRED (TS_NCLS * 64 + 128)
+// per-launch profile (64-bit sums over the workers, added once per worker at its exit):
+// [t] ticks and [t + 6] count per task type, then idle ticks, claim waits, failed claims
+#define TS_PROF (TS_NCLS * 64 + 192)
+#define TS_NPROF 15
 
 struct TsJob {
   TeJob J;                   // J.deps: the frame's SB counters; J.sb_words / sb_nbits / clpf_bits: the frame parity's
@@ -59,7 +63,7 @@ struct TsJob {
   const uint8_t *src;        // FETCH source (host), nullptr: the input is resident at dst
   uint8_t *dst;              // the input frame in HBM (I420, stride W)
   int next, next2;           // this stream's jobs for frames f + 1, f + 2 (-1: none)
-  int cls, need0, is_i;
+  int cls, aux, need0, is_i;  // queue class of the job's RD tasks / of its other tasks
   uint8_t *cy, *cu, *cv;     // the reconstruction (loop filters, padding)
   int sy, sc, qp, qpc, deblock;
 };
@@ -68,6 +72,9 @@ struct TsArgs {
   TeScratchMem *scratch;
   unsigned *ctl, *items, *err;
   unsigned qoff[TS_NCLS];
+  unsigned qtot[TS_NCLS];    // tasks of each class (ticket claims past it find nothing)
+  int ncls;                  // classes in use (stream i -> class i * ncls / n)
+  int claim;                 // 0: compare-and-swap claims (never block), 1: tickets (a claim may wait for its slot)
   unsigned total;            // tasks of the launch
   unsigned n_ijobs;          // I-frame jobs (idle workers may retire once they are all done)
   int min_alive;
@@ -91,22 +98,39 @@ __device__ __forceinline__ void ts_dep(const TsArgs &A, unsigned *cnt, unsigned 
   const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old + 1 == need) ts_push(A, cls, item);
 }
-// (lane 0) the oldest ready task of the highest class with one, TE_Q_EMPTY if none
-__device__ __forceinline__ unsigned ts_pop(const TsArgs &A) {
-  for (int c = 0; c < TS_NCLS; c++) {
+// (lane 0) the oldest ready task of the highest class with one, TE_Q_EMPTY if none.
+// claim 0: a slot below the tail is taken by compare-and-swap on the head
+// (never waits; contended when many idle workers race for one item);
+// claim 1: a ticket (one fetch-and-add) as soon as the class looks non-empty --
+// a ticket past the items pushed so far waits for its slot (every slot below
+// the class's task count fills: its tasks depend only on its own), one past
+// the class's task count is dropped.
+__device__ __forceinline__ unsigned ts_pop(const TsArgs &A, unsigned long long &fails, unsigned long long &waits) {
+  for (int c = 0; c < A.ncls; c++) {
     unsigned h = te_ld_relaxed(&A.ctl[TS_HEAD(c)]);
-    for (;;) {
-      const unsigned t = te_ld_relaxed(&A.ctl[TS_TAIL(c)]);
-      if (h >= t) break;
-      const unsigned seen = __hip_atomic_compare_exchange_strong(&A.ctl[TS_HEAD(c)], &h, h + 1, __ATOMIC_RELAXED,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (seen) {  // slot h is ours; its producer bumped the tail before storing the item
-        unsigned item;
-        while ((item = te_ld_relaxed(&A.items[A.qoff[c] + h])) == TE_Q_EMPTY) __builtin_amdgcn_s_sleep(1);
-        return item;
+    if (A.claim) {
+      if (h >= A.qtot[c] || h >= te_ld_relaxed(&A.ctl[TS_TAIL(c)])) continue;
+      h = __hip_atomic_fetch_add(&A.ctl[TS_HEAD(c)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (h >= A.qtot[c]) continue;
+    } else {
+      bool got = false;
+      for (;;) {
+        const unsigned t = te_ld_relaxed(&A.ctl[TS_TAIL(c)]);
+        if (h >= t) break;
+        if (__hip_atomic_compare_exchange_strong(&A.ctl[TS_HEAD(c)], &h, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          got = true;
+          break;
+        }
+        fails++;  // h now holds the head another worker moved it to
       }
-      // h now holds the head another worker moved it to
+      if (!got) continue;
     }
+    unsigned item;
+    const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+    while ((item = te_ld_relaxed(&A.items[A.qoff[c] + h])) == TE_Q_EMPTY) __builtin_amdgcn_s_sleep(1);
+    waits += __builtin_amdgcn_s_memrealtime() - w0;
+    return item;
   }
   return TE_Q_EMPTY;
 }
@@ -121,51 +145,6 @@ __device__ __forceinline__ uint16_t ts_cellinfo(const TeCell &c) {
   const int big = (abs(c.ip.mv0.x) >= 4) | (abs(c.ip.mv0.y) >= 4) | (abs(c.ip.mv1.x) >= 4) | (abs(c.ip.mv1.y) >= 4);
   return (uint16_t)((c.mode & 7) | ((c.cbp_y != 0) << 3) | ((c.cbp_u != 0) << 4) | ((c.cbp_v != 0) << 5) | (big << 6) |
                     (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
-}
-
-// CLPF of one flagged full SB by one wave (k_clpf_body's filter): the SB's
-// unfiltered Y | U | V staged in the worker's prediction buffer (LDS, free
-// between tasks), four pixels per lane step, each 8x8 block (4x4 chroma)
-// filtered where it is not BIPRED and has coded residual in the plane.
-__device__ void ts_clpf_sb(const TsJob &T, int k, int l) {
-  const int lane = threadIdx.x;
-  uint8_t *pb = g_te_pb;
-  TE_NB_FORGET();
-  const int W = T.J.F.W, cs = W >> 2;
-  uint8_t *y0 = T.cy + (long long)(k * 64) * T.sy + l * 64;
-  uint8_t *u0 = T.cu + (long long)(k * 32) * T.sc + l * 32;
-  uint8_t *v0 = T.cv + (long long)(k * 32) * T.sc + l * 32;
-  for (int e = lane; e < 256; e += 64) {
-    const int r = e >> 2, c = (e & 3) * 16;
-    *(uint4 *)&pb[r * 64 + c] = *(const uint4 *)(y0 + (long long)r * T.sy + c);
-  }
-  {
-    const int r = lane >> 1, c = (lane & 1) * 16;
-    *(uint4 *)&pb[4096 + r * 32 + c] = *(const uint4 *)(u0 + (long long)r * T.sc + c);
-    *(uint4 *)&pb[5120 + r * 32 + c] = *(const uint4 *)(v0 + (long long)r * T.sc + c);
-  }
-  te_sync();
-  const uint16_t *ci0 = T.J.cellinfo + (long long)(k * 16) * cs + l * 16;  // the SB's first 4x4 cell
-  for (int d = lane; d < 1024; d += 64) {  // luma dwords: row d >> 4, columns (d & 15) * 4 ..
-    const int r = d >> 4, c = (d & 15) * 4;
-    const uint16_t ci = ci0[(r >> 3) * 2 * cs + (c >> 3) * 2];
-    if (!(CI_MODE(ci) != 3 && CI_CBPY(ci))) continue;
-    uint32_t w = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) w |= (uint32_t)clpf_px(pb, 64, 64, r, c + j) << (8 * j);
-    *(uint32_t *)(y0 + (long long)r * T.sy + c) = w;
-  }
-  for (int d = lane; d < 512; d += 64) {  // chroma dwords: plane d >> 8, row (d & 255) >> 3, columns (d & 7) * 4 ..
-    const int pl = d >> 8, r = (d & 255) >> 3, c = (d & 7) * 4;
-    const uint16_t ci = ci0[(r >> 2) * 2 * cs + (c >> 2) * 2];
-    if (!(CI_MODE(ci) != 3 && (pl ? CI_CBPV(ci) : CI_CBPU(ci)))) continue;
-    const uint8_t *s = pb + 4096 + pl * 1024;
-    uint32_t w = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) w |= (uint32_t)clpf_px(s, 32, 32, r, c + j) << (8 * j);
-    *(uint32_t *)((pl ? v0 : u0) + (long long)r * T.sc + c) = w;
-  }
-  te_sync();
 }
 
 // FETCH: bytes [a, b) of the I420 frame, host -> HBM, 16 bytes per lane access,
@@ -193,26 +172,38 @@ __device__ void ts_copy_range(uint8_t *dst, const uint8_t *src, long long a, lon
 __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
   __shared__ TeFrame s_F;
   __shared__ TeSB s_sb;
+  __shared__ unsigned long long s_prof[TS_NPROF];  // (lane 0) this worker's profile, added to the launch's at exit
+  if (threadIdx.x < TS_NPROF) s_prof[threadIdx.x] = 0;
   g_te_mem = &A.scratch[blockIdx.x];
   te_load_basis(g_te_tx);
   te_load_zig();
   TeSB &sb = s_sb;
   const int lane = threadIdx.x;
   int cur = -1;  // the job whose frame parameters s_F holds
-  unsigned long long idle0 = 0;
+  unsigned long long idle0 = 0, prog0 = __builtin_amdgcn_s_memrealtime();
+  unsigned nd = 0, nd_seen = 0;
   bool idle = false;
+  unsigned long long t_prev = __builtin_amdgcn_s_memrealtime(), t_task = 0;
   for (;;) {
     unsigned item = TE_Q_EMPTY, state = 0;  // 0: nothing ready, 1: a task, 2: leave
     if (lane == 0) {
-      item = ts_pop(A);
+      const unsigned long long t_now = __builtin_amdgcn_s_memrealtime();
+      if (idle) s_prof[12] += t_now - t_prev;
+      t_prev = t_now;
+      unsigned long long fails = 0, waits = 0;
+      item = ts_pop(A, fails, waits);
+      s_prof[13] += waits;
+      s_prof[14] += fails;
+      t_task = __builtin_amdgcn_s_memrealtime();
       if (item != TE_Q_EMPTY) {
         state = 1;
-      } else if (te_ld_relaxed(&A.ctl[TS_NDONE]) >= A.total || te_ld_relaxed(A.err)) {
+      } else if ((nd = te_ld_relaxed(&A.ctl[TS_NDONE])) >= A.total || te_ld_relaxed(A.err)) {
         state = 2;  // every task done (or the launch failed): the grid drains
       } else {
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();  // 100 MHz
         if (!idle) idle = true, idle0 = now;
-        if (now - idle0 > A.spin_limit) {  // a wedged dependency: give up, reported; never hang the GPU
+        if (nd != nd_seen) nd_seen = nd, prog0 = now;  // the launch is moving (a long SB elsewhere is not a wedge)
+        if (now - prog0 > A.spin_limit) {  // no task finished anywhere for that long: give up, reported; never hang the GPU
           atomicOr(A.err, 1u);
           state = 2;
         } else if (now - idle0 > A.retire_ticks && te_ld_relaxed(&A.ctl[TS_IDONE]) >= A.n_ijobs) {
@@ -256,7 +247,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
       const int k = idx / nsbh, l = idx - k * nsbh;
       if (idx == 0 && T.next >= 0 && A.jobs[T.next].src && lane == 0) {  // the next frame's input starts moving
         const TsJob &N = A.jobs[T.next];
-        for (int r = 0; r < nsbv; r++) ts_push(A, N.cls, ts_item(T.next, TS_FETCH, r));
+        for (int r = 0; r < nsbv; r++) ts_push(A, N.aux, ts_item(T.next, TS_FETCH, r));
       }
       sb.bits.w = J.sb_words + (size_t)idx * THOR_ENC_SB_WORDS;
       sb.bits.cap = THOR_ENC_SB_WORDS * 32;
@@ -281,8 +272,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
           if (l == nsbh - 1) ts_dep(A, &J.deps[idx + nsbh], 1u + (l > 0), T.cls, ts_item(j, TS_RD, idx + nsbh));
         }
         if (l == nsbh - 1) {  // row k complete (and with it every row above)
-          if (k >= 1) ts_push(A, T.cls, ts_item(j, TS_DBV, k - 1));
-          if (k == nsbv - 1) ts_push(A, T.cls, ts_item(j, TS_DBV, k));
+          if (k >= 1) ts_push(A, T.aux, ts_item(j, TS_DBV, k - 1));
+          if (k == nsbv - 1) ts_push(A, T.aux, ts_item(j, TS_DBV, k));
         }
       }
     } else if (type == TS_FETCH) {
@@ -309,8 +300,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) {
-        ts_dep(A, &T.dbh[k], 1u + (k > 0), T.cls, ts_item(j, TS_DBH, k));
-        if (k + 1 < nsbv) ts_dep(A, &T.dbh[k + 1], 2u, T.cls, ts_item(j, TS_DBH, k + 1));
+        ts_dep(A, &T.dbh[k], 1u + (k > 0), T.aux, ts_item(j, TS_DBH, k));
+        if (k + 1 < nsbv) ts_dep(A, &T.dbh[k + 1], 2u, T.aux, ts_item(j, TS_DBH, k + 1));
       }
     } else if (type == TS_DBH) {
       const int k = idx;
@@ -327,16 +318,16 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) {
-        if (k > 0) ts_dep(A, &T.fin[k - 1], 2u, T.cls, ts_item(j, TS_FIN, k - 1));
-        ts_dep(A, &T.fin[k], 1u + (k + 1 < nsbv), T.cls, ts_item(j, TS_FIN, k));
+        if (k > 0) ts_dep(A, &T.fin[k - 1], 2u, T.aux, ts_item(j, TS_FIN, k - 1));
+        ts_dep(A, &T.fin[k], 1u + (k + 1 < nsbv), T.aux, ts_item(j, TS_FIN, k));
       }
     } else if (type == TS_FIN) {
       const int k = idx;
       if (J.clpf && k < (H >> 6)) {
         for (int l = 0; l < (W >> 6); l++) {
-          const int d = te_clpf_decide(s_F, k, l);
+          const int d = te_clpf_decide_blk(J.cellinfo, W, J.F.ry, J.F.rsy, J.F.oy, J.F.osy, k, l);
           if (lane == 0) J.clpf_bits[k * (W >> 6) + l] = (int8_t)d;
-          if (d == 1) ts_clpf_sb(T, k, l);
+          if (d == 1) te_clpf_apply_blk(J.cellinfo, W, T.cy, T.sy, T.cu, T.cv, T.sc, k, l);
         }
       }
       te_sync();
@@ -360,7 +351,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
       if (lane == 0) {
         const unsigned old = __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1 == (unsigned)nsbv) {  // the frame is a finished reference
-          ts_push(A, T.cls, ts_item(j, TS_PACK, 0));
+          ts_push(A, T.aux, ts_item(j, TS_PACK, 0));
           if (T.next >= 0) {
             const TsJob &N = A.jobs[T.next];
             ts_dep(A, &N.J.deps[0], (unsigned)N.need0, N.cls, ts_item(T.next, TS_RD, 0));
@@ -440,8 +431,17 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
         ts_dep(A, &N.J.deps[0], (unsigned)N.need0, N.cls, ts_item(T.next2, TS_RD, 0));
       }
     }
-    if (lane == 0) __hip_atomic_fetch_add(&A.ctl[TS_NDONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+      __hip_atomic_fetch_add(&A.ctl[TS_NDONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+      s_prof[type] += t1 - t_task;
+      s_prof[6 + type] += 1;
+      t_prev = t1;
+    }
   }
+  if (lane == 0)
+    for (int i = 0; i < TS_NPROF; i++)
+      if (s_prof[i]) atomicAdd((unsigned long long *)&A.ctl[TS_PROF + 2 * i], s_prof[i]);
 }
 
 // ============================================================================
@@ -471,6 +471,7 @@ struct TsPool {  // per device: the sequence launch's buffers (grown, never shru
   int *meta = nullptr;        // host, page-locked
   size_t nmeta = 0;
   int max_workers = 0;
+  long long prof[TS_NPROF] = {};
   TsRun run;
 };
 static std::map<int, TsPool *> g_ts_pools;
@@ -589,6 +590,15 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
     EHIP(hipHostMalloc((void **)&S.arena, aw * 4 + 64, hipHostMallocCoherent | hipHostMallocMapped));
     S.arena_words = aw;
   }
+  // scheduling knobs (experiments): THOR_SEQ_CLASSES (1..16, default 16), THOR_SEQ_CLAIM
+  // (0 compare-and-swap, 1 tickets), THOR_SEQ_RETIRE (0: workers never leave early)
+  auto knob = [](const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+  };
+  int ncls = knob("THOR_SEQ_CLASSES", TS_NCLS);
+  ncls = ncls < 1 ? 1 : (ncls > TS_NCLS ? TS_NCLS : ncls);
+  const int prio = knob("THOR_SEQ_PRIO", 0) && ncls >= 3;
   // the jobs: each context's frames in coding order, its host state advanced frame by frame
   hipStream_t st = lead->stream;
   std::vector<TsJob> jobs(njobs);
@@ -618,7 +628,7 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
   };
   for (int i = 0; i < n; i++) {
     thor_enc *e = es[i];
-    const int cls = (int)((long long)i * TS_NCLS / n);
+    const int cls = (int)((long long)i * ncls / n);
     for (int f = 0; f < nframes; f++) {
       const int jx = i * nframes + f;
       TsJob &T = jobs[jx];
@@ -645,7 +655,14 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
       T.dst = orig;
       T.next = f + 1 < nframes ? jx + 1 : -1;
       T.next2 = f + 2 < nframes ? jx + 2 : -1;
+      // classes: stream groups (THOR_SEQ_PRIO 0), or by task kind (1): the loop filters, packing and
+      // input copies first (a frame's hand-off to the next), then P-frame SBs, then I-frame SBs by stream group
       T.cls = cls;
+      T.aux = cls;
+      if (prio) {
+        T.aux = 0;
+        T.cls = pl.frame_type != TE_I ? 1 : 2 + (int)((long long)i * (ncls - 2) / n);
+      }
       T.need0 = (fetch ? nsbv : 0) + (f > 0) + (f > 1);
       T.is_i = pl.frame_type == TE_I;
       uint8_t *cs = e->slots + (long long)cur * e->slot_bytes;
@@ -659,7 +676,8 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
       T.deblock = e->p.deblocking;
       run.frame_num[i][f] = pl.frame_num;
       // tasks of the job: RD nsb, DBV / DBH / FIN nsbv each, PACK 1 (+ FETCH nsbv)
-      qn[cls] += nsb + 3 * nsbv + 1 + (fetch ? nsbv : 0);
+      qn[T.cls] += nsb;
+      qn[T.aux] += 3 * nsbv + 1 + (fetch ? nsbv : 0);
       // advance the context as thor_enc_frames_begin does
       for (int r = 32; r > 0; r--) e->slot_of_window[r] = e->slot_of_window[r - 1];
       e->slot_of_window[0] = cur;
@@ -689,7 +707,7 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
     const int jx = i * nframes;
     const TsJob &T = jobs[jx];
     if (fetch)
-      for (int r = 0; r < nsbv; r++) init[T.cls].push_back(ts_item(jx, TS_FETCH, r));
+      for (int r = 0; r < nsbv; r++) init[T.aux].push_back(ts_item(jx, TS_FETCH, r));
     else
       init[T.cls].push_back(ts_item(jx, TS_RD, 0));
     for (int f = 0; f < nframes; f++) n_i += jobs[jx + f].is_i;
@@ -721,12 +739,17 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
   A.ctl = S.ctl;
   A.items = S.items;
   A.err = P.err;
-  for (int c = 0; c < TS_NCLS; c++) A.qoff[c] = qoff[c];
+  for (int c = 0; c < TS_NCLS; c++) {
+    A.qoff[c] = qoff[c];
+    A.qtot[c] = qn[c];
+  }
+  A.ncls = ncls;
+  A.claim = knob("THOR_SEQ_CLAIM", 0);
   A.total = total;
   A.n_ijobs = n_i;
   A.min_alive = nwork / 2;
   A.spin_limit = g_spin_limit.load();
-  A.retire_ticks = 50000;  // 0.5 ms without a ready task
+  A.retire_ticks = knob("THOR_SEQ_RETIRE", 1) ? 50000 : ~0ULL >> 1;  // 0.5 ms without a ready task
   A.arena = S.arena;
   A.arena_words = S.arena_words;
   A.meta = S.meta;
@@ -748,13 +771,13 @@ int thor_enc_seq_begin(thor_enc_t *const *es, int n, int nframes, const uint8_t 
   return THOR_OK;
 }
 
-// Which frames of the launch in flight are final: out[i * nframes + f] = the
+// Which frames of the launch in flight (or the last one ended) are final: out[i * nframes + f] = the
 // chunk size in bytes (4-byte length + payload), -1 not yet.  Non-blocking.
 // Returns the number of final frames.
 int thor_enc_seq_ready(thor_enc_t *e0, long long *out, int count) {
   if (!e0) return THOR_ERR_ARG;
   TsPool &S = ts_pool_for(e0->device);
-  if (!S.run.active) return THOR_ERR_ARG;
+  if (!S.meta || S.run.n <= 0) return THOR_ERR_ARG;  // (the launch in flight, or the last one ended)
   const int nj = S.run.n * S.run.nframes;
   int done = 0;
   for (int m = 0; m < nj; m++) {
@@ -805,6 +828,8 @@ int thor_enc_seq_end(thor_enc_t *e0, long long *stats) {
     EHIP(hipMemcpy(&err, P.err, sizeof(unsigned), hipMemcpyDeviceToHost));
     EHIP(hipMemcpy(ctl.data(), S.ctl, ctl.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
   }
+  for (int i = 0; i < TS_NPROF; i++)
+    S.prof[i] = (long long)ctl[TS_PROF + 2 * i] | ((long long)ctl[TS_PROF + 2 * i + 1] << 32);
   if (stats) {
     stats[0] = S.max_workers < TE_MAX_WORKERS ? S.max_workers : TE_MAX_WORKERS;
     stats[1] = ctl[TS_RETIRED];
@@ -843,6 +868,17 @@ int thor_enc_seq_end(thor_enc_t *e0, long long *stats) {
     thor_enc_seq_chunk(e0, i, R.nframes - 1, e->chunk.data(), e->chunk.size());
   }
   return THOR_OK;
+}
+
+// The last ended launch's profile (sums over its workers, 100 MHz ticks):
+// per task type (RD, FETCH, DBV, DBH, FIN, PACK) the time in tasks, then the
+// task counts, then idle time, time waiting for a claimed slot, failed claims.
+// Returns the count (15), copies min(15, n).
+int thor_enc_seq_profile(thor_enc_t *e0, long long *out, int n) {
+  if (!e0) return THOR_ERR_ARG;
+  TsPool &S = ts_pool_for(e0->device);
+  for (int i = 0; i < TS_NPROF && i < n && out; i++) out[i] = S.prof[i];
+  return TS_NPROF;
 }
 
 }  // extern "C"

@@ -225,6 +225,13 @@ class SeqLaunch:
         st = (C.c_longlong * 4)()
         L.check(self.lib.thor_enc_seq_end(self.encs[0].h, st), "thor_enc_seq_end")
         self.stats = {"workers": st[0], "retired": st[1], "tasks": st[2], "arena_words": st[3]}
+        pr = (C.c_longlong * 15)()
+        self.lib.thor_enc_seq_profile(self.encs[0].h, pr, 15)
+        names = ["rd", "fetch", "dbv", "dbh", "fin", "pack"]
+        self.profile = {"task_ms": {k: round(pr[i] / 1e5, 1) for i, k in enumerate(names)},
+                        "tasks": {k: pr[6 + i] for i, k in enumerate(names)},
+                        "idle_ms": round(pr[12] / 1e5, 1), "claim_wait_ms": round(pr[13] / 1e5, 1),
+                        "failed_claims": pr[14]}
         return self.stats
 
 

@@ -6,7 +6,7 @@ bench clips, tests/golden/bench_clips.json), coded
   fetch : the same with the raw frames read from page-locked host memory by
           the launch itself (FETCH tasks)
 Each stream's .bit md5 is checked against the reference Thorenc's.
-Usage: python3 tools/seq_speed.py [K] [modes, comma separated] [reps]"""
+Usage: python3 tools/seq_speed.py [K] [modes, comma separated; mode:KNOB=v sets THOR_SEQ_KNOB] [reps]"""
 import hashlib
 import json
 import os
@@ -69,15 +69,24 @@ def run_batch():
     return [b"".join(b) for b in bits], None
 
 
-def run_seq(fetch):
+def run_seq(fetch, pre=0, nseq=None):
+    """pre frames per frame batch first, then nseq (default: the rest) in one
+    sequence launch, then the rest per frame batch"""
     for e in encs:
         e.reset()
+    from thor_amd.encoder import encode_batch
+
+    head = [[] for _ in range(K)]
+    for _ in range(pre):
+        for k, ch in enumerate(encode_batch(encs)):
+            head[k].append(ch)
+    nseq = nseq or nf - pre
     if fetch:
         for b in inbuf:
             b.zero_()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    s = SeqLaunch(encs, nf, host=(lambda i, k: host[i % nclip][k].data_ptr()) if fetch else None)
+    s = SeqLaunch(encs, nseq, host=(lambda i, k: host[i % nclip][k].data_ptr()) if fetch else None)
     first = None
     tl = []
     while True:
@@ -87,24 +96,41 @@ def run_seq(fetch):
             first = time.perf_counter() - t0
         if not tl or tl[-1][1] != d:
             tl.append((round((time.perf_counter() - t0) * 1e3, 1), d))
-        if d == K * nf or time.perf_counter() - t0 > 120:  # (a wedged launch gives up after 60 s)
+        if d == K * nseq or time.perf_counter() - t0 > 120:  # (a wedged launch gives up after 60 s)
             break
         time.sleep(0.001)
     st = s.end()
-    bits = [b"".join(s.chunk(k, f) for f in range(nf)) for k in range(K)]
+    t_seq = time.perf_counter() - t0
+    tail = [[] for _ in range(K)]
+    for _ in range(nf - pre - nseq):
+        for k, ch in enumerate(encode_batch(encs)):
+            tail[k].append(ch)
+    bits = [b"".join(head[k] + [s.chunk(k, f) for f in range(nseq)] + tail[k]) for k in range(K)]
     # frames final per 100 ms
-    marks = [(t, d) for t, d in tl if d in (1, K, K * nf // 2, K * nf)]
-    return bits, {"stats": st, "first_final_ms": round(first * 1e3, 1), "marks": marks[:8]}
+    marks = [(t, d) for t, d in tl if d in (1, K, K * nseq // 2, K * nseq)]
+    return bits, {"seq_ms": round(t_seq * 1e3, 1), "stats": st, "profile": s.profile, "env": {k: v for k, v in os.environ.items() if k.startswith("THOR_SEQ")}, "first_final_ms": round(first * 1e3, 1), "marks": marks[:8]}
 
 
-for m in MODES:
+for spec in MODES:
+    # mode[:KNOB=v[:KNOB=v]]: THOR_SEQ_<KNOB> set for this mode's runs (read at each launch)
+    m, *kv = spec.split(":")
+    for k in [k for k in os.environ if k.startswith("THOR_SEQ_")]:
+        del os.environ[k]
+    for x in kv:
+        k, v = x.split("=")
+        os.environ["THOR_SEQ_" + k] = v
     for r in range(REPS):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        bits, extra = run_batch() if m == "batch" else run_seq(m == "fetch")
+        if m == "batch":
+            bits, extra = run_batch()
+        else:  # seq / fetch [ /PRE / NSEQ ]: e.g. seq/1 = frame 0 per batch, frames 1-7 in one launch
+            parts = m.split("/")
+            bits, extra = run_seq(parts[0] == "fetch", int(parts[1]) if len(parts) > 1 else 0,
+                                  int(parts[2]) if len(parts) > 2 else None)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"mode": m, "streams": K, "rep": r, "ms": round(dt * 1e3, 1),
+        print(json.dumps({"mode": spec, "streams": K, "rep": r, "ms": round(dt * 1e3, 1),
                           "enc_mpx_s": round(K * nf * W * H / dt / 1e6, 1), "check": check(bits), "extra": extra}),
               flush=True)
 for e in encs:
