@@ -445,6 +445,10 @@ int thor_enc_seq_end(thor_enc_t *e0, long long *stats);
  * then the task counts, then idle time, time waiting for a claimed queue slot
  * and failed claims.  Returns 15; copies min(15, n) values. */
 int thor_enc_seq_profile(thor_enc_t *e0, long long *out, int n);
+/* The per-frame batch RD kernel's profile since the last call on `device`,
+ * summed over its workers (100 MHz ticks): time coding superblocks, time
+ * waiting for a queue slot, superblocks coded; cleared.  Returns 3. */
+int thor_enc_rows_profile(int device, long long *out);
 /* The last coded frame's reconstruction (deblocked, CLPF'd), host planes. */
 int thor_enc_read_recon(thor_enc_t *e, uint8_t *y, uint8_t *u, uint8_t *v);
 /* Per-superblock RD costs (parity instrumentation, tests/golden/rd_costs.npz):

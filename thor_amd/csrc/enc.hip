@@ -102,6 +102,9 @@ __device__ __forceinline__ void te_dep_done(const TeJob &J, int s, int k, int l,
     __hip_atomic_store(&items[slot], te_q_item(s, k, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+// k_enc_rows' profile, summed over its workers across launches (100 MHz ticks): time coding SBs,
+// time waiting for a queue slot, SBs coded (thor_enc_rows_profile reads and clears it)
+__device__ unsigned long long g_te_rows_prof[4];
 __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, unsigned total, unsigned *q,
                                                  unsigned *items, TeScratchMem *scratch, unsigned *err,
                                                  unsigned long long spin_limit, int stall_row) {
@@ -115,8 +118,10 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   TeSB &sb = s_sb;
   const int lane = threadIdx.x;
   int cur = -1;  // the job whose frame parameters s_F holds
+  unsigned long long t_work = 0, t_wait = 0, n_sb = 0;  // (lane 0) this worker's profile
   for (;;) {
     unsigned h = 0;
+    const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) h = __hip_atomic_fetch_add(&q[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h = __builtin_amdgcn_readfirstlane(h);
     if (h >= total) break;
@@ -138,6 +143,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     }
     if (__builtin_amdgcn_readfirstlane(gave_up)) break;  // this wave waits no more, so the grid drains
     item = __builtin_amdgcn_readfirstlane(item);
+    const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
+    t_wait += tb0 - tw0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int s = (int)(item >> 22), k = (int)((item >> 11) & 2047), l = (int)(item & 2047);
@@ -169,7 +176,14 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
         if (l >= 1) te_dep_done(J, s, k + 1, l - 1, q, items);
         if (l == J.nsbh - 1) te_dep_done(J, s, k + 1, l, q, items);
       }
+      t_work += __builtin_amdgcn_s_memrealtime() - tb0;
+      n_sb++;
     }
+  }
+  if (lane == 0) {
+    atomicAdd(&g_te_rows_prof[0], t_work);
+    atomicAdd(&g_te_rows_prof[1], t_wait);
+    atomicAdd(&g_te_rows_prof[2], n_sb);
   }
 }
 
@@ -1179,6 +1193,19 @@ int thor_enc_debug_stall(int row, int spin_ms) {
   g_stall_row.store(row);
   g_spin_limit.store(spin_ms > 0 ? (unsigned long long)spin_ms * 100000ULL : 30000000000ULL);
   return THOR_OK;
+}
+
+// k_enc_rows' profile since the last call, summed over its workers (100 MHz ticks): time coding
+// SBs, time waiting for a queue slot, SBs coded; cleared.  Returns 3.
+int thor_enc_rows_profile(int device, long long *out) {
+  unsigned long long v[4] = {0, 0, 0, 0};
+  EHIP(hipSetDevice(device));
+  EHIP(hipDeviceSynchronize());
+  EHIP(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_te_rows_prof), sizeof(v)));
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  EHIP(hipMemcpyToSymbol(HIP_SYMBOL(g_te_rows_prof), z, sizeof(z)));
+  for (int i = 0; out && i < 3; i++) out[i] = (long long)v[i];
+  return 3;
 }
 
 int thor_enc_frame(thor_enc_t *e, const uint8_t *orig, int orig_stride) {

@@ -128,7 +128,7 @@ __device__ __forceinline__ unsigned ts_pop(const TsArgs &A, unsigned long long &
     }
     unsigned item;
     const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
-    while ((item = te_ld_relaxed(&A.items[A.qoff[c] + h])) == TE_Q_EMPTY) __builtin_amdgcn_s_sleep(1);
+    while ((item = te_ld_relaxed(&A.items[A.qoff[c] + h])) == TE_Q_EMPTY) __builtin_amdgcn_s_sleep(4);
     waits += __builtin_amdgcn_s_memrealtime() - w0;
     return item;
   }
@@ -166,6 +166,174 @@ __device__ void ts_copy_range(uint8_t *dst, const uint8_t *src, long long a, lon
     for (; i < n; i += 64) d[i] = s[i];
   } else {
     for (long long i = a + lane; i < b; i += 64) dst[i] = src[i];
+  }
+}
+
+// The tasks other than RD (FETCH, DBV, DBH, FIN, PACK), out of line: k_enc_seq's
+// RD path keeps the register allocation k_enc_rows has (the task bodies inlined
+// beside te_encode_sb cost the P-frame SBs a third more time).
+__device__ __noinline__ void ts_aux(const TsArgs &A, int j, int type, int idx) {
+  const int lane = threadIdx.x;
+  const TsJob &T = A.jobs[j];
+  const TeJob &J = T.J;
+  const int W = J.F.W, H = J.F.H, nsbh = J.nsbh, nsbv = J.nsbv;
+  (void)nsbh;
+  if (type == TS_FETCH) {
+    const int k = idx;
+    const long long ys = (long long)W * H, cw = W >> 1;
+    const long long y0 = (long long)(k * 64) * W, y1 = (long long)min(k * 64 + 64, H) * W;
+    const long long c0 = (long long)(k * 32) * cw, c1 = (long long)min(k * 32 + 32, H >> 1) * cw;
+    ts_copy_range(T.dst, T.src, y0, y1);
+    ts_copy_range(T.dst, T.src, ys + c0, ys + c1);
+    ts_copy_range(T.dst, T.src, ys + ys / 4 + c0, ys + ys / 4 + c1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) ts_dep(A, &J.deps[0], (unsigned)T.need0, T.cls, ts_item(j, TS_RD, 0));
+  } else if (type == TS_DBV) {
+    const int k = idx;
+    if (T.deblock) {
+      const int ne = (W >> 3) - 1, g0 = k * 8, g1 = min(k * 8 + 8, H >> 3);
+      for (int b = g0 * ne; b < g1 * ne; b += 64 * DB_ITEMS)
+        luma_v_items<DB_ITEMS>(b + lane, 64, T.cy, T.sy, W, H, J.cellinfo, T.qp, g0, g1);
+      for (int t = g0 * ne + lane; t < g1 * ne; t += 64)
+        for (int pl = 0; pl < 2; pl++)
+          k_deblock_chroma_v_body(t, pl, T.cu, T.cv, T.sc, W, H, J.cellinfo, T.qpc, g0, g1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      ts_dep(A, &T.dbh[k], 1u + (k > 0), T.aux, ts_item(j, TS_DBH, k));
+      if (k + 1 < nsbv) ts_dep(A, &T.dbh[k + 1], 2u, T.aux, ts_item(j, TS_DBH, k + 1));
+    }
+  } else if (type == TS_DBH) {
+    const int k = idx;
+    if (T.deblock) {
+      // edges at luma rows i = (kk + 1) * 8 in [64k, 64k + 56]
+      const int ng = W >> 3, kk0 = k * 8 - 1 < 0 ? 0 : k * 8 - 1, kk1 = min(k * 8 + 7, (H >> 3) - 1);
+      const int i0 = k * 64, i1 = k * 64 + 56;
+      for (int b = kk0 * ng; b < kk1 * ng; b += 64 * DB_ITEMS)
+        luma_h_items<DB_ITEMS>(b + lane, 64, T.cy, T.sy, W, H, J.cellinfo, T.qp, i0, i1);
+      for (int t = kk0 * ng + lane; t < kk1 * ng; t += 64)
+        for (int pl = 0; pl < 2; pl++)
+          k_deblock_chroma_h_body(t, pl, T.cu, T.cv, T.sc, W, H, J.cellinfo, T.qpc, i0, i1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      if (k > 0) ts_dep(A, &T.fin[k - 1], 2u, T.aux, ts_item(j, TS_FIN, k - 1));
+      ts_dep(A, &T.fin[k], 1u + (k + 1 < nsbv), T.aux, ts_item(j, TS_FIN, k));
+    }
+  } else if (type == TS_FIN) {
+    const int k = idx;
+    if (J.clpf && k < (H >> 6)) {
+      for (int l = 0; l < (W >> 6); l++) {
+        const int d = te_clpf_decide_blk(J.cellinfo, W, J.F.ry, J.F.rsy, J.F.oy, J.F.osy, k, l);
+        if (lane == 0) J.clpf_bits[k * (W >> 6) + l] = (int8_t)d;
+        if (d == 1) te_clpf_apply_blk(J.cellinfo, W, T.cy, T.sy, T.cu, T.cv, T.sc, k, l);
+      }
+    }
+    te_sync();
+    {  // padding of the row's pixels (and the top / bottom pad rows at the frame's ends)
+      const int r0 = k * 64, r1 = min(k * 64 + 64, H);
+      const PadPlane py(T.cy, T.sy, W, H, THOR_PAD_Y, r0, r1);
+      for (int e = lane; e < py.total; e += 64) py.chunk(e);
+      const PadPlane pu(T.cu, T.sc, W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
+      for (int e = lane; e < pu.total; e += 64) pu.chunk(e);
+      const PadPlane pv(T.cv, T.sc, W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
+      for (int e = lane; e < pv.total; e += 64) pv.chunk(e);
+    }
+    {  // the row's cell state to zero (deblock_data, cleared per frame): the next frame's RD loop
+      const int cs = W >> 2, q0 = k * 16, q1 = min(k * 16 + 16, H >> 2);
+      uint4 *c = (uint4 *)(J.F.cells + (long long)q0 * cs);
+      const long long n16 = (long long)(q1 - q0) * cs * (long long)sizeof(TeCell) / 16;
+      for (long long i = lane; i < n16; i += 64) c[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      const unsigned old = __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1 == (unsigned)nsbv) {  // the frame is a finished reference
+        ts_push(A, T.aux, ts_item(j, TS_PACK, 0));
+        if (T.next >= 0) {
+          const TsJob &N = A.jobs[T.next];
+          ts_dep(A, &N.J.deps[0], (unsigned)N.need0, N.cls, ts_item(T.next, TS_RD, 0));
+        }
+        if (T.is_i) atomicAdd(&A.ctl[TS_IDONE], 1u);
+      }
+    }
+  } else {  // TS_PACK
+    const int nsb = nsbh * nsbv;
+    const int per = (nsb + 63) >> 6, s0 = min(lane * per, nsb), s1 = min(s0 + per, nsb);
+    int mine = 0;
+    for (int i = s0; i < s1; i++) mine += te_sb_bits(J, i);
+    int incl = mine;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const int sbits = __builtin_amdgcn_readlane(incl, 63);
+    int nclpf = 0;
+    const int nf = (W >> 6) * (H >> 6);
+    if (J.clpf)
+      for (int i = lane; i < nf; i += 64) nclpf += J.clpf_bits[i] >= 0;
+    const long long total = (long long)J.hdr_bits + sbits + (J.clpf ? 2 + (long long)te_sum((uint32_t)nclpf) : 0);
+    const long long nw = (total + 31) >> 5;
+    unsigned long long off = 0;
+    int ok = nw <= A.out_cap_words;
+    if (ok && lane == 0) {
+      off = __hip_atomic_fetch_add((unsigned long long *)&A.ctl[TS_ARENA], (unsigned long long)((nw + 3) & ~3LL),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (off + nw > A.arena_words) ok = 0;
+    }
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    off = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
+          (unsigned)__builtin_amdgcn_readfirstlane((int)(off & 0xffffffffu));
+    if (!ok) {
+      if (lane == 0) atomicOr(A.err, 4u);  // the frame exceeds the output buffer or the host arena
+    } else {
+      uint32_t *out = J.out_words;
+      for (long long i = lane; i < ((nw + 3) & ~3LL) + 4; i += 64) out[i] = 0u;
+      __threadfence();
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) te_or_bits(out, 0, J.hdr_words, J.hdr_bits);
+      long long pos = (long long)J.hdr_bits + (incl - mine);
+      for (int i = s0; i < s1; i++) {
+        const int b = te_sb_bits(J, i);
+        te_or_bits(out, pos, J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, b);
+        pos += b;
+      }
+      if (lane == 0 && J.clpf) {
+        long long p = (long long)J.hdr_bits + sbits;
+        const uint32_t two = 0x80000000u;  // bits 1, 0
+        te_or_bits(out, p, &two, 2);
+        p += 2;
+        for (int i = 0; i < nf; i++) {
+          const int d = J.clpf_bits[i];
+          if (d < 0) continue;
+          if (d) atomicOr(&out[p >> 5], 0x80000000u >> (p & 31));
+          p++;
+        }
+      }
+      __threadfence();
+      __builtin_amdgcn_wave_barrier();
+      uint4 *dst = (uint4 *)(A.arena + off);
+      const uint4 *src = (const uint4 *)out;
+      for (long long i = lane; i < (nw + 3) >> 2; i += 64) dst[i] = src[i];
+      // a system-scope RELEASE (the words reach host memory before the size): __threadfence_system
+      // would also invalidate this XCD's L2 under every other worker there
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        A.meta[2 * j] = (int)off;
+        __hip_atomic_store(&A.meta[2 * j + 1], (int)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0 && T.next2 >= 0) {  // frame f + 2 may write this frame's SB buffers
+      const TsJob &N = A.jobs[T.next2];
+      ts_dep(A, &N.J.deps[0], (unsigned)N.need0, N.cls, ts_item(T.next2, TS_RD, 0));
+    }
   }
 }
 
@@ -235,7 +403,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
     const TsJob &T = A.jobs[j];
     const TeJob &J = T.J;
     const int W = J.F.W, H = J.F.H, nsbh = J.nsbh, nsbv = J.nsbv;
-    if ((type == TS_RD || type == TS_FIN) && j != cur) {  // the job's frame parameters into LDS
+    if (type == TS_RD && j != cur) {  // the job's frame parameters into LDS
       const uint32_t *src = (const uint32_t *)&J.F;
       uint32_t *dst = (uint32_t *)&s_F;
       te_sync();
@@ -276,160 +444,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
           if (k == nsbv - 1) ts_push(A, T.aux, ts_item(j, TS_DBV, k));
         }
       }
-    } else if (type == TS_FETCH) {
-      const int k = idx;
-      const long long ys = (long long)W * H, cw = W >> 1;
-      const long long y0 = (long long)(k * 64) * W, y1 = (long long)min(k * 64 + 64, H) * W;
-      const long long c0 = (long long)(k * 32) * cw, c1 = (long long)min(k * 32 + 32, H >> 1) * cw;
-      ts_copy_range(T.dst, T.src, y0, y1);
-      ts_copy_range(T.dst, T.src, ys + c0, ys + c1);
-      ts_copy_range(T.dst, T.src, ys + ys / 4 + c0, ys + ys / 4 + c1);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) ts_dep(A, &J.deps[0], (unsigned)T.need0, T.cls, ts_item(j, TS_RD, 0));
-    } else if (type == TS_DBV) {
-      const int k = idx;
-      if (T.deblock) {
-        const int ne = (W >> 3) - 1, g0 = k * 8, g1 = min(k * 8 + 8, H >> 3);
-        for (int b = g0 * ne; b < g1 * ne; b += 64 * DB_ITEMS)
-          luma_v_items<DB_ITEMS>(b + lane, 64, T.cy, T.sy, W, H, J.cellinfo, T.qp, g0, g1);
-        for (int t = g0 * ne + lane; t < g1 * ne; t += 64)
-          for (int pl = 0; pl < 2; pl++)
-            k_deblock_chroma_v_body(t, pl, T.cu, T.cv, T.sc, W, H, J.cellinfo, T.qpc, g0, g1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        ts_dep(A, &T.dbh[k], 1u + (k > 0), T.aux, ts_item(j, TS_DBH, k));
-        if (k + 1 < nsbv) ts_dep(A, &T.dbh[k + 1], 2u, T.aux, ts_item(j, TS_DBH, k + 1));
-      }
-    } else if (type == TS_DBH) {
-      const int k = idx;
-      if (T.deblock) {
-        // edges at luma rows i = (kk + 1) * 8 in [64k, 64k + 56]
-        const int ng = W >> 3, kk0 = k * 8 - 1 < 0 ? 0 : k * 8 - 1, kk1 = min(k * 8 + 7, (H >> 3) - 1);
-        const int i0 = k * 64, i1 = k * 64 + 56;
-        for (int b = kk0 * ng; b < kk1 * ng; b += 64 * DB_ITEMS)
-          luma_h_items<DB_ITEMS>(b + lane, 64, T.cy, T.sy, W, H, J.cellinfo, T.qp, i0, i1);
-        for (int t = kk0 * ng + lane; t < kk1 * ng; t += 64)
-          for (int pl = 0; pl < 2; pl++)
-            k_deblock_chroma_h_body(t, pl, T.cu, T.cv, T.sc, W, H, J.cellinfo, T.qpc, i0, i1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        if (k > 0) ts_dep(A, &T.fin[k - 1], 2u, T.aux, ts_item(j, TS_FIN, k - 1));
-        ts_dep(A, &T.fin[k], 1u + (k + 1 < nsbv), T.aux, ts_item(j, TS_FIN, k));
-      }
-    } else if (type == TS_FIN) {
-      const int k = idx;
-      if (J.clpf && k < (H >> 6)) {
-        for (int l = 0; l < (W >> 6); l++) {
-          const int d = te_clpf_decide_blk(J.cellinfo, W, J.F.ry, J.F.rsy, J.F.oy, J.F.osy, k, l);
-          if (lane == 0) J.clpf_bits[k * (W >> 6) + l] = (int8_t)d;
-          if (d == 1) te_clpf_apply_blk(J.cellinfo, W, T.cy, T.sy, T.cu, T.cv, T.sc, k, l);
-        }
-      }
-      te_sync();
-      {  // padding of the row's pixels (and the top / bottom pad rows at the frame's ends)
-        const int r0 = k * 64, r1 = min(k * 64 + 64, H);
-        const PadPlane py(T.cy, T.sy, W, H, THOR_PAD_Y, r0, r1);
-        for (int e = lane; e < py.total; e += 64) py.chunk(e);
-        const PadPlane pu(T.cu, T.sc, W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
-        for (int e = lane; e < pu.total; e += 64) pu.chunk(e);
-        const PadPlane pv(T.cv, T.sc, W >> 1, H >> 1, THOR_PAD_C, r0 >> 1, r1 >> 1);
-        for (int e = lane; e < pv.total; e += 64) pv.chunk(e);
-      }
-      {  // the row's cell state to zero (deblock_data, cleared per frame): the next frame's RD loop
-        const int cs = W >> 2, q0 = k * 16, q1 = min(k * 16 + 16, H >> 2);
-        uint4 *c = (uint4 *)(J.F.cells + (long long)q0 * cs);
-        const long long n16 = (long long)(q1 - q0) * cs * (long long)sizeof(TeCell) / 16;
-        for (long long i = lane; i < n16; i += 64) c[i] = make_uint4(0u, 0u, 0u, 0u);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        const unsigned old = __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1 == (unsigned)nsbv) {  // the frame is a finished reference
-          ts_push(A, T.aux, ts_item(j, TS_PACK, 0));
-          if (T.next >= 0) {
-            const TsJob &N = A.jobs[T.next];
-            ts_dep(A, &N.J.deps[0], (unsigned)N.need0, N.cls, ts_item(T.next, TS_RD, 0));
-          }
-          if (T.is_i) atomicAdd(&A.ctl[TS_IDONE], 1u);
-        }
-      }
-    } else {  // TS_PACK
-      const int nsb = nsbh * nsbv;
-      const int per = (nsb + 63) >> 6, s0 = min(lane * per, nsb), s1 = min(s0 + per, nsb);
-      int mine = 0;
-      for (int i = s0; i < s1; i++) mine += te_sb_bits(J, i);
-      int incl = mine;
-      for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d);
-        if (lane >= d) incl += v;
-      }
-      const int sbits = __builtin_amdgcn_readlane(incl, 63);
-      int nclpf = 0;
-      const int nf = (W >> 6) * (H >> 6);
-      if (J.clpf)
-        for (int i = lane; i < nf; i += 64) nclpf += J.clpf_bits[i] >= 0;
-      const long long total = (long long)J.hdr_bits + sbits + (J.clpf ? 2 + (long long)te_sum((uint32_t)nclpf) : 0);
-      const long long nw = (total + 31) >> 5;
-      unsigned long long off = 0;
-      int ok = nw <= A.out_cap_words;
-      if (ok && lane == 0) {
-        off = __hip_atomic_fetch_add((unsigned long long *)&A.ctl[TS_ARENA], (unsigned long long)((nw + 3) & ~3LL),
-                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (off + nw > A.arena_words) ok = 0;
-      }
-      ok = __builtin_amdgcn_readfirstlane(ok);
-      off = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
-            (unsigned)__builtin_amdgcn_readfirstlane((int)(off & 0xffffffffu));
-      if (!ok) {
-        if (lane == 0) atomicOr(A.err, 4u);  // the frame exceeds the output buffer or the host arena
-      } else {
-        uint32_t *out = J.out_words;
-        for (long long i = lane; i < ((nw + 3) & ~3LL) + 4; i += 64) out[i] = 0u;
-        __threadfence();
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) te_or_bits(out, 0, J.hdr_words, J.hdr_bits);
-        long long pos = (long long)J.hdr_bits + (incl - mine);
-        for (int i = s0; i < s1; i++) {
-          const int b = te_sb_bits(J, i);
-          te_or_bits(out, pos, J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, b);
-          pos += b;
-        }
-        if (lane == 0 && J.clpf) {
-          long long p = (long long)J.hdr_bits + sbits;
-          const uint32_t two = 0x80000000u;  // bits 1, 0
-          te_or_bits(out, p, &two, 2);
-          p += 2;
-          for (int i = 0; i < nf; i++) {
-            const int d = J.clpf_bits[i];
-            if (d < 0) continue;
-            if (d) atomicOr(&out[p >> 5], 0x80000000u >> (p & 31));
-            p++;
-          }
-        }
-        __threadfence();
-        __builtin_amdgcn_wave_barrier();
-        uint4 *dst = (uint4 *)(A.arena + off);
-        const uint4 *src = (const uint4 *)out;
-        for (long long i = lane; i < (nw + 3) >> 2; i += 64) dst[i] = src[i];
-        __threadfence_system();
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          A.meta[2 * j] = (int)off;
-          __hip_atomic_store(&A.meta[2 * j + 1], (int)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0 && T.next2 >= 0) {  // frame f + 2 may write this frame's SB buffers
-        const TsJob &N = A.jobs[T.next2];
-        ts_dep(A, &N.J.deps[0], (unsigned)N.need0, N.cls, ts_item(T.next2, TS_RD, 0));
-      }
+    } else {
+      ts_aux(A, j, type, idx);
     }
     if (lane == 0) {
       __hip_atomic_fetch_add(&A.ctl[TS_NDONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

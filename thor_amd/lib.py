@@ -68,7 +68,7 @@ BATCHED_SYMBOLS = [
     "thor_enc_tu_batch", "thor_enc_cost_batch",
     "thor_enc_default_params", "thor_enc_check_params", "thor_enc_create", "thor_enc_destroy", "thor_enc_num_frames",
     "thor_enc_next_input", "thor_enc_stream", "thor_enc_set_cu_mask", "thor_enc_frames", "thor_enc_frames_begin", "thor_enc_frames_end", "thor_enc_frame", "thor_enc_frame_bytes",
-    "thor_enc_plan_input", "thor_enc_seq_begin", "thor_enc_seq_ready", "thor_enc_seq_chunk", "thor_enc_seq_end", "thor_enc_seq_profile",
+    "thor_enc_plan_input", "thor_enc_seq_begin", "thor_enc_seq_ready", "thor_enc_seq_chunk", "thor_enc_seq_end", "thor_enc_seq_profile", "thor_enc_rows_profile",
     "thor_enc_read_recon", "thor_enc_reset", "thor_enc_debug_stall", "thor_enc_record_sb_costs", "thor_enc_sb_costs",
     "thor_parser_create", "thor_parser_destroy", "thor_parser_seq", "thor_parse_frame", "thor_frame_image",
     "thor_ti_create", "thor_ti_destroy", "thor_interpolate_frames", "thor_ti_read_fields", "thor_ti_status",
@@ -196,6 +196,8 @@ def load(path: str = LIB_PATH):
     L.thor_enc_seq_ready.restype = i
     L.thor_enc_seq_chunk.argtypes = [P, i, i, P, C.c_size_t]
     L.thor_enc_seq_chunk.restype = C.c_longlong
+    L.thor_enc_rows_profile.argtypes = [i, P]
+    L.thor_enc_rows_profile.restype = i
     L.thor_enc_seq_profile.argtypes = [P, P, i]
     L.thor_enc_seq_profile.restype = i
     L.thor_enc_seq_end.argtypes = [P, P]

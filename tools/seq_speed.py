@@ -56,17 +56,33 @@ def check(bits):
     return "bit-exact" if not bad else "MISMATCH streams %s" % bad[:8]
 
 
-def run_batch():
+def rows_profile():
+    import ctypes as C
+
+    v = (C.c_longlong * 3)()
+    lib.thor_enc_rows_profile(0, v)
+    return {"rd_ms": round(v[0] / 1e5, 1), "wait_ms": round(v[1] / 1e5, 1), "sbs": v[2]}
+
+
+def run_batch(nb=None):
+    """every frame per frame batch; with nb, the rows profile of the first nb frames apart"""
     for e in encs:
         e.reset()
+    rows_profile()
     bits = [[] for _ in range(K)]
+    prof = {}
     encode_batch_begin(encs)
     for i in range(nf):
-        if i + 1 < nf:
+        if i + 1 < nf and i + 1 != nb:
             encode_batch_begin(encs)
         for k, ch in enumerate(encode_batch_end(encs)):
             bits[k].append(ch)
-    return [b"".join(b) for b in bits], None
+        if nb and i + 1 == nb:
+            prof["first_%d" % nb] = rows_profile()
+            if nb < nf:
+                encode_batch_begin(encs)
+    prof["rows_profile"] = rows_profile()
+    return [b"".join(b) for b in bits], prof
 
 
 def run_seq(fetch, pre=0, nseq=None):
@@ -122,8 +138,8 @@ for spec in MODES:
     for r in range(REPS):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if m == "batch":
-            bits, extra = run_batch()
+        if m.startswith("batch"):  # batch[/NB]: the first NB frames' profile apart
+            bits, extra = run_batch(int(m.split("/")[1]) if "/" in m else None)
         else:  # seq / fetch [ /PRE / NSEQ ]: e.g. seq/1 = frame 0 per batch, frames 1-7 in one launch
             parts = m.split("/")
             bits, extra = run_seq(parts[0] == "fetch", int(parts[1]) if len(parts) > 1 else 0,
