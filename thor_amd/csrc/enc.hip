@@ -10,12 +10,14 @@
 //                   enc/encode_block.c:2819-2879).  The RD loop of
 //                   the SB (enc_rd.h) writes the reconstruction into the ring
 //                   slot, the 4x4 side info and the SB's bit string.
-//   k_enc_cellinfo  side info -> the decoder's 16-bit cell words
-//   k_deblock_v/h   the decoder's loop filter kernels (loopfilter.hip)
+//                   Each SB's cells also become the loop filters' 16-bit words there.
+//   k_enc_db_v/h    deblocking of every job's frame (the decoder's bodies, loopfilter.hip)
 //   k_enc_clpf      CLPF decision per full SB (clpf_decision, enc/encode_frame.c:50-63)
-//   k_clpf, k_pad   the decoder's CLPF and padding kernels
+//                   and CLPF of the flagged ones, one 8x8 block per lane
+//   k_enc_pad       padding (the decoder's body)
 //   k_enc_pack      frame header + SB bit strings + CLPF bits -> the frame's
-//                   bytes (putbits / flush_all_bits, enc/putbits.c:57-129)
+//                   bytes (putbits / flush_all_bits, enc/putbits.c:57-129),
+//                   written straight into page-locked host memory
 #include <atomic>
 
 #include "common.h"
@@ -49,7 +51,7 @@ struct TeJob {
   int hdr_bits;
   uint32_t *out_words;  // packed frame
   int *out_bits;
-  int nsbh, nsbv, clpf;
+  int nsbh, nsbv, clpf, deblock;
   int32_t *sb_costs;    // optional [nsb][cost_stride]: each SB's delta-QP trial costs, then its final cost
   int cost_stride;
 };
@@ -102,6 +104,26 @@ __device__ __forceinline__ void te_dep_done(const TeJob &J, int s, int k, int l,
     __hip_atomic_store(&items[slot], te_q_item(s, k, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+// the 16-bit loop-filter word of a cell (the decoder's packing, prep_body in recon.hip)
+__device__ __forceinline__ uint16_t te_cellinfo_word(const TeCell &c) {
+  const int size = c.size < 8 ? 8 : c.size;
+  const int lsz = size >= 64 ? 6 : (size >= 32 ? 5 : (size >= 16 ? 4 : 3));
+  const int tb = c.tb_split > 0, pb = c.pb_part;
+  const int lqv = lsz - (((tb || pb == 2 || pb == 3) && size > 8) ? 1 : 0);
+  const int lqh = lsz - (((tb || pb == 1 || pb == 3) && size > 8) ? 1 : 0);
+  const int big = (abs(c.ip.mv0.x) >= 4) | (abs(c.ip.mv0.y) >= 4) | (abs(c.ip.mv1.x) >= 4) | (abs(c.ip.mv1.y) >= 4);
+  return (uint16_t)((c.mode & 7) | ((c.cbp_y != 0) << 3) | ((c.cbp_u != 0) << 4) | ((c.cbp_v != 0) << 5) | (big << 6) |
+                    (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
+}
+// the loop-filter words of SB (k, l)'s cells, once the SB is coded (its cells are final then)
+__device__ __forceinline__ void te_sb_cellinfo(const TeJob &J, int k, int l) {
+  const int cs = J.F.W >> 2, r0 = k * 16, c0 = l * 16;
+  for (int e = threadIdx.x; e < 256; e += 64) {
+    const int r = r0 + (e >> 4), c = c0 + (e & 15);
+    if (r < (J.F.H >> 2) && c < cs) J.cellinfo[r * cs + c] = te_cellinfo_word(J.F.cells[r * cs + c]);
+  }
+}
+
 // k_enc_rows' profile, summed over its workers across launches (100 MHz ticks): time coding SBs,
 // time waiting for a queue slot, SBs coded (thor_enc_rows_profile reads and clears it)
 __device__ unsigned long long g_te_rows_prof[4];
@@ -165,6 +187,8 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
       J.sb_nbits[sbi] = sb.bits.pos;
       if (sb.bits.pos > sb.bits.cap) atomicOr(err, 2u);
     }
+    te_sync();  // the SB's cells (written by every lane) -> the loop filters' 16-bit words
+    te_sb_cellinfo(J, k, l);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
@@ -192,7 +216,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
 // context), 16-byte stores; the scheduler queue: each job's SB (0, 0) in slot
 // s, the job's other SBs' slots empty, head 0, tail n.
 __global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ jobs, long long cell_bytes, unsigned *q,
-                                                   unsigned *items) {
+                                                   unsigned *items, unsigned long long *arena_ctr) {
   const int s = blockIdx.y;
   const TeJob &J = jobs[s];
   uint4 *c = (uint4 *)J.F.cells;
@@ -210,26 +234,9 @@ __global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ job
     if (s == 0) {
       q[0] = 0u;
       q[1] = gridDim.y;
+      *arena_ctr = 0ull;  // this batch's packed frames start at the host arena's first word
     }
   }
-}
-
-// TeCell (deblock_data_t) -> the 16-bit cell words the decoder's loop filter
-// kernels read (same packing as prep_body, recon.hip).
-__global__ __launch_bounds__(256) void k_enc_cellinfo(const TeJob *__restrict__ jobs) {
-  const TeJob &J = jobs[blockIdx.y];
-  const int ncell = (J.F.W >> 2) * (J.F.H >> 2);
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= ncell) return;
-  const TeCell c = J.F.cells[i];
-  const int size = c.size < 8 ? 8 : c.size;
-  const int lsz = size >= 64 ? 6 : (size >= 32 ? 5 : (size >= 16 ? 4 : 3));
-  const int tb = c.tb_split > 0, pb = c.pb_part;
-  const int lqv = lsz - (((tb || pb == 2 || pb == 3) && size > 8) ? 1 : 0);
-  const int lqh = lsz - (((tb || pb == 1 || pb == 3) && size > 8) ? 1 : 0);
-  const int big = (abs(c.ip.mv0.x) >= 4) | (abs(c.ip.mv0.y) >= 4) | (abs(c.ip.mv1.x) >= 4) | (abs(c.ip.mv1.y) >= 4);
-  J.cellinfo[i] = (uint16_t)((c.mode & 7) | ((c.cbp_y != 0) << 3) | ((c.cbp_u != 0) << 4) | ((c.cbp_v != 0) << 5) |
-                             (big << 6) | (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
 }
 
 // CLPF of a full SB with one 8x8 block per lane (block b = lane: row b >> 3,
@@ -365,17 +372,57 @@ __device__ void te_clpf_apply_blk(const uint16_t *cellinfo, int W, uint8_t *ry, 
   }
 }
 
-// CLPF decision of every full SB (after deblocking), one wave per SB.
+// The frame's loop filters, every job of the batch in one launch per pass
+// (grid y = job; the decoder's deblocking bodies, loopfilter.hip):
+// vertical edges, then horizontal edges, then CLPF decision + CLPF of each
+// full SB (one wave per SB: decide, then filter it in place when flagged --
+// an SB reads nothing outside itself), then padding.
+__global__ __launch_bounds__(256) void k_enc_db_v(const TeJob *__restrict__ jobs, int nbl) {
+  const TeJob &J = jobs[blockIdx.y];
+  if (!J.deblock) return;
+  const TeFrame &F = J.F;
+  const int b = blockIdx.x;
+  if (b < nbl) {
+    luma_v_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, F.ry, F.rsy, F.W, F.H, J.cellinfo, F.qp);
+    return;
+  }
+  const int c = (b - nbl) >= nbl, bb = b - nbl - c * nbl;  // every chroma edge segment, per plane
+  for (int r = 0; r < DB_ITEMS; r++)
+    k_deblock_chroma_v_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, F.ru, F.rv, F.rsc, F.W, F.H, J.cellinfo,
+                            te_chroma_qp(F.qp));
+}
+__global__ __launch_bounds__(256) void k_enc_db_h(const TeJob *__restrict__ jobs, int nbl) {
+  const TeJob &J = jobs[blockIdx.y];
+  if (!J.deblock) return;
+  const TeFrame &F = J.F;
+  const int b = blockIdx.x;
+  if (b < nbl) {
+    luma_h_items<DB_ITEMS>(b * 256 + (int)threadIdx.x, nbl * 256, F.ry, F.rsy, F.W, F.H, J.cellinfo, F.qp);
+    return;
+  }
+  const int c = (b - nbl) >= nbl, bb = b - nbl - c * nbl;
+  for (int r = 0; r < DB_ITEMS; r++)
+    k_deblock_chroma_h_body(bb * 256 + (int)threadIdx.x + r * nbl * 256, c, F.ru, F.rv, F.rsc, F.W, F.H, J.cellinfo,
+                            te_chroma_qp(F.qp));
+}
 __global__ __launch_bounds__(64) void k_enc_clpf(const TeJob *__restrict__ jobs) {
   const TeJob &J = jobs[blockIdx.y];
   const int nh = J.F.W >> 6, nv = J.F.H >> 6;
   const int sb = blockIdx.x;
   if (sb >= nh * nv || !J.clpf) return;
-  const int d = te_clpf_decide_blk(J.cellinfo, J.F.W, J.F.ry, J.F.rsy, J.F.oy, J.F.osy, sb / nh, sb % nh);
+  const TeFrame &F = J.F;
+  const int k = sb / nh, l = sb % nh;
+  const int d = te_clpf_decide_blk(J.cellinfo, F.W, F.ry, F.rsy, F.oy, F.osy, k, l);
   if (threadIdx.x == 0) {
     J.clpf_bits[sb] = (int8_t)d;
     J.clpf_flags[sb] = (uint8_t)(d == 1);
   }
+  if (d == 1) te_clpf_apply_blk(J.cellinfo, F.W, F.ry, F.rsy, F.ru, F.rv, F.rsc, k, l);
+}
+__global__ __launch_bounds__(256) void k_enc_pad(const TeJob *__restrict__ jobs) {
+  const TeJob &J = jobs[blockIdx.y];
+  const TeFrame &F = J.F;
+  k_pad_body(blockIdx.x * 256 + threadIdx.x, F.ry, F.ru, F.rv, F.rsy, F.rsc, F.W, F.H, 0, F.H);
 }
 
 // Frame bit string: header | SB strings (raster) | [CLPF: 1, 0, one bit per
@@ -397,11 +444,21 @@ __device__ __forceinline__ int te_sb_bits(const TeJob &J, int i) {
   const int b = J.sb_nbits[i];
   return b < 0 ? 0 : (b > THOR_ENC_SB_WORDS * 32 ? THOR_ENC_SB_WORDS * 32 : b);
 }
-__global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs, long long *scan_tmp, int out_cap_words) {
+// ... then the packed words, byte-swapped (the stream's byte order), into the
+// batch's page-locked host arena at a word offset the block takes from
+// `arena_ctr`, and (offset, bit count) into `meta` behind a system-scope
+// release: the host reads the frame with no copy kernel (small D2H copies run
+// as blit kernels, which wait for CU slots the next batch's workers hold).
+// Offset -1: the arena was full (the host copies J.out_words instead);
+// bit count -1: the frame is over the output buffer.
+__global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs, long long *scan_tmp, int out_cap_words,
+                                                  uint32_t *arena, unsigned long long arena_words,
+                                                  unsigned long long *arena_ctr, int *meta, const unsigned *err) {
   const TeJob &J = jobs[blockIdx.x];
   const int nsb = J.nsbh * J.nsbv;
   long long *off = scan_tmp + (size_t)blockIdx.x * (nsb + 1);
   __shared__ long long total;
+  __shared__ long long aoff;
   if (threadIdx.x == 0) {
     long long o = J.hdr_bits;
     for (int i = 0; i < nsb; i++) {
@@ -419,7 +476,12 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
   __syncthreads();
   const long long nw = (total + 31) >> 5;
   if (nw > out_cap_words) {
-    if (threadIdx.x == 0) *J.out_bits = -1;
+    if (threadIdx.x == 0) {
+      *J.out_bits = -1;
+      meta[2 * blockIdx.x] = -1;
+      if (blockIdx.x == 0) meta[2 * THOR_ENC_MAX_BATCH] = (int)*err;
+      __hip_atomic_store(&meta[2 * blockIdx.x + 1], -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     return;
   }
   for (long long i = threadIdx.x; i < nw + 1 && i < out_cap_words; i += 256) J.out_words[i] = 0;
@@ -440,12 +502,29 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
       p++;
     }
   }
-  if (threadIdx.x == 0) *J.out_bits = (int)total;
-}
-
-// Every job's coded-bit count into one array (one readback per batch).
-__global__ __launch_bounds__(512) void k_enc_nbits(const TeJob *__restrict__ jobs, int n, int *__restrict__ out) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = *jobs[i].out_bits;
+  if (threadIdx.x == 0) {
+    *J.out_bits = (int)total;
+    const unsigned long long need = (unsigned long long)((nw + 3) & ~3LL);
+    const unsigned long long o = arena ? atomicAdd(arena_ctr, need) : ~0ull;
+    aoff = arena && o + need <= arena_words ? (long long)o : -1;
+  }
+  __threadfence();  // every thread's ORs are in before any thread reads the words back
+  __syncthreads();
+  if (aoff >= 0) {
+    const uint4 *src = (const uint4 *)J.out_words;
+    uint4 *dst = (uint4 *)(arena + aoff);
+    for (long long i = threadIdx.x; i < (nw + 3) >> 2; i += 256) {
+      const uint4 v = src[i];
+      dst[i] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z), __builtin_bswap32(v.w));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the host reads them)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    meta[2 * blockIdx.x] = (int)aoff;
+    if (blockIdx.x == 0) meta[2 * THOR_ENC_MAX_BATCH] = (int)*err;  // k_enc_rows' error flags (it ran before)
+    __hip_atomic_store(&meta[2 * blockIdx.x + 1], (int)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ============================================================================
@@ -554,18 +633,24 @@ struct EncPool {
   // counts (one readback), and pinned staging for the coded words (async
   // readbacks, one synchronisation)
   uint32_t *hdr_all = nullptr;
-  int *nb_all = nullptr;  // [2][THOR_ENC_MAX_BATCH]: the bit counts of up to two batches in flight
-  int *nb_host = nullptr;  // pinned, same shape
+  // per in-flight batch buffer (two): page-locked staging of the jobs and headers (truly
+  // asynchronous uploads), the host arena k_enc_pack writes the packed frames into and the
+  // (offset, bit count) meta words, and the arena's device allocation counter
+  TeJob *jobs_host[2] = {nullptr, nullptr};
+  uint32_t *hdr_host[2] = {nullptr, nullptr};
+  uint32_t *arena[2] = {nullptr, nullptr};
+  size_t arena_words[2] = {0, 0};
+  size_t arena_want[2] = {0, 0};
+  int *meta[2] = {nullptr, nullptr};
+  unsigned long long *arena_ctr = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
-  uint8_t *rb_host = nullptr;
-  size_t rb_cap = 0;
   // batches begun and not yet ended (thor_enc_frames_begin / _end), oldest first
   struct Pending {
     std::vector<thor_enc *> es;
     std::vector<int> cur;        // the slot each context coded into
     std::vector<uint32_t *> words;  // the output buffer each context packed into
     std::vector<int> frame_num;
-    int buf;                     // nb_all / nb_host / ev index
+    int buf;                     // jobs_host / hdr_host / arena / meta / ev index
     hipStream_t st;
     // each context's state before the batch (restored when the batch fails)
     struct Snap {
@@ -580,15 +665,6 @@ struct EncPool {
 };
 static std::mutex g_pools_mu;
 static std::map<int, EncPool *> g_pools;
-static std::map<int, hipStream_t> g_copy_streams;  // per device: thor_enc_frames_end's readbacks
-
-static hipStream_t copy_stream_for(int device) {
-  std::lock_guard<std::mutex> lk(g_pools_mu);
-  hipStream_t &s = g_copy_streams[device];
-  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
-  return s;
-}
-
 static EncPool &pool_for(int device) {
   std::lock_guard<std::mutex> lk(g_pools_mu);
   EncPool *&p = g_pools[device];
@@ -620,8 +696,12 @@ static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n, size_t nsb_tota
     EHIP(hipMemset(P.err, 0, 64));
     EHIP(hipMalloc(&P.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
     EHIP(hipMalloc(&P.hdr_all, THOR_ENC_MAX_BATCH * 64 * sizeof(uint32_t)));
-    EHIP(hipMalloc(&P.nb_all, 2 * THOR_ENC_MAX_BATCH * sizeof(int)));
-    EHIP(hipHostMalloc((void **)&P.nb_host, 2 * THOR_ENC_MAX_BATCH * sizeof(int), hipHostMallocDefault));
+    EHIP(hipMalloc(&P.arena_ctr, 2 * sizeof(unsigned long long)));
+    for (int b = 0; b < 2; b++) {
+      EHIP(hipHostMalloc((void **)&P.jobs_host[b], THOR_ENC_MAX_BATCH * sizeof(TeJob), hipHostMallocDefault));
+      EHIP(hipHostMalloc((void **)&P.hdr_host[b], THOR_ENC_MAX_BATCH * 64 * sizeof(uint32_t), hipHostMallocDefault));
+      EHIP(hipHostMalloc((void **)&P.meta[b], (THOR_ENC_MAX_BATCH * 2 + 2) * sizeof(int), hipHostMallocCoherent | hipHostMallocMapped));
+    }
     for (int i = 0; i < 2; i++) EHIP(hipEventCreateWithFlags(&P.ev[i], hipEventDisableTiming));
   }
   if (nwork > P.nwork) {
@@ -850,6 +930,7 @@ static int enc_prepare(thor_enc *e, const uint8_t *orig, int orig_stride, TeJob 
   J.nsbh = e->nsbh;
   J.nsbv = e->nsbv;
   J.clpf = P.clpf;
+  J.deblock = P.deblocking;
   J.sb_costs = e->sb_costs;
   J.cost_stride = e->cost_stride;
   // header bits (sequence header before the first frame)
@@ -945,18 +1026,22 @@ static int frames_begin_locked(EncPool &P, thor_enc_t *const *es, int n, const u
   std::vector<TeJob> jobs(n);
   std::vector<TeFramePlan> plans(n);
   std::vector<int> cur(n);
-  std::vector<uint32_t> hdr((size_t)n * 64);
+  // the buffer set no pending batch holds (at most one is pending here)
+  int buf = 0;
+  for (const EncPool::Pending &q : P.pending)
+    if (q.buf == 0) buf = 1;
+  uint32_t *hdr = P.hdr_host[buf];
   for (int i = 0; i < n; i++) {
     thor_enc *e = es[i];
     if (e->stream != st) {  // the members' earlier work on their own streams comes first
       EHIP(hipStreamSynchronize(e->stream));
     }
     const int s = orig_stride ? orig_stride[i] : W;
-    if ((rc = enc_prepare(e, orig[i], s, jobs[i], plans[i], cur[i], st, &hdr[(size_t)i * 64], P.hdr_all + i * 64)) !=
+    if ((rc = enc_prepare(e, orig[i], s, jobs[i], plans[i], cur[i], st, hdr + (size_t)i * 64, P.hdr_all + i * 64)) !=
         THOR_OK)
       return rc;
   }
-  EHIP(hipMemcpyAsync(P.hdr_all, hdr.data(), hdr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  EHIP(hipMemcpyAsync(P.hdr_all, hdr, (size_t)n * 64 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   // interpolated references: each context's on its own stream (they overlap), all done before the RD loop;
   // each after every pending batch (their loop filters still write the slots the interpolation reads,
   // their RD loops may still read the interpolation slot it overwrites)
@@ -975,13 +1060,26 @@ static int frames_begin_locked(EncPool &P, thor_enc_t *const *es, int n, const u
         if ((rc = thor_ti_status(es[i]->ti)) != THOR_OK) return rc;
       }
   for (int i = 0; i < n; i++) jobs[i].qbase = n + i * (lead->nsb - 1);  // slots [n, n * nsb): empty
-  EHIP(hipMemcpyAsync(P.jobs, jobs.data(), n * sizeof(TeJob), hipMemcpyHostToDevice, st));
+  memcpy(P.jobs_host[buf], jobs.data(), n * sizeof(TeJob));
+  EHIP(hipMemcpyAsync(P.jobs, P.jobs_host[buf], n * sizeof(TeJob), hipMemcpyHostToDevice, st));
+  {  // the host arena: room for every frame of the batch at W*H/16 bytes (grown after an overflow)
+    size_t want = (size_t)n * (((size_t)W * H / 16) / 4 + 1024);
+    if (P.arena_want[buf] > want) want = P.arena_want[buf];
+    if (want > P.arena_words[buf]) {
+      if (P.arena[buf]) (void)hipHostFree(P.arena[buf]);
+      P.arena[buf] = nullptr;
+      P.arena_words[buf] = 0;
+      EHIP(hipHostMalloc((void **)&P.arena[buf], want * 4 + 64, hipHostMallocCoherent | hipHostMallocMapped));
+      P.arena_words[buf] = want;
+    }
+  }
   {
     const long long cb = (long long)(W / 4) * (H / 4) * (long long)sizeof(TeCell);
     static_assert(sizeof(TeCell) % 4 == 0, "cells clear as words");
     const long long n16 = (cb + 15) / 16;
     const int gx = (int)((n16 + 255) / 256 < 1024 ? (n16 + 255) / 256 : 1024);
-    k_enc_clear<<<dim3(gx > 0 ? gx : 1, n), 256, 0, st>>>(P.jobs, ((cb + 15) / 16) * 16, P.ticket, P.qitems);
+    k_enc_clear<<<dim3(gx > 0 ? gx : 1, n), 256, 0, st>>>(P.jobs, ((cb + 15) / 16) * 16, P.ticket, P.qitems,
+                                                        P.arena_ctr + buf);
     EHIP(hipGetLastError());
   }
   // persistent workers take SBs from the queue until every slot is taken:
@@ -990,60 +1088,24 @@ static int frames_begin_locked(EncPool &P, thor_enc_t *const *es, int n, const u
   k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(
       P.jobs, (unsigned)(n * lead->nsb), P.ticket, P.qitems, P.scratch, P.err, g_spin_limit.load(), g_stall_row.load());
   EHIP(hipGetLastError());
-  const int ncell = (W / 4) * (H / 4);
-  k_enc_cellinfo<<<dim3((ncell + 255) / 256, n), 256, 0, st>>>(P.jobs);
-  EHIP(hipGetLastError());
-  // loop filters: the decoder's kernels over each stream's frame
-  for (int o = 0; o < n; o += THOR_MAX_BATCH) {
-    const int m = n - o < THOR_MAX_BATCH ? n - o : THOR_MAX_BATCH;
-    FrameBatch fb;
-    memset(&fb, 0, sizeof(fb));
-    for (int i = 0; i < m; i++) {
-      thor_enc *e = es[o + i];
-      FrameCtx &f = fb.f[i];
-      uint8_t *c = e->slots + (long long)cur[o + i] * e->slot_bytes;
-      f.cy = c + e->offy;
-      f.cu = c + e->offu;
-      f.cv = c + e->offv;
-      f.sy = e->sy;
-      f.sc = e->sc;
-      f.W = W;
-      f.H = H;
-      f.cellinfo = e->cellinfo;
-      f.qp = plans[o + i].qp;
-      f.qpc = chroma_qp_host(plans[o + i].qp);
-      f.deblock = e->p.deblocking;
-      f.clpf_on = e->p.clpf;
-      f.clpf_flags = e->clpf_flags;
-      f.n_clpf = -1;
-      f.frame_num = plans[o + i].frame_num;
-    }
-    if (lead->p.deblocking) {
-      const int nv = ((W >> 3) - 1) * (H >> 3), nh = (W >> 3) * ((H >> 3) - 1);
-      const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
-      k_deblock_v<<<dim3(3 * bv, m), 256, 0, st>>>(fb, bv, 0);
-      k_deblock_h<<<dim3(3 * bh, m), 256, 0, st>>>(fb, bh, 0);
-      EHIP(hipGetLastError());
-    }
-    if (lead->p.clpf && lead->nsb_full > 0) {
-      k_enc_clpf<<<dim3(lead->nsb_full, m), 64, 0, st>>>(P.jobs + o);
-      k_clpf<<<dim3(lead->nsb_full, m), 256, 0, st>>>(fb);
-      EHIP(hipGetLastError());
-    }
-    k_pad<<<dim3((pad_chunks(W, H) + 255) / 256, m), 256, 0, st>>>(fb, 0, 0);
+  // loop filters of every job, one launch per pass (the cell words came from k_enc_rows itself)
+  {
+    const int nv = ((W >> 3) - 1) * (H >> 3), nh = (W >> 3) * ((H >> 3) - 1);
+    const int bv = (nv + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS), bh = (nh + 256 * DB_ITEMS - 1) / (256 * DB_ITEMS);
+    k_enc_db_v<<<dim3(3 * bv, n), 256, 0, st>>>(P.jobs, bv);
+    k_enc_db_h<<<dim3(3 * bh, n), 256, 0, st>>>(P.jobs, bh);
     EHIP(hipGetLastError());
   }
-  k_enc_pack<<<n, 256, 0, st>>>(P.jobs, P.scan, lead->out_cap_words);
+  if (lead->nsb_full > 0) {
+    k_enc_clpf<<<dim3(lead->nsb_full, n), 64, 0, st>>>(P.jobs);
+    EHIP(hipGetLastError());
+  }
+  k_enc_pad<<<dim3((pad_chunks(W, H) + 255) / 256, n), 256, 0, st>>>(P.jobs);
   EHIP(hipGetLastError());
-  // the bit counts in one copy into pinned memory, an event behind it: in the
-  // buffer no pending batch holds (at most one is pending here)
-  int buf = 0;
-  for (const EncPool::Pending &q : P.pending)
-    if (q.buf == 0) buf = 1;
-  int *nb_dev = P.nb_all + buf * THOR_ENC_MAX_BATCH, *nb_host = P.nb_host + buf * THOR_ENC_MAX_BATCH;
-  k_enc_nbits<<<1, 512, 0, st>>>(P.jobs, n, nb_dev);
+  // the packed frames straight into the host arena, their sizes into the meta words; an event behind
+  k_enc_pack<<<n, 256, 0, st>>>(P.jobs, P.scan, lead->out_cap_words, P.arena[buf], P.arena_words[buf],
+                                P.arena_ctr + buf, P.meta[buf], P.err);
   EHIP(hipGetLastError());
-  EHIP(hipMemcpyAsync(nb_host, nb_dev, n * sizeof(int), hipMemcpyDeviceToHost, st));
   EHIP(hipEventRecord(P.ev[buf], st));
   // the batch is in flight: advance every context (the next plan, the reference window)
   EncPool::Pending q;
@@ -1096,11 +1158,11 @@ static int frames_end_locked(EncPool &P, thor_enc_t *const *es, int n) {
   P.pending.erase(P.pending.begin() + qi);
   hipStream_t st = q.st;
   EHIP(hipEventSynchronize(P.ev[q.buf]));
-  const int *nbits = P.nb_host + q.buf * THOR_ENC_MAX_BATCH;
-  unsigned err = 0;
-  EHIP(hipMemcpy(&err, P.err, sizeof(unsigned), hipMemcpyDeviceToHost));
+  // k_enc_pack left (arena offset, bit count) per context and the error flags in page-locked memory
+  const volatile int *meta = P.meta[q.buf];
+  const unsigned err = (unsigned)meta[2 * THOR_ENC_MAX_BATCH];
   bool bad = err != 0;
-  for (int i = 0; i < n && !bad; i++) bad = nbits[i] < 0;
+  for (int i = 0; i < n && !bad; i++) bad = meta[2 * i + 1] < 0;
   if (bad) {  // drop what is in flight, restore the contexts to before this batch (and the other pending ones)
     EHIP(hipStreamSynchronize(st));
     for (const EncPool::Pending &r : P.pending) EHIP(hipStreamSynchronize(r.st));
@@ -1117,31 +1179,25 @@ static int frames_end_locked(EncPool &P, thor_enc_t *const *es, int n) {
     }
     return THOR_ERR_NOMEM;  // a frame over the output buffer
   }
-  std::vector<size_t> woff(n + 1, 0);
-  for (int i = 0; i < n; i++) woff[i + 1] = woff[i] + ((((size_t)nbits[i] + 7) / 8 + 3) / 4) * 4;
-  if (woff[n] > P.rb_cap) {
-    if (P.rb_host) (void)hipHostFree(P.rb_host);
-    P.rb_host = nullptr;
-    P.rb_cap = 0;
-    EHIP(hipHostMalloc((void **)&P.rb_host, woff[n] * 2 + 4096, hipHostMallocDefault));
-    P.rb_cap = woff[n] * 2 + 4096;
-  }
-  // on a stream of their own: the batch's stream may already run the next batch
-  hipStream_t cs = copy_stream_for(es[0]->device);
-  for (int i = 0; i < n; i++)
-    if (woff[i + 1] > woff[i])
-      EHIP(hipMemcpyAsync(P.rb_host + woff[i], q.words[i], woff[i + 1] - woff[i], hipMemcpyDeviceToHost, cs));
-  EHIP(hipStreamSynchronize(cs));
+  const uint8_t *arena = (const uint8_t *)P.arena[q.buf];
+  std::vector<uint32_t> tmp;
   for (int i = 0; i < n; i++) {
     thor_enc *e = q.es[i];
-    const size_t nb = ((size_t)nbits[i] + 7) / 8;
-    const uint32_t *w = (const uint32_t *)(P.rb_host + woff[i]);
+    const int off = meta[2 * i];
+    const size_t nb = ((size_t)meta[2 * i + 1] + 7) / 8;
     e->chunk.resize(4 + nb);
     e->chunk[0] = (uint8_t)(nb >> 24);
     e->chunk[1] = (uint8_t)(nb >> 16);
     e->chunk[2] = (uint8_t)(nb >> 8);
     e->chunk[3] = (uint8_t)nb;
-    for (size_t b = 0; b < nb; b++) e->chunk[4 + b] = (uint8_t)(w[b >> 2] >> (24 - 8 * (b & 3)));
+    if (off >= 0) {  // the stream's bytes, already in order
+      memcpy(e->chunk.data() + 4, arena + (size_t)off * 4, nb);
+    } else {  // the arena was full: this frame's words from device memory; a larger arena next time
+      tmp.resize((nb + 3) / 4);
+      EHIP(hipMemcpy(tmp.data(), q.words[i], tmp.size() * 4, hipMemcpyDeviceToHost));
+      for (size_t b = 0; b < nb; b++) e->chunk[4 + b] = (uint8_t)(tmp[b >> 2] >> (24 - 8 * (b & 3)));
+      P.arena_want[q.buf] = 2 * P.arena_words[q.buf];
+    }
   }
   return THOR_OK;
 }

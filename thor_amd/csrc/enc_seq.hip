@@ -135,18 +135,6 @@ __device__ __forceinline__ unsigned ts_pop(const TsArgs &A, unsigned long long &
   return TE_Q_EMPTY;
 }
 
-// the 16-bit loop-filter word of a cell (k_enc_cellinfo's packing)
-__device__ __forceinline__ uint16_t ts_cellinfo(const TeCell &c) {
-  const int size = c.size < 8 ? 8 : c.size;
-  const int lsz = size >= 64 ? 6 : (size >= 32 ? 5 : (size >= 16 ? 4 : 3));
-  const int tb = c.tb_split > 0, pb = c.pb_part;
-  const int lqv = lsz - (((tb || pb == 2 || pb == 3) && size > 8) ? 1 : 0);
-  const int lqh = lsz - (((tb || pb == 1 || pb == 3) && size > 8) ? 1 : 0);
-  const int big = (abs(c.ip.mv0.x) >= 4) | (abs(c.ip.mv0.y) >= 4) | (abs(c.ip.mv1.x) >= 4) | (abs(c.ip.mv1.y) >= 4);
-  return (uint16_t)((c.mode & 7) | ((c.cbp_y != 0) << 3) | ((c.cbp_u != 0) << 4) | ((c.cbp_v != 0) << 5) | (big << 6) |
-                    (lqv << 8) | (lqh << 11) | ((lsz - 3) << 14));
-}
-
 // FETCH: bytes [a, b) of the I420 frame, host -> HBM, 16 bytes per lane access,
 // eight in flight (the host reads cross PCIe: latency bound per wave).
 __device__ void ts_copy_range(uint8_t *dst, const uint8_t *src, long long a, long long b) {
@@ -402,7 +390,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
     const int j = (int)(item >> 20), type = (int)((item >> 17) & 7), idx = (int)(item & (TS_MAX_SB - 1));
     const TsJob &T = A.jobs[j];
     const TeJob &J = T.J;
-    const int W = J.F.W, H = J.F.H, nsbh = J.nsbh, nsbv = J.nsbv;
+    const int nsbh = J.nsbh, nsbv = J.nsbv;
     if (type == TS_RD && j != cur) {  // the job's frame parameters into LDS
       const uint32_t *src = (const uint32_t *)&J.F;
       uint32_t *dst = (uint32_t *)&s_F;
@@ -426,11 +414,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_seq(const TsArgs A) {
         if (sb.bits.pos > sb.bits.cap) atomicOr(A.err, 2u);
       }
       te_sync();  // the SB's cells (written by every lane) before their loop-filter words
-      const int cs = W >> 2, r0 = k * 16, c0 = l * 16;
-      for (int e = lane; e < 256; e += 64) {
-        const int r = r0 + (e >> 4), c = c0 + (e & 15);
-        if (r < (H >> 2) && c < cs) J.cellinfo[r * cs + c] = ts_cellinfo(J.F.cells[r * cs + c]);
-      }
+      te_sb_cellinfo(J, k, l);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) {  // dependants (enc.hip's rule), and the row's vertical deblocking
