@@ -1148,9 +1148,14 @@ def main():
     path_ms = prep_ms + recon_ms
     path_achieved = alg / (path_ms / 1e3) / 1e9 if path_ms > 0 else 0.0
     traffic = None
+    traffic_source = None
     tj = a.traffic_json or os.path.join(ROOT, "tools", "traffic_latest.json")
     if os.path.exists(tj):
-        traffic = json.load(open(tj)).get("recon_hbm_bytes_per_p_launch")
+        tjd = json.load(open(tj))
+        traffic = tjd.get("recon_hbm_bytes_per_p_launch")
+        # the PMC passes this static figure came from: their profile tag and the commit of the kernels measured
+        traffic_source = {"file": os.path.relpath(tj, ROOT), "profile_tag": tjd.get("tag"),
+                          "kernels_commit": tjd.get("commit"), "profile": tjd.get("profile")}
 
     out = None
     if rank == 0:
@@ -1216,6 +1221,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "alg_bytes_per_launch": round(alg),
                 "avg_launch_us": round(recon_ms * 1e3, 2),
                 **({"avg_launch_us_before_steps": round(rf_early * 1e3, 2)} if rf_early is not None else {}),

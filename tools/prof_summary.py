@@ -81,7 +81,11 @@ def main():
     if not os.path.exists(os.path.join(d, "fetch", "run_results.db")):
         print("no PMC passes under", d)
         return
-    traffic = {"tag": tag, "correction": "fetch_bytes = FETCH_SIZE_KiB*1024*2 (gfx950 half-count); "
+    import subprocess
+
+    commit = subprocess.run(["git", "-C", os.path.dirname(os.path.abspath(__file__)), "rev-parse", "--short=12", "HEAD"],
+                            capture_output=True, text=True).stdout.strip() or None
+    traffic = {"tag": tag, "commit": commit, "profile": "profiles/%s_traffic.json" % tag, "correction": "fetch_bytes = FETCH_SIZE_KiB*1024*2 (gfx950 half-count); "
                                          "write_bytes = WRITE_SIZE_KiB*1024", "kernels": {}}
     f, nf = pmc(os.path.join(d, "fetch", "run_results.db"), "FETCH_SIZE")
     w, nw = pmc(os.path.join(d, "write", "run_results.db"), "WRITE_SIZE")
