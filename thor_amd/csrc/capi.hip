@@ -458,7 +458,7 @@ static int batch_prepare(thor_dec_t *const *ds, int n, const thor_frame_hdr_t *h
     f.nblocks = in.nblocks;
     f.ntus = in.n_tu;
     f.nintra = in.n_intra;
-    f.nprep = (in.nblocks + 3) / 4;
+    f.nprep = (in.nblocks + 4 * PREP_CPW - 1) / (4 * PREP_CPW);  // workgroups of 4 waves x PREP_CPW CUs (prep_body)
     f.nres = (in.n_tu + 3) / 4;
     f.full_sb = in.n_intra < in.nblocks;  // full SB images only when inter CUs were reconstructed
     f.qp = hdrs[i].qp;

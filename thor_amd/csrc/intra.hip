@@ -629,8 +629,8 @@ __device__ __forceinline__ void intra_setup_body(const thor_block_t *__restrict_
 }
 
 // k_frame_prep: everything a frame needs before reconstruction, in one launch
-// of 256-lane workgroups: [0, nprep) the per-4x4 side info (prep_body, four
-// CUs per workgroup), [nprep, nprep + nres) the residuals of the coded
+// of 256-lane workgroups: [0, nprep) the per-4x4 side info (prep_body,
+// 4 x PREP_CPW CUs per workgroup), [nprep, nprep + nres) the residuals of the coded
 // transform blocks (resid_tu, four per workgroup), and one last workgroup that
 // sets up the intra chains (row segments of the intra list, progress words).
 // All three only read the frame's parse output.

@@ -22,9 +22,16 @@ __device__ __forceinline__ void slow_mark(const FrameCtx &f, int sbx, int sby, i
   f.hplan[2 * (sby * sbw + sbx) + h] = make_uint4(0u, PLAN_SLOW, 0u, (unsigned)f.gen);
 }
 
+// PREP_CPW CUs per wave, 64 / PREP_CPW lanes each (round 6: 4 -- a 4K P frame is ~2 000 64x64 SKIP CUs
+// whose waves spent their short lives waiting on one descriptor load; a quarter as many waves, the four
+// descriptor loads of a wave in flight together)
+#ifndef PREP_CPW
+#define PREP_CPW 4
+#endif
+#define PREP_LPC (64 / PREP_CPW)
 __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
-  const int b = bx * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  const int b = (bx * 4 + (threadIdx.x >> 6)) * PREP_CPW + ((threadIdx.x & 63) / PREP_LPC);
+  const int lane = threadIdx.x & (PREP_LPC - 1);  // lane within the CU's group
   if (b >= f.nblocks) return;
   const int cstride = f.W >> 2;
   const thor_block_t &B = f.blk[b];
@@ -82,7 +89,7 @@ __device__ __forceinline__ void prep_body(int bx, const FrameCtx &f) {
   }
   int div = S >> 3;
   int y4 = B.ypos >> 2, x4 = B.xpos >> 2;
-  for (int c = lane; c < bw * bh; c += 64) {
+  for (int c = lane; c < bw * bh; c += PREP_LPC) {
     int m = c / bw, n = c - m * bw;
     int q = 2 * (m / div) + (n / div);
     int a0 = B.mv0[2 * q], a1 = B.mv0[2 * q + 1], a2 = B.mv1[2 * q], a3 = B.mv1[2 * q + 1];
