@@ -6,7 +6,7 @@ cd /root/repo
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-legs"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-legs --no-rows"
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- $B > $OUT/trace_bench.json 2> $OUT/trace.err || { echo TRACE_FAIL; tail -20 $OUT/trace.err; exit 1; }
 # PMC passes on the decoder alone (the encoder's persistent workers run for minutes with counters on):
 # one 4K LDB-low frame per launch, frames in decode order I P P P P P P P
