@@ -87,6 +87,19 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 #endif
 #define TE_WPE __attribute__((amdgpu_waves_per_eu(THOR_ENC_WPE)))
 #define TE_Q_EMPTY 0xffffffffu
+// Priority levels of the SB queue (TE_QLEVELS > 1, an experiment): an SB of row k goes to level
+// k * TE_QLEVELS / nsbv, a worker takes the oldest ready SB of the lowest non-empty level -- the upper
+// rows of every stream gate its whole frame, so the streams that are behind get the workers first.
+// Level v's head / tail at q[64 v] / q[64 v + 32] (separate 128-byte lines), its items at off[v].
+#ifndef TE_QLEVELS
+#define TE_QLEVELS 1
+#endif
+struct TeQLevels {
+  unsigned off[8], cap[8];
+};
+#define TE_QHEAD(v) ((v)*64)
+#define TE_QTAIL(v) ((v)*64 + 32)
+#define TE_QDONE (8 * 64)
 // A queue item: job s (< THOR_ENC_MAX_BATCH = 512: 9 bits), SB row k and column l
 // (11 bits each: frames up to 65 535 px, te_check_params' limit, have <= 1 024
 // SB rows / columns).  The top bit stays clear, so no item equals TE_Q_EMPTY.
@@ -96,12 +109,20 @@ __device__ __forceinline__ unsigned te_q_item(int s, int k, int l) { return (uns
 // results back to device scope (every dependency's did, before its count), and
 // the worker that takes the SB acquires once -- an acquire / release per
 // atomic here would write back and invalidate the XCD's L2 several times per SB.
-__device__ __forceinline__ void te_dep_done(const TeJob &J, int s, int k, int l, unsigned *q, unsigned *items) {
+__device__ __forceinline__ void te_dep_done(const TeJob &J, int s, int k, int l, unsigned *q, unsigned *items,
+                                            const TeQLevels &QL) {
   const unsigned need = (unsigned)((l > 0) + (k > 0));
   const unsigned old = __hip_atomic_fetch_add(&J.deps[k * J.nsbh + l], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old + 1 == need) {
+#if TE_QLEVELS > 1
+    const int v = k * TE_QLEVELS / J.nsbv;
+    const unsigned slot = __hip_atomic_fetch_add(&q[TE_QTAIL(v)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&items[QL.off[v] + slot], te_q_item(s, k, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    (void)QL;
     const unsigned slot = __hip_atomic_fetch_add(&q[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&items[slot], te_q_item(s, k, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   }
 }
 // the 16-bit loop-filter word of a cell (the decoder's packing, prep_body in recon.hip)
@@ -129,7 +150,7 @@ __device__ __forceinline__ void te_sb_cellinfo(const TeJob &J, int k, int l) {
 __device__ unsigned long long g_te_rows_prof[4];
 __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict__ jobs, unsigned total, unsigned *q,
                                                  unsigned *items, TeScratchMem *scratch, unsigned *err,
-                                                 unsigned long long spin_limit, int stall_row) {
+                                                 unsigned long long spin_limit, int stall_row, const TeQLevels QL) {
   __shared__ TeFrame s_F;  // the job's frame parameters, read all through the RD loop
   __shared__ TeSB s_sb;    // the superblock's bit writer and ME candidate lists
   // the worker's buffers (te_here): LDS at fixed addresses (g_te_*), global at
@@ -144,13 +165,61 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   for (;;) {
     unsigned h = 0;
     const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+#if TE_QLEVELS > 1
+    // the lowest level with a ready SB: a ticket there when it looks non-empty (a ticket past its
+    // items so far waits for its slot: every slot below the level's SB count fills); every level's
+    // tickets all handed out: leave; nothing ready anywhere for spin_limit with no SB finished: give up
+    unsigned item = 0, gave_up = 0;
+    int quit = 0;
+    if (lane == 0) {
+      unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned seen = te_ld_relaxed(&q[TE_QDONE]);
+      for (;;) {
+        bool all = true, got = false;
+        for (int v = 0; v < TE_QLEVELS && !got; v++) {
+          unsigned hv = te_ld_relaxed(&q[TE_QHEAD(v)]);
+          if (hv >= QL.cap[v]) continue;
+          all = false;
+          if (hv >= te_ld_relaxed(&q[TE_QTAIL(v)])) continue;
+          hv = __hip_atomic_fetch_add(&q[TE_QHEAD(v)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (hv >= QL.cap[v]) continue;
+          const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+          while ((item = te_ld_relaxed(&items[QL.off[v] + hv])) == TE_Q_EMPTY) {
+            __builtin_amdgcn_s_sleep(4);
+            if (__builtin_amdgcn_s_memrealtime() - t1 > spin_limit) {
+              atomicOr(err, 1u);
+              gave_up = 1;
+              break;
+            }
+          }
+          got = true;
+        }
+        if (got || all) {
+          quit = !got;
+          break;
+        }
+        const unsigned d = te_ld_relaxed(&q[TE_QDONE]);
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if (d != seen) seen = d, t0 = now;
+        if (now - t0 > spin_limit || te_ld_relaxed(err)) {
+          atomicOr(err, 1u);
+          gave_up = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane(quit)) break;
+    {
+#else
     if (lane == 0) h = __hip_atomic_fetch_add(&q[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h = __builtin_amdgcn_readfirstlane(h);
     if (h >= total) break;
     unsigned item = 0, gave_up = 0;
     {
+#endif
       TE_P(TP_WAIT);
-      if (lane == 0) {
+      if (TE_QLEVELS == 1 && lane == 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
         while ((item = te_ld_relaxed(&items[h])) == TE_Q_EMPTY) {
           __builtin_amdgcn_s_sleep(4);
@@ -195,11 +264,12 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
       // dependants: (k, l + 1) by its left neighbour; (k + 1, l - 1) by its up-right one, and
       // (k + 1, l) too at the row end (its up-right is clipped to this SB).  stall_row: a
       // diagnostics hook (thor_enc_debug_stall) -- that row never releases the row below
-      if (l + 1 < J.nsbh) te_dep_done(J, s, k, l + 1, q, items);
+      if (l + 1 < J.nsbh) te_dep_done(J, s, k, l + 1, q, items, QL);
       if (k + 1 < J.nsbv && k != stall_row) {
-        if (l >= 1) te_dep_done(J, s, k + 1, l - 1, q, items);
-        if (l == J.nsbh - 1) te_dep_done(J, s, k + 1, l, q, items);
+        if (l >= 1) te_dep_done(J, s, k + 1, l - 1, q, items, QL);
+        if (l == J.nsbh - 1) te_dep_done(J, s, k + 1, l, q, items, QL);
       }
+      if (TE_QLEVELS > 1) __hip_atomic_fetch_add(&q[TE_QDONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       t_work += __builtin_amdgcn_s_memrealtime() - tb0;
       n_sb++;
     }
@@ -232,8 +302,14 @@ __global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ job
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     items[s] = te_q_item(s, 0, 0);
     if (s == 0) {
+#if TE_QLEVELS > 1
+      for (int v = 0; v < TE_QLEVELS; v++) q[TE_QHEAD(v)] = q[TE_QTAIL(v)] = 0u;
+      q[TE_QTAIL(0)] = gridDim.y;  // every job's SB (0, 0): level 0's slots [0, n)
+      q[TE_QDONE] = 0u;
+#else
       q[0] = 0u;
       q[1] = gridDim.y;
+#endif
       *arena_ctr = 0ull;  // this batch's packed frames start at the host arena's first word
     }
   }
@@ -691,7 +767,7 @@ static void pending_restore(const EncPool::Pending &q, const thor_enc *skip) {
 // (the caller holds P.mu and has made P's device current)
 static int pool_reserve(EncPool &P, size_t nwork, size_t scan_n, size_t nsb_total) {
   if (!P.ticket) {
-    EHIP(hipMalloc(&P.ticket, 64));
+    EHIP(hipMalloc(&P.ticket, 4096));  // queue heads / tails (TE_QLEVELS: one 128-byte line each)
     EHIP(hipMalloc(&P.err, 64));
     EHIP(hipMemset(P.err, 0, 64));
     EHIP(hipMalloc(&P.jobs, THOR_ENC_MAX_BATCH * sizeof(TeJob)));
@@ -1082,11 +1158,25 @@ static int frames_begin_locked(EncPool &P, thor_enc_t *const *es, int n, const u
                                                         P.arena_ctr + buf);
     EHIP(hipGetLastError());
   }
+  // the queue's priority levels (TE_QLEVELS > 1): level v holds the SBs of rows k with k * L / nsbv == v,
+  // its slots after the lower levels'; level 0 starts with every job's SB (0, 0)
+  TeQLevels QL;
+  memset(&QL, 0, sizeof(QL));
+  {
+    unsigned o = 0;
+    for (int v = 0; v < TE_QLEVELS; v++) {
+      int rows = 0;
+      for (int k = 0; k < lead->nsbv; k++) rows += k * TE_QLEVELS / lead->nsbv == v;
+      QL.off[v] = o;
+      QL.cap[v] = (unsigned)(n * rows * lead->nsbh);
+      o += QL.cap[v];
+    }
+  }
   // persistent workers take SBs from the queue until every slot is taken:
   // more workgroups than the chip holds at once (two per SIMD at this kernel's
   // register and LDS use) would only start as the first ones run out of work
   k_enc_rows<<<nwork < TE_MAX_WORKERS ? nwork : TE_MAX_WORKERS, 64, 0, st>>>(
-      P.jobs, (unsigned)(n * lead->nsb), P.ticket, P.qitems, P.scratch, P.err, g_spin_limit.load(), g_stall_row.load());
+      P.jobs, (unsigned)(n * lead->nsb), P.ticket, P.qitems, P.scratch, P.err, g_spin_limit.load(), g_stall_row.load(), QL);
   EHIP(hipGetLastError());
   // loop filters of every job, one launch per pass (the cell words came from k_enc_rows itself)
   {
