@@ -90,6 +90,9 @@ __device__ __forceinline__ unsigned te_ld_relaxed(const unsigned *p) {
 // Priority levels of the SB queue (TE_QLEVELS > 1, an experiment): an SB of row k goes to level
 // k * TE_QLEVELS / nsbv, a worker takes the oldest ready SB of the lowest non-empty level -- the upper
 // rows of every stream gate its whole frame, so the streams that are behind get the workers first.
+// Measured SLOWER (240 x 4K x 8 frames, 4 levels: 1.73-1.76 s vs 1.54-1.57 s; the P-frame SBs cost
+// 24 % more summed RD time -- leaving readiness order costs the neighbouring SBs' shared L2 lines,
+// profiles/r07/queue_levels_*.txt), so the product keeps one FIFO.
 // Level v's head / tail at q[64 v] / q[64 v + 32] (separate 128-byte lines), its items at off[v].
 #ifndef TE_QLEVELS
 #define TE_QLEVELS 1
