@@ -103,6 +103,15 @@ struct TeQLevels {
 #define TE_QHEAD(v) ((v)*64)
 #define TE_QTAIL(v) ((v)*64 + 32)
 #define TE_QDONE (8 * 64)
+// Continuation (TE_CONT, single queue): the worker that makes its right neighbour (k, l + 1) ready
+// codes it next itself instead of queueing it -- the row's chain skips a queue round trip and the SB
+// runs where its left neighbour's data and the overlapping search window are warm.  The queue then
+// fills fewer slots than there are SBs: q[TE_QTOTAL] counts the slots that will fill (decremented per
+// kept SB); a ticket at or past it will never fill and its worker leaves.
+#ifndef TE_CONT
+#define TE_CONT 0
+#endif
+#define TE_QTOTAL (8 * 64 + 32)
 // A queue item: job s (< THOR_ENC_MAX_BATCH = 512: 9 bits), SB row k and column l
 // (11 bits each: frames up to 65 535 px, te_check_params' limit, have <= 1 024
 // SB rows / columns).  The top bit stays clear, so no item equals TE_Q_EMPTY.
@@ -165,6 +174,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   const int lane = threadIdx.x;
   int cur = -1;  // the job whose frame parameters s_F holds
   unsigned long long t_work = 0, t_wait = 0, n_sb = 0;  // (lane 0) this worker's profile
+  unsigned keep = TE_Q_EMPTY;  // (lane 0, TE_CONT) the SB this worker codes next, without the queue
   for (;;) {
     unsigned h = 0;
     const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
@@ -214,6 +224,36 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     }
     if (__builtin_amdgcn_readfirstlane(quit)) break;
     {
+#elif TE_CONT
+    unsigned item = 0, gave_up = 0;
+    int quit = 0;
+    if (lane == 0) {
+      if (keep != TE_Q_EMPTY) {
+        item = keep;
+        keep = TE_Q_EMPTY;
+      } else {
+        h = __hip_atomic_fetch_add(&q[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (h >= te_ld_relaxed(&q[TE_QTOTAL])) {
+          quit = 1;
+        } else {
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+          while ((item = te_ld_relaxed(&items[h])) == TE_Q_EMPTY) {
+            __builtin_amdgcn_s_sleep(4);
+            if (h >= te_ld_relaxed(&q[TE_QTOTAL])) {  // kept SBs left this slot unfilled for good
+              quit = 1;
+              break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > spin_limit) {
+              atomicOr(err, 1u);
+              gave_up = 1;
+              break;
+            }
+          }
+        }
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane(quit)) break;
+    {
 #else
     if (lane == 0) h = __hip_atomic_fetch_add(&q[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h = __builtin_amdgcn_readfirstlane(h);
@@ -222,7 +262,7 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
     {
 #endif
       TE_P(TP_WAIT);
-      if (TE_QLEVELS == 1 && lane == 0) {
+      if (TE_QLEVELS == 1 && !TE_CONT && lane == 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
         while ((item = te_ld_relaxed(&items[h])) == TE_Q_EMPTY) {
           __builtin_amdgcn_s_sleep(4);
@@ -267,7 +307,18 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
       // dependants: (k, l + 1) by its left neighbour; (k + 1, l - 1) by its up-right one, and
       // (k + 1, l) too at the row end (its up-right is clipped to this SB).  stall_row: a
       // diagnostics hook (thor_enc_debug_stall) -- that row never releases the row below
+#if TE_CONT && TE_QLEVELS == 1
+      if (l + 1 < J.nsbh) {  // the right neighbour: kept when this completes it
+        const unsigned need = 1u + (k > 0);
+        const unsigned old = __hip_atomic_fetch_add(&J.deps[sbi + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == need) {
+          keep = te_q_item(s, k, l + 1);
+          __hip_atomic_fetch_sub(&q[TE_QTOTAL], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#else
       if (l + 1 < J.nsbh) te_dep_done(J, s, k, l + 1, q, items, QL);
+#endif
       if (k + 1 < J.nsbv && k != stall_row) {
         if (l >= 1) te_dep_done(J, s, k + 1, l - 1, q, items, QL);
         if (l == J.nsbh - 1) te_dep_done(J, s, k + 1, l, q, items, QL);
@@ -312,6 +363,7 @@ __global__ __launch_bounds__(256) void k_enc_clear(const TeJob *__restrict__ job
 #else
       q[0] = 0u;
       q[1] = gridDim.y;
+      q[TE_QTOTAL] = (unsigned)gridDim.y * (unsigned)nsb;  // (TE_CONT) slots that will fill
 #endif
       *arena_ctr = 0ull;  // this batch's packed frames start at the host arena's first word
     }
