@@ -107,7 +107,9 @@ struct TeQLevels {
 // codes it next itself instead of queueing it -- the row's chain skips a queue round trip and the SB
 // runs where its left neighbour's data and the overlapping search window are warm.  The queue then
 // fills fewer slots than there are SBs: q[TE_QTOTAL] counts the slots that will fill (decremented per
-// kept SB); a ticket at or past it will never fill and its worker leaves.
+// kept SB); a ticket at or past it will never fill and its worker leaves.  Measured SLOWER (240 x 4K x 8
+// frames: 1.64-1.67 s vs 1.54-1.57 s, queue waits of the I frame doubled, P-frame RD time +3 %;
+// profiles/r07/continuation_*.txt): off.
 #ifndef TE_CONT
 #define TE_CONT 0
 #endif
