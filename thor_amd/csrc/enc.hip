@@ -176,7 +176,9 @@ __global__ __launch_bounds__(64) TE_WPE void k_enc_rows(const TeJob *__restrict_
   const int lane = threadIdx.x;
   int cur = -1;  // the job whose frame parameters s_F holds
   unsigned long long t_work = 0, t_wait = 0, n_sb = 0;  // (lane 0) this worker's profile
-  unsigned keep = TE_Q_EMPTY;  // (lane 0, TE_CONT) the SB this worker codes next, without the queue
+#if TE_CONT
+  unsigned keep = TE_Q_EMPTY;  // (lane 0) the SB this worker codes next, without the queue
+#endif
   for (;;) {
     unsigned h = 0;
     const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
@@ -589,22 +591,38 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
                                                   unsigned long long *arena_ctr, int *meta, const unsigned *err) {
   const TeJob &J = jobs[blockIdx.x];
   const int nsb = J.nsbh * J.nsbv;
-  long long *off = scan_tmp + (size_t)blockIdx.x * (nsb + 1);
-  __shared__ long long total;
+  (void)scan_tmp;
+  __shared__ long long total, sbend;
   __shared__ long long aoff;
-  if (threadIdx.x == 0) {
+  __shared__ long long part[256];  // per thread: its SBs' bit count, then their first bit position
+  __shared__ int cpart[256];       // per thread: its CLPF candidates, then the first one's bit index
+  // thread t packs SBs [s0, s1) and CLPF candidates [c0, c1): the offsets from two block scans
+  const int t = threadIdx.x;
+  const int per = (nsb + 255) >> 8, s0 = min(t * per, nsb), s1 = min(s0 + per, nsb);
+  const int nf = J.clpf ? (J.F.W >> 6) * (J.F.H >> 6) : 0;
+  const int perc = (nf + 255) >> 8, c0 = min(t * perc, nf), c1 = min(c0 + perc, nf);
+  {
+    long long mine = 0;
+    for (int i = s0; i < s1; i++) mine += te_sb_bits(J, i);
+    int cm = 0;
+    for (int i = c0; i < c1; i++) cm += J.clpf_bits[i] >= 0;
+    part[t] = mine;
+    cpart[t] = cm;
+  }
+  __syncthreads();
+  if (t == 0) {  // exclusive scans over the 256 partial sums (LDS)
     long long o = J.hdr_bits;
-    for (int i = 0; i < nsb; i++) {
-      off[i] = o;
-      o += te_sb_bits(J, i);
+    int co = 0;
+    for (int i = 0; i < 256; i++) {
+      const long long v = part[i];
+      part[i] = o;
+      o += v;
+      const int c = cpart[i];
+      cpart[i] = co;
+      co += c;
     }
-    off[nsb] = o;
-    if (J.clpf) {
-      o += 2;
-      const int nf = (J.F.W >> 6) * (J.F.H >> 6);
-      for (int i = 0; i < nf; i++) o += J.clpf_bits[i] >= 0;
-    }
-    total = o;
+    sbend = o;
+    total = o + (J.clpf ? 2 + co : 0);
   }
   __syncthreads();
   const long long nw = (total + 31) >> 5;
@@ -619,16 +637,22 @@ __global__ __launch_bounds__(256) void k_enc_pack(const TeJob *__restrict__ jobs
   }
   for (long long i = threadIdx.x; i < nw + 1 && i < out_cap_words; i += 256) J.out_words[i] = 0;
   __syncthreads();
-  if (threadIdx.x == 0) te_or_bits(J.out_words, 0, J.hdr_words, J.hdr_bits);
-  for (int i = threadIdx.x; i < nsb; i += 256)
-    te_or_bits(J.out_words, off[i], J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, te_sb_bits(J, i));
-  if (threadIdx.x == 0 && J.clpf) {
-    long long p = off[nsb];
-    const uint32_t two = 0x80000000u;  // bits 1, 0
-    te_or_bits(J.out_words, p, &two, 2);
-    p += 2;
-    const int nf = (J.F.W >> 6) * (J.F.H >> 6);
-    for (int i = 0; i < nf; i++) {
+  if (t == 0) te_or_bits(J.out_words, 0, J.hdr_words, J.hdr_bits);
+  {
+    long long pos = part[t];
+    for (int i = s0; i < s1; i++) {
+      const int b = te_sb_bits(J, i);
+      te_or_bits(J.out_words, pos, J.sb_words + (size_t)i * THOR_ENC_SB_WORDS, b);
+      pos += b;
+    }
+  }
+  if (J.clpf) {
+    if (t == 0) {
+      const uint32_t two = 0x80000000u;  // bits 1, 0
+      te_or_bits(J.out_words, sbend, &two, 2);
+    }
+    long long p = sbend + 2 + cpart[t];
+    for (int i = c0; i < c1; i++) {
       const int d = J.clpf_bits[i];
       if (d < 0) continue;
       if (d) atomicOr(&J.out_words[p >> 5], 0x80000000u >> (p & 31));
