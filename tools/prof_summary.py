@@ -110,8 +110,10 @@ def main():
         traffic["recon_note"] = ("tools/decode_frames.py k4_low 8: one k_recon launch per frame; per_p_launch = 8 "
                                  "frames, the bench's batched launch (THOR_MAX_BATCH)")
     json.dump(traffic, open(os.path.join(out, "%s_traffic.json" % tag), "w"), indent=1)
-    # the GPU box does not receive profiles/ (.gpurunignore): bench.py reads this copy
-    json.dump(traffic, open(os.path.join(root, "tools", "traffic_latest.json"), "w"), indent=1)
+    # the GPU box does not receive profiles/ (.gpurunignore): bench.py reads tools/traffic_latest.json,
+    # replaced only on request (PROF_LATEST=1), so a summary run cannot swap the bench's figure silently
+    if os.environ.get("PROF_LATEST") == "1":
+        json.dump(traffic, open(os.path.join(root, "tools", "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
 
