@@ -1005,18 +1005,12 @@ def main():
                     def host_leg(j):  # parse + one host image + one copy, native (GIL released)
                         return decs[ks[j]].upload_payload(parsers[j], chunks[j], pools[ks[j]][i])
 
-                    # each decoder group's GPU reconstruction is enqueued as soon as ITS streams are
-                    # parsed and uploaded (the futures finish roughly in submission order), so the
-                    # last frame's decode overlaps the host work of the groups after it
-                    futs = [pool.submit(host_leg, j) for j in range(len(ks))]
-                    ds = [None] * len(ks)
+                    ds = list(pool.map(host_leg, range(len(ks))))
                     for g in gs:
                         if g:
-                            for j in g:
-                                ds[j] = futs[j].result()
                             decode_batch([decs[ks[j]] for j in g], [ds[j] for j in g])
                     for j in range(len(ks)):
-                        devs[j][i] = ds[j] if ds[j] is not None else futs[j].result()
+                        devs[j][i] = ds[j]
                     pipe_tl["dec_enq_ms"][i] = round((time.perf_counter() - t0) * 1e3, 1)
             except BaseException as e:  # re-raised by the caller
                 err.append(e)
