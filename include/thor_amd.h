@@ -425,7 +425,11 @@ long long thor_enc_frame_bytes(const thor_enc_t *e, uint8_t *dst, size_t cap);
  * thor_enc_seq_ready: out[i * nframes + f] = chunk size of that frame if it is
  * final, else -1 (non-blocking); returns how many are final.
  * thor_enc_seq_chunk: the chunk (4-byte big-endian length + payload) of
- * context i's f-th frame, min(size, cap) bytes copied; returns its size.
+ * context i's f-th frame, min(size, cap) bytes copied; returns its size.  Both
+ * read the launch in flight or, after thor_enc_seq_end, the last one ended,
+ * until the next thor_enc_seq_begin on the device (one caller at a time).
+ * THOR_SEQ_CLASSES / THOR_SEQ_CLAIM / THOR_SEQ_PRIO / THOR_SEQ_RETIRE in the
+ * environment select the scheduling variants measured in DESIGN.md §3b.
  * thor_enc_seq_end: waits; on a device error every context returns to its
  * state before the launch (THOR_ERR_HIP, THOR_ERR_NOMEM when a frame outgrew
  * the output buffer or the arena); else each context's last frame is also its
